@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Benchmark: edges-traversed/s of the LCC+NLCC driver loop (BASELINE.json metric).
+
+One "step" = one complete run_pattern_matching_beta pattern search
+(run_pattern_matching_beta.cpp:539-1356: every LCC superstep, every NLC line,
+post-processing and interleaved LCC calls until the loop terminates) over the
+graph already resident in HBM.  Default workload = BASELINE.json configs[1]
+(C2): R-MAT scale 24 from P_gen = 4 generator ranks, degree-log2 labels,
+examples/rmat_log2_tree_pattern, one MI355X.
+
+Edges traversed: adjacency entries scanned by LCC senders
+(full CSR degree in superstep 0 of the first call, |M[v]| later) plus those
+scanned by NLCC/TDS initiators and relays; counted identically by the oracle.
+
+N > 1 GPUs (torch.distributed.run, one process per GPU): every rank runs an
+independent replica of the workload ("replicas", weak scaling) -- see
+DESIGN.md "Multi-GPU" for why and what the sharded design is.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "edges-traversed/sec (LCC+NLCC) on R-MAT + tree pattern, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--p-gen", type=int, default=4)
+    ap.add_argument("--pattern", default="rmat_log2_tree_pattern")
+    ap.add_argument("--max-iterations", type=int, default=64)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_lcc_first.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl")
+
+    import numpy as np
+    import fuzzypatternmatching_amd as pm
+
+    pattern_dir = os.path.join(ROOT, "patterns", args.pattern)
+    t0 = time.time()
+    g = pm.rmat_graph(args.scale, args.p_gen)
+    log(f"[rank {rank}] generated R-MAT S={args.scale} P_gen={args.p_gen}: V={g.n} E={g.nnz} "
+        f"in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    m = pm.PatternMatcher(g, pattern_dir, device=local_rank if world > 1 else 0)
+    log(f"[rank {rank}] uploaded graph in {time.time() - t0:.1f}s")
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        m.run_beta("", args.max_iterations)
+    barrier_sync()
+    t_start = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        stats.append(m.run_beta("", args.max_iterations))
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    edges = sum(s["lcc_edges"] + s["nlcc_edges"] + s["tds_edges"] for s in stats)
+    kern_ms = float(np.mean([s["lcc_first_kernel_ms"] for s in stats]))
+    kern_bytes = stats[-1]["lcc_first_bytes"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        e = torch.tensor([edges], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        edges = int(e.item())
+    s0 = stats[-1]
+    log(f"[rank {rank}] per step: {s0['iterations']} iterations (terminated={s0['terminated']}), "
+        f"lcc {s0['lcc_edges']} nlcc {s0['nlcc_edges']} tds {s0['tds_edges']} edges, walks {s0['walks']}, "
+        f"final |S|={s0['final_vertices']} |M|={s0['final_edges']}, host {s0['seconds'] * 1e3:.3f} ms, "
+        f"device {s0['device_seconds'] * 1e3:.3f} ms, lcc_first kernel {kern_ms:.4f} ms")
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    achieved = kern_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            pmc = json.load(open(args.pmc))
+            if pmc.get("scale") == args.scale and pmc.get("p_gen") == args.p_gen and pmc.get("pattern") == args.pattern:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception as ex:  # noqa: BLE001
+            log(f"pmc file unreadable: {ex}")
+    roofline = {"bound": "hbm", "kernel": "k_lcc_first", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": kern_bytes, "avg_launch_ms": round(kern_ms, 5)}
+
+    cpu = None
+    if args.cpu_baseline == "auto" and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        t0 = time.time()
+        so = oracle.run(g.off, g.col, pattern_dir, None, max_iterations=args.max_iterations)
+        oe = so["lcc_edges"] + so["nlcc_edges"] + so["tds_edges"]
+        cpu = {"value": round(oe / so["seconds"], 1), "unit": "edges/s", "cores": 1, "kind": "port",
+               "sample": f"one full pattern search of the same workload (S={args.scale}, P_gen={args.p_gen}, "
+                         f"{args.pattern}) by oracle/pm_oracle.cpp, single thread, "
+                         f"{so['seconds']:.2f}s timed ({time.time() - t0:.1f}s incl. setup)",
+               "edges": oe}
+        if oe != (s0["lcc_edges"] + s0["nlcc_edges"] + s0["tds_edges"]):
+            log(f"WARNING: oracle edge count {oe} != GPU {s0['lcc_edges'] + s0['nlcc_edges'] + s0['tds_edges']}")
+
+    out = {
+        "metric": METRIC,
+        "value": round(edges / elapsed, 1),
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic R-MAT (generate_rmat.cpp stream, a,b,c,d=.57/.19/.19/.05, scrambled, symmetrized), "
+                "degree-log2 labels",
+        "config": {"workload": f"C2: R-MAT scale-{args.scale} (P_gen={args.p_gen}) + {args.pattern}, "
+                               f"full LCC+NLCC driver loop per step",
+                   "scale": args.scale, "p_gen": args.p_gen, "pattern": args.pattern,
+                   "vertices": g.n, "directed_entries": g.nnz,
+                   "parallelism": "single" if world == 1 else f"replicas{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

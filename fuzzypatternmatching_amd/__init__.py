@@ -1,0 +1,191 @@
+"""MI355X-native label-constrained pattern matching (HavoqGT run_pattern_matching_beta hot path).
+
+Host-side mirror of the reference's driver interface.  The compute runs in
+lib/libpm.so (hand-written HIP kernels for gfx950) behind the C-ABI in
+include/pm_abi.h; this module owns host buffers and forwards calls.
+
+    g = rmat_graph(scale=16, p_gen=4)          # generate_rmat.cpp semantics
+    m = PatternMatcher(g, "patterns/rmat_log2_tree_pattern")
+    stats = m.run_beta("/tmp/results")          # run_pattern_matching_beta.cpp:539-1425
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _abi
+
+__all__ = ["Graph", "rmat_graph", "pattern_summary", "write_graph", "read_graph", "PatternMatcher", "PMError"]
+
+DEFAULT_HUB_THRESHOLD = 1048576  # generate_rmat.cpp:106
+
+
+class PMError(RuntimeError):
+    pass
+
+
+class Graph:
+    """Row-sorted CSR with multiplicity: off[n+1] (u64), col[off[n]] (u32)."""
+
+    def __init__(self, off, col, symmetric=True, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
+        self.off = np.ascontiguousarray(off, dtype=np.uint64)
+        self.col = np.ascontiguousarray(col, dtype=np.uint32)
+        self.n = int(self.off.shape[0] - 1)
+        self.symmetric = bool(symmetric)
+        self.nranks = int(nranks)
+        self.hub_threshold = int(hub_threshold)
+
+    @property
+    def nnz(self):
+        return int(self.off[-1])
+
+    def degrees(self):
+        return np.diff(self.off)
+
+    @staticmethod
+    def from_edges(src, dst, n=None, symmetric=None, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
+        """Directed edge list (with multiplicity) -> row-sorted CSR."""
+        src = np.asarray(src, dtype=np.uint64)
+        dst = np.asarray(dst, dtype=np.uint64)
+        if n is None:
+            n = int(max(src.max(initial=0), dst.max(initial=0)) + 1) if src.size else 0
+        order = np.lexsort((dst, src))
+        src, dst = src[order], dst[order]
+        off = np.zeros(n + 1, dtype=np.uint64)
+        np.add.at(off, src.astype(np.int64) + 1, 1)
+        off = np.cumsum(off).astype(np.uint64)
+        if symmetric is None:
+            fwd = np.stack([src, dst], 1)
+            rev = np.stack([dst, src], 1)
+            a = fwd[np.lexsort((fwd[:, 1], fwd[:, 0]))]
+            b = rev[np.lexsort((rev[:, 1], rev[:, 0]))]
+            symmetric = bool(np.array_equal(a, b))
+        return Graph(off, dst.astype(np.uint32), symmetric, nranks, hub_threshold)
+
+
+def _lib():
+    return _abi.load()
+
+
+def _err(ctx=None):
+    msg = _lib().pm_last_error(ctx)
+    return PMError(msg.decode() if msg else "unknown error")
+
+
+def _take_host_csr(off_p, col_p, n):
+    lib = _lib()
+    off = np.ctypeslib.as_array(ctypes.cast(off_p, ctypes.POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy()
+    nnz = int(off[-1])
+    col = (np.ctypeslib.as_array(ctypes.cast(col_p, ctypes.POINTER(ctypes.c_uint32)), shape=(max(nnz, 1),))[:nnz].copy())
+    lib.pm_free_host(off_p)
+    lib.pm_free_host(col_p)
+    return off, col
+
+
+def rmat_graph(scale, p_gen=1, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """Symmetrized R-MAT graph of generate_rmat.cpp with P_gen generator ranks."""
+    lib = _lib()
+    off_p, col_p, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    if lib.pm_rmat_csr(scale, p_gen, ctypes.byref(off_p), ctypes.byref(col_p), ctypes.byref(n)) != 0:
+        raise _err()
+    off, col = _take_host_csr(off_p, col_p, n.value)
+    return Graph(off, col, True, nranks, hub_threshold)
+
+
+def pattern_summary(pattern_dir):
+    """Parsed pattern directory (graph.hpp / pattern_util.hpp rules) as a dict."""
+    import json
+    buf = ctypes.create_string_buffer(1 << 20)
+    if _lib().pm_pattern_summary(pattern_dir.encode(), buf, len(buf)) != 0:
+        raise _err()
+    return json.loads(buf.value.decode())
+
+
+def write_graph(base, g, nranks=None):
+    nr = g.nranks if nranks is None else nranks
+    rc = _lib().pm_write_graph(base.encode(), g.n, g.off.ctypes.data, g.col.ctypes.data, int(g.symmetric), nr,
+                               g.hub_threshold)
+    if rc != 0:
+        raise _err()
+
+
+def read_graph(base):
+    lib = _lib()
+    off_p, col_p, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    sym, nr, hub = ctypes.c_int(), ctypes.c_uint32(), ctypes.c_uint64()
+    if lib.pm_read_graph(base.encode(), ctypes.byref(off_p), ctypes.byref(col_p), ctypes.byref(n), ctypes.byref(sym),
+                         ctypes.byref(nr), ctypes.byref(hub)) != 0:
+        raise _err()
+    off, col = _take_host_csr(off_p, col_p, n.value)
+    return Graph(off, col, bool(sym.value), nr.value, hub.value)
+
+
+class PatternMatcher:
+    """One device context: graph resident in HBM + one pattern directory."""
+
+    def __init__(self, graph, pattern_dir, device=0, labels=None):
+        self.graph = graph
+        self._desc = _abi.GraphDesc(graph.n, graph.off.ctypes.data, graph.col.ctypes.data, int(graph.symmetric),
+                                    graph.nranks, graph.hub_threshold)
+        self._ctx = _lib().pm_create(ctypes.byref(self._desc), pattern_dir.encode(), device)
+        if not self._ctx:
+            raise _err()
+        if labels is not None:
+            self.set_labels(labels)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            _lib().pm_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise _err(self._ctx)
+
+    def set_labels(self, labels):
+        lab = np.ascontiguousarray(labels, dtype=np.uint64)
+        if lab.shape[0] != self.graph.n:
+            raise ValueError("labels must have one entry per vertex id")
+        self._check(_lib().pm_vertex_data_set(self._ctx, lab.ctypes.data))
+
+    def degree_labels(self):
+        self._check(_lib().pm_vertex_data_degree(self._ctx))
+
+    def reset(self):
+        self._check(_lib().pm_reset(self._ctx))
+
+    def lcc_bsp(self, init_step, itr=0):
+        st = _abi.LccStats()
+        self._check(_lib().pm_lcc_bsp(self._ctx, int(init_step), itr, ctypes.byref(st)))
+        return {f[0]: getattr(st, f[0]) for f in st._fields_ if f[0] != "reserved"}
+
+    def token_passing(self, pl):
+        st = _abi.TpStats()
+        self._check(_lib().pm_token_passing(self._ctx, pl, ctypes.byref(st)))
+        return {f[0]: getattr(st, f[0]) for f in st._fields_}
+
+    def post_token_passing(self, pl):
+        d = ctypes.c_uint32()
+        self._check(_lib().pm_post_token_passing(self._ctx, pl, ctypes.byref(d)))
+        return bool(d.value)
+
+    def run_beta(self, result_dir="", max_iterations=0):
+        st = _abi.RunStats()
+        if result_dir:
+            os.makedirs(result_dir, exist_ok=True)
+        self._check(_lib().pm_run_beta(self._ctx, result_dir.encode(), max_iterations, ctypes.byref(st)))
+        return st.as_dict()
+
+    def export_state(self):
+        """Returns (tpub[n] u16, mdeg[n] u32, nbrs u32) of the current state map."""
+        n = self.graph.n
+        tpub = np.zeros(n, np.uint16)
+        mdeg = np.zeros(n, np.uint32)
+        ne = ctypes.c_uint64()
+        self._check(_lib().pm_export_state(self._ctx, tpub.ctypes.data, mdeg.ctypes.data, None, ctypes.byref(ne)))
+        nbrs = np.zeros(max(ne.value, 1), np.uint32)
+        self._check(_lib().pm_export_state(self._ctx, None, None, nbrs.ctypes.data, ctypes.byref(ne)))
+        return tpub, mdeg, nbrs[: ne.value]

@@ -1,0 +1,113 @@
+"""ctypes binding of the C-ABI declared in include/pm_abi.h.
+
+The shared library lib/libpm.so (HIP kernels for gfx950 + host driver) is the
+product; this module only declares signatures.  It fails loudly when the
+library is missing: there is no Python or CPU fallback for the hot path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpm.so")
+
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_i32 = ctypes.c_int32
+c_vp = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+
+
+class GraphDesc(ctypes.Structure):
+    _fields_ = [
+        ("n", c_u64),
+        ("off", c_vp),
+        ("col", c_vp),
+        ("symmetric", c_i32),
+        ("nranks", c_u32),
+        ("hub_threshold", c_u64),
+    ]
+
+
+class LccStats(ctypes.Structure):
+    _fields_ = [
+        ("supersteps", c_u64),
+        ("edges_traversed", c_u64),
+        ("active_vertices", c_u64),
+        ("active_edges", c_u64),
+        ("not_finished", c_u32),
+        ("reserved", c_u32),
+    ]
+
+
+class TpStats(ctypes.Structure):
+    _fields_ = [
+        ("sources", c_u64),
+        ("acked_sources", c_u64),
+        ("edges_traversed", c_u64),
+        ("tokens", c_u64),
+        ("walks", c_u64),
+    ]
+
+
+class RunStats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", c_u64),
+        ("terminated", c_u32),
+        ("reserved", c_u32),
+        ("lcc_edges", c_u64),
+        ("nlcc_edges", c_u64),
+        ("tds_edges", c_u64),
+        ("walks", c_u64),
+        ("final_vertices", c_u64),
+        ("final_edges", c_u64),
+        ("seconds", ctypes.c_double),
+        ("device_seconds", ctypes.c_double),
+        ("lcc_first_kernel_ms", ctypes.c_double),
+        ("lcc_first_bytes", c_u64),
+    ]
+
+    def as_dict(self):
+        return {f[0]: getattr(self, f[0]) for f in self._fields_ if f[0] != "reserved"}
+
+
+# (name, restype, argtypes) -- every symbol include/pm_abi.h declares.
+SIGNATURES = [
+    ("pm_create", c_vp, [ctypes.POINTER(GraphDesc), c_char_p, ctypes.c_int]),
+    ("pm_destroy", None, [c_vp]),
+    ("pm_last_error", c_char_p, [c_vp]),
+    ("pm_vertex_data_degree", ctypes.c_int, [c_vp]),
+    ("pm_vertex_data_set", ctypes.c_int, [c_vp, c_vp]),
+    ("pm_reset", ctypes.c_int, [c_vp]),
+    ("pm_lcc_bsp", ctypes.c_int, [c_vp, ctypes.c_int, c_u64, ctypes.POINTER(LccStats)]),
+    ("pm_token_passing", ctypes.c_int, [c_vp, c_u32, ctypes.POINTER(TpStats)]),
+    ("pm_post_token_passing", ctypes.c_int, [c_vp, c_u32, ctypes.POINTER(c_u32)]),
+    ("pm_run_beta", ctypes.c_int, [c_vp, c_char_p, c_u64, ctypes.POINTER(RunStats)]),
+    ("pm_export_state", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_u64)]),
+    ("pm_rmat_csr", ctypes.c_int, [c_u64, c_u64, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_u64)]),
+    ("pm_free_host", None, [c_vp]),
+    ("pm_write_graph", ctypes.c_int, [c_char_p, c_u64, c_vp, c_vp, ctypes.c_int, c_u32, c_u64]),
+    ("pm_read_graph", ctypes.c_int, [c_char_p, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_u64),
+                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_u32), ctypes.POINTER(c_u64)]),
+    ("pm_pattern_summary", ctypes.c_int, [c_char_p, c_char_p, c_u64]),
+    ("pm_build_arch", c_char_p, []),
+]
+
+_lib = None
+
+
+def load():
+    """Loads lib/libpm.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP path has no fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,698 @@
+// C-ABI (include/pm_abi.h) and host driver of the MI355X pattern-matching path.
+//
+// pm_run_beta restates the driver loop of src/run_pattern_matching_beta.cpp
+// (:539-1425) on top of the device kernels in pm_kernels.hip and writes the
+// same result directory layout.
+
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <bitset>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pm_abi.h"
+#include "host/graph_store.hpp"
+#include "pm_internal.hpp"
+
+struct pm_ctx : public pm::Ctx {};
+
+namespace pm {
+
+static std::string g_last_error;
+
+static void mkdir_p(const std::string& path) {
+  std::string cur;
+  for (size_t i = 0; i < path.size(); ++i) {
+    cur += path[i];
+    if (path[i] == '/' && cur.size() > 1) ::mkdir(cur.c_str(), 0755);
+  }
+  ::mkdir(path.c_str(), 0755);
+}
+
+static std::string fmt_double(double x) {
+  std::ostringstream o;
+  o << x;
+  return o.str();
+}
+
+template <typename T>
+static T* dalloc(uint64_t n) {
+  T* p = nullptr;
+  PM_HIP_CHECK(hipMalloc(&p, std::max<uint64_t>(1, n) * sizeof(T)));
+  return p;
+}
+
+static void require_gfx950(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= device)
+    throw std::runtime_error("no HIP device " + std::to_string(device) + " available (the HIP path has no CPU fallback)");
+  hipDeviceProp_t prop;
+  PM_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    throw std::runtime_error(std::string("device arch ") + prop.gcnArchName + " is not gfx950 (MI355X)");
+}
+
+static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int device) {
+  if (!g || !g->off || !g->col) throw std::runtime_error("pm_create: null graph");
+  require_gfx950(device);
+  auto c = std::make_unique<pm_ctx>();
+  c->device = device;
+  PM_HIP_CHECK(hipSetDevice(device));
+  PM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->n = g->n;
+  c->nnz = g->off[g->n];
+  c->symmetric = g->symmetric != 0;
+  c->nranks = g->nranks ? g->nranks : 1;
+  c->hub_threshold = g->hub_threshold;
+  if (!c->symmetric)
+    throw std::runtime_error("directed (non-symmetric) input graphs are not supported by the GPU path yet");
+  if (c->n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 vertices");
+  c->pattern = load_pattern_dir(pattern_dir);
+  const PatternGraph& pg = c->pattern.graph;
+  if (pg.diameter == 0) throw std::runtime_error("pattern_stat: diameter is 0 or missing");
+  for (int t = 0; t < kMaxTemplateVertices; ++t) c->pa.adj[t] = pg.adj[t];
+  c->pa.K = static_cast<int32_t>(pg.vertex_data.size());
+  for (int t = 0; t < c->pa.K; ++t) c->pa.plabel[t] = pg.vertex_data[t];
+  for (const auto& l : c->pattern.lines)
+    if (l.selected_vertices) throw std::runtime_error("pattern_nlc selected_vertices=1 is not supported yet");
+  for (uint64_t v = 0; v < c->n; ++v)
+    if (g->off[v + 1] - g->off[v] >= c->hub_threshold) c->hubs_host.push_back(v);
+  // device graph + state
+  c->d_off = dalloc<uint64_t>(c->n + 1);
+  c->d_col = dalloc<uint32_t>(c->nnz);
+  PM_HIP_CHECK(hipMemcpy(c->d_off, g->off, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMemcpy(c->d_col, g->col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (!c->hubs_host.empty()) {
+    c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
+    PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  }
+  c->d_labels = dalloc<uint64_t>(c->n);
+  c->d_tl = dalloc<uint16_t>(c->n);
+  c->d_tpub[0] = dalloc<uint16_t>(c->n);
+  c->d_tpub[1] = dalloc<uint16_t>(c->n);
+  c->d_tst = dalloc<uint16_t>(c->n);
+  c->d_mcol = dalloc<uint32_t>(c->nnz);
+  c->d_mst = dalloc<uint8_t>(c->nnz);
+  c->d_mlen = dalloc<uint32_t>(c->n);
+  c->d_malive = dalloc<uint32_t>(c->n);
+  c->d_slist = dalloc<uint32_t>(c->n);
+  c->d_sources = dalloc<uint32_t>(c->n);
+  c->d_nS = dalloc<uint32_t>(1);
+  c->d_flags = dalloc<uint32_t>(4);
+  c->d_tsm = dalloc<uint8_t>(c->n);
+  size_t free_b = 0, total_b = 0;
+  PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+  size_t arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
+  arena = std::max<size_t>(arena, size_t(64) << 20);
+  c->arena.base = dalloc<char>(arena);
+  c->arena.cap = arena;
+  // default labels = degree labels
+  launch_degree_labels(*c);
+  c->labels_host.assign(c->n, 0);
+  for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(g->off[v + 1] - g->off[v]);
+  PM_HIP_CHECK(hipStreamSynchronize(c->stream));
+  return c.release();
+}
+
+static void destroy_ctx(pm_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  void* ptrs[] = {c->d_off, c->d_col, c->d_labels, c->d_hubs, c->d_tl, c->d_tpub[0], c->d_tpub[1], c->d_tst,
+                  c->d_mcol, c->d_mst, c->d_mlen, c->d_malive, c->d_slist, c->d_sources, c->d_nS, c->d_flags,
+                  c->d_tsm, c->d_counts, c->arena.base};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static void reset_state(Ctx& c) {
+  PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[0], 0, c.n * sizeof(uint16_t), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[1], 0, c.n * sizeof(uint16_t), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_tsm, 0, c.n, c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_flags, 0, 4 * sizeof(uint32_t), c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.cur = 0;
+  c.nS_host = 0;
+  c.lcc_started = false;
+  c.nsources = 0;
+}
+
+// Per-superstep outputs of one LCC call.
+struct LccOut {
+  std::vector<std::vector<uint64_t>> vcount, ecount;  // [superstep][rank]
+  std::vector<uint64_t> trav;
+  std::vector<double> seconds;
+  bool not_finished = false;
+  uint64_t matching_rows = 0;  // vertices with a label match (superstep 0 of the first call)
+};
+
+static void ensure_counts(Ctx& c, size_t slots) {
+  if (c.counts_slots >= slots) return;
+  if (c.d_counts) (void)hipFree(c.d_counts);
+  c.d_counts = dalloc<uint64_t>(slots * (2 * c.nranks + 2));
+  c.counts_slots = slots;
+}
+
+// label_propagation_pattern_matching_bsp (nonunique_ee.hpp:1033-1153).
+static LccOut lcc_call(Ctx& c, bool init_step) {
+  const uint64_t D = c.pattern.graph.diameter;
+  const uint64_t slot_words = 2 * c.nranks + 2;
+  ensure_counts(c, D);
+  PM_HIP_CHECK(hipMemsetAsync(c.d_counts, 0, D * slot_words * sizeof(uint64_t), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_flags, 0, 2 * sizeof(uint32_t), c.stream));
+  std::vector<hipEvent_t> ev(D + 1);
+  for (auto& e : ev) PM_HIP_CHECK(hipEventCreate(&e));
+  PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
+  hipEvent_t k_beg = nullptr, k_end = nullptr;
+  for (uint64_t ss = 0; ss < D; ++ss) {
+    uint64_t* slot = c.d_counts + ss * slot_words;
+    uint64_t* trav = slot + 2 * c.nranks;
+    if (ss == 0 && init_step) {
+      if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
+      launch_label_match(c);
+      PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
+      PM_HIP_CHECK(hipEventCreate(&k_beg));
+      PM_HIP_CHECK(hipEventCreate(&k_end));
+      PM_HIP_CHECK(hipEventRecord(k_beg, c.stream));
+      launch_lcc_first(c, slot, trav);
+      PM_HIP_CHECK(hipEventRecord(k_end, c.stream));
+      PM_HIP_CHECK(hipMemcpyAsync(&c.nS_host, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+      PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+      c.lcc_started = true;
+    } else {
+      if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
+      launch_lcc_step(c, slot, trav);
+    }
+    PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
+  }
+  std::vector<uint64_t> host(D * slot_words);
+  uint32_t flags[2] = {0, 0};
+  PM_HIP_CHECK(hipMemcpyAsync(host.data(), c.d_counts, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(flags, c.d_flags, sizeof(flags), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  LccOut out;
+  for (uint64_t ss = 0; ss < D; ++ss) {
+    std::vector<uint64_t> vc(c.nranks), ec(c.nranks);
+    for (uint32_t r = 0; r < c.nranks; ++r) {
+      vc[r] = host[ss * slot_words + 2 * r];
+      ec[r] = host[ss * slot_words + 2 * r + 1];
+    }
+    out.vcount.push_back(vc);
+    out.ecount.push_back(ec);
+    out.trav.push_back(host[ss * slot_words + 2 * c.nranks]);
+    if (ss == 0 && init_step) out.matching_rows = host[ss * slot_words + 2 * c.nranks + 1];
+    float ms = 0.f;
+    PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[ss], ev[ss + 1]));
+    out.seconds.push_back(ms * 1e-3);
+    c.device_seconds += ms * 1e-3;
+  }
+  if (k_beg) {
+    float ms = 0.f;
+    PM_HIP_CHECK(hipEventElapsedTime(&ms, k_beg, k_end));
+    c.lcc_first_ms = ms;
+    (void)hipEventDestroy(k_beg);
+    (void)hipEventDestroy(k_end);
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  out.not_finished = flags[0] != 0;
+  if (flags[1])
+    throw std::runtime_error(
+        "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message); "
+        "the push-form LCC kernel needed for this case is not implemented yet");
+  return out;
+}
+
+// Algorithmic bytes of the fused superstep-0 kernel (roofline):
+// every vertex: Tl (2 B) ; matching rows: 2 offsets (16 B) + per entry 4 B id
+// + 2 B Tl gather + 1 B edge state ; survivors: T_state/T_pub/mlen/malive/slist (16 B)
+// + 4 B per distinct contributing neighbour written.
+static uint64_t lcc_first_bytes(const Ctx& c, uint64_t scanned, uint64_t survivors, uint64_t edges,
+                                uint64_t matching_rows) {
+  return c.n * 2 + matching_rows * 16 + scanned * (4 + 2) + survivors * 16 + edges * (4 + 1);
+}
+
+struct DriverFiles {
+  std::vector<std::string> superstep, step, iteration;
+  std::vector<std::vector<std::string>> vcount, ecount, mcount;  // per rank
+};
+
+static void add_count_lines(Ctx& c, DriverFiles& f, uint64_t itr, const char* tag, uint64_t idx,
+                            const std::vector<uint64_t>& vc, const std::vector<uint64_t>& ec, uint64_t msgs) {
+  for (uint32_t r = 0; r < c.nranks; ++r) {
+    const std::string pre = std::to_string(itr) + ", " + tag + ", " + std::to_string(idx) + ", ";
+    f.vcount[r].push_back(pre + std::to_string(vc[r]));
+    f.ecount[r].push_back(pre + std::to_string(ec[r]));
+    f.mcount[r].push_back(pre + std::to_string(r == 0 ? msgs : 0));
+  }
+}
+
+static void count_state(Ctx& c, std::vector<uint64_t>& vc, std::vector<uint64_t>& ec) {
+  ensure_counts(c, 1);
+  PM_HIP_CHECK(hipMemsetAsync(c.d_counts, 0, (2 * c.nranks + 2) * sizeof(uint64_t), c.stream));
+  if (c.nS_host) launch_count_state(c, c.d_counts);
+  std::vector<uint64_t> host(2 * c.nranks);
+  PM_HIP_CHECK(hipMemcpyAsync(host.data(), c.d_counts, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  vc.assign(c.nranks, 0);
+  ec.assign(c.nranks, 0);
+  for (uint32_t r = 0; r < c.nranks; ++r) {
+    vc[r] = host[2 * r];
+    ec[r] = host[2 * r + 1];
+  }
+}
+
+static uint32_t owner_host(const Ctx& c, uint64_t v) {
+  if (c.nranks <= 1) return 0;
+  if (!c.hubs_host.empty()) {
+    auto it = std::lower_bound(c.hubs_host.begin(), c.hubs_host.end(), v);
+    if (it != c.hubs_host.end() && *it == v) return static_cast<uint32_t>((it - c.hubs_host.begin()) % c.nranks);
+  }
+  return static_cast<uint32_t>(v % c.nranks);
+}
+
+static void export_state(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32_t>& mdeg,
+                         std::vector<uint32_t>& nbrs) {
+  tpub.resize(c.n);
+  PM_HIP_CHECK(hipMemcpy(tpub.data(), c.d_tpub[c.cur], c.n * sizeof(uint16_t), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> mlen(c.n), malive(c.n);
+  PM_HIP_CHECK(hipMemcpy(mlen.data(), c.d_mlen, c.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(malive.data(), c.d_malive, c.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<uint64_t> off(c.n + 1);
+  PM_HIP_CHECK(hipMemcpy(off.data(), c.d_off, (c.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  mdeg.assign(c.n, 0);
+  nbrs.clear();
+  std::vector<uint32_t> rowc;
+  std::vector<uint8_t> rows;
+  for (uint64_t v = 0; v < c.n; ++v) {
+    if (!tpub[v]) continue;
+    mdeg[v] = malive[v];
+    const uint32_t L = mlen[v];
+    if (!L) continue;
+    rowc.resize(L);
+    rows.resize(L);
+    PM_HIP_CHECK(hipMemcpy(rowc.data(), c.d_mcol + off[v], L * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    PM_HIP_CHECK(hipMemcpy(rows.data(), c.d_mst + off[v], L, hipMemcpyDeviceToHost));
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < L; ++i)
+      if (rows[i] & 1u) {
+        nbrs.push_back(rowc[i]);
+        ++k;
+      }
+    if (k != malive[v]) throw std::runtime_error("internal: alive count mismatch in export");
+  }
+}
+
+static void write_lines(const std::string& path, const std::vector<std::string>& lines) {
+  std::ofstream f(path, std::ofstream::out);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  for (const auto& l : lines) f << l << "\n";
+}
+
+// run_pattern_matching_beta.cpp:539-1425
+static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations, pm_run_stats* st) {
+  const Pattern& P = c.pattern;
+  const bool files = !out_dir.empty();
+  reset_state(c);
+  DriverFiles f;
+  f.vcount.assign(c.nranks, {});
+  f.ecount.assign(c.nranks, {});
+  f.mcount.assign(c.nranks, {});
+  std::vector<std::vector<std::vector<std::string>>> subgraphs(P.lines.size(),
+                                                               std::vector<std::vector<std::string>>(c.nranks));
+  pm_run_stats s{};
+  c.device_seconds = 0.0;
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  const auto t_pattern = std::chrono::steady_clock::now();
+  auto since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+  };
+  bool init_step = true, nf = false, terminated = true;
+  uint64_t itr = 0;
+  uint64_t first_scanned = 0, first_surv = 0, first_edges = 0, first_matching = 0;
+  uint64_t last_v = 0, last_e = 0;
+  auto totals = [&](const std::vector<uint64_t>& vc, const std::vector<uint64_t>& ec) {
+    last_v = 0;
+    last_e = 0;
+    for (auto x : vc) last_v += x;
+    for (auto x : ec) last_e += x;
+  };
+  auto record_lcc = [&](const LccOut& lo, uint64_t itr_) {
+    for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
+      f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
+      add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
+      s.lcc_edges += lo.trav[ss];
+      totals(lo.vcount[ss], lo.ecount[ss]);
+    }
+  };
+  do {
+    if (max_iterations && itr >= max_iterations) {
+      terminated = false;
+      break;
+    }
+    nf = false;
+    const auto t_itr = std::chrono::steady_clock::now();
+    const auto t_lp = std::chrono::steady_clock::now();
+    const bool was_init = init_step;
+    LccOut lo = lcc_call(c, init_step);
+    if (was_init) {
+      first_scanned = lo.trav[0];
+      first_matching = lo.matching_rows;
+      for (auto x : lo.vcount[0]) first_surv += x;
+      for (auto x : lo.ecount[0]) first_edges += x;
+    }
+    record_lcc(lo, itr);
+    nf = nf || lo.not_finished;
+    f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lp)));
+    init_step = false;
+    if (itr == 0) nf = true;  // forced token passing (beta.cpp:686-688)
+    if (nf) {
+      nf = false;
+      for (size_t pl = 0; pl < P.lines.size(); ++pl) {
+        const NlcLine& line = P.lines[pl];
+        for (auto& r : subgraphs[pl]) r.clear();  // reopened with truncation (beta.cpp:713-717)
+        const auto t_tp = std::chrono::steady_clock::now();
+        TpResult tr;
+        if (pl >= 4) {  // beta.cpp:762-767
+          std::vector<uint32_t> walks;
+          uint32_t stride = 0;
+          tr = run_tds_line(c, line, walks, stride);
+          s.tds_edges += tr.edges;
+          s.walks = tr.walks;
+          for (uint64_t i = 0; i < tr.walks; ++i) {
+            const uint32_t* w = walks.data() + i * stride;
+            const uint32_t last = w[stride - 1];
+            const uint32_t r = owner_host(c, last);
+            std::string l = "[" + std::to_string(r) + "], ";
+            for (uint32_t p = 0; p < stride; ++p) l += std::to_string(w[p]) + ", ";
+            l += "[" + std::to_string(last) + "]";
+            subgraphs[pl][r].push_back(std::move(l));
+          }
+        } else {
+          tr = run_path_line(c, line);
+          s.nlcc_edges += tr.edges;
+        }
+        const uint32_t deleted = launch_post_tp(c, line);
+        if (deleted) nf = true;
+        f.superstep.push_back(std::to_string(itr) + ", TP, " + std::to_string(pl) + ", " + fmt_double(since(t_tp)));
+        std::vector<uint64_t> vc, ec;
+        count_state(c, vc, ec);
+        add_count_lines(c, f, itr, "TP", pl, vc, ec, tr.edges);
+        totals(vc, ec);
+        if (deleted && line.interleave_lp) {  // beta.cpp:1163-1197
+          const auto t_lpi = std::chrono::steady_clock::now();
+          LccOut li = lcc_call(c, false);
+          record_lcc(li, itr);
+          nf = nf || li.not_finished;
+          f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lpi)));
+        }
+      }
+    } else {
+      nf = false;
+    }
+    f.iteration.push_back(std::to_string(itr) + ", " + fmt_double(since(t_itr)));
+    ++itr;
+  } while (nf);
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  const double secs = since(t_pattern);
+  s.iterations = itr;
+  s.terminated = terminated ? 1 : 0;
+  s.seconds = secs;
+  s.device_seconds = c.device_seconds;
+  s.lcc_first_kernel_ms = c.lcc_first_ms;
+  c.lcc_first_bytes = lcc_first_bytes(c, first_scanned, first_surv, first_edges, first_matching);
+  s.lcc_first_bytes = c.lcc_first_bytes;
+  s.final_vertices = last_v;
+  s.final_edges = last_e;
+  if (files) {
+    // result dump (beta.cpp:1370-1425) -- after pattern_time_end, as in the reference
+    std::vector<uint16_t> tpub;
+    std::vector<uint32_t> mdeg, nbrs;
+    export_state(c, tpub, mdeg, nbrs);
+    const std::string d = out_dir + "/0";
+    const char* subdirs[] = {"all_ranks_active_vertices_count", "all_ranks_active_edges_count", "all_ranks_messages",
+                             "all_ranks_active_vertices", "all_ranks_active_edges", "all_ranks_subgraphs",
+                             "all_ranks_vertex_data"};
+    for (auto sd : subdirs) mkdir_p(d + "/" + sd);
+    write_lines(out_dir + "/result_pattern_set",
+                {"0, " + std::to_string(c.nranks) + ", " + std::to_string(itr) + ", " + fmt_double(secs) + ", " +
+                 std::to_string(P.graph.edge_count) + ", " + std::to_string(P.graph.vertex_count) + ", " +
+                 std::to_string(P.lines.size())});
+    write_lines(d + "/result_iteration", f.iteration);
+    write_lines(d + "/result_step", f.step);
+    write_lines(d + "/result_superstep", f.superstep);
+    std::vector<std::vector<std::string>> av(c.nranks), ae(c.nranks);
+    uint64_t pos = 0;
+    for (uint64_t v = 0; v < c.n; ++v) {
+      if (!tpub[v]) continue;
+      const uint32_t r = owner_host(c, v);
+      av[r].push_back(std::to_string(r) + ", " + std::to_string(v) + ", 0, " + std::to_string(c.labels_host[v]) + ", " +
+                      std::bitset<16>(tpub[v]).to_string());
+      for (uint32_t k = 0; k < mdeg[v]; ++k)
+        ae[r].push_back(std::to_string(r) + ", " + std::to_string(v) + ", " + std::to_string(nbrs[pos + k]));
+      pos += mdeg[v];
+    }
+    for (uint32_t r = 0; r < c.nranks; ++r) {
+      const std::string rs = std::to_string(r);
+      write_lines(d + "/all_ranks_active_vertices_count/active_vertices_" + rs, f.vcount[r]);
+      write_lines(d + "/all_ranks_active_edges_count/active_edges_" + rs, f.ecount[r]);
+      write_lines(d + "/all_ranks_messages/messages_" + rs, f.mcount[r]);
+      write_lines(d + "/all_ranks_active_vertices/active_vertices_" + rs, av[r]);
+      write_lines(d + "/all_ranks_active_edges/active_edges_" + rs, ae[r]);
+      for (size_t pl = 0; pl < P.lines.size(); ++pl)
+        write_lines(d + "/all_ranks_subgraphs/subgraphs_" + std::to_string(pl) + "_" + rs, subgraphs[pl][r]);
+    }
+  }
+  if (st) *st = s;
+}
+
+}  // namespace pm
+
+
+extern "C" {
+
+pm_ctx* pm_create(const pm_graph_desc* graph, const char* pattern_dir, int device) {
+  try {
+    return pm::create_ctx(graph, pattern_dir, device);
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+void pm_destroy(pm_ctx* ctx) { pm::destroy_ctx(ctx); }
+
+const char* pm_last_error(const pm_ctx* ctx) {
+  if (ctx && !ctx->err.empty()) return ctx->err.c_str();
+  return pm::g_last_error.c_str();
+}
+
+#define PM_API_BODY(ctx, ...)             \
+  do {                                    \
+    if (!(ctx)) return -1;                \
+    try {                                 \
+      (void)hipSetDevice((ctx)->device);  \
+      __VA_ARGS__;                        \
+      return 0;                           \
+    } catch (const std::exception& e) {   \
+      (ctx)->err = e.what();              \
+      pm::g_last_error = e.what();        \
+      return -1;                          \
+    }                                     \
+  } while (0)
+
+int pm_vertex_data_degree(pm_ctx* ctx) {
+  PM_API_BODY(ctx, {
+    pm::launch_degree_labels(*ctx);
+    std::vector<uint64_t> off(ctx->n + 1);
+    PM_HIP_CHECK(hipMemcpy(off.data(), ctx->d_off, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint64_t v = 0; v < ctx->n; ++v) ctx->labels_host[v] = pm::degree_label(off[v + 1] - off[v]);
+    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int pm_vertex_data_set(pm_ctx* ctx, const uint64_t* labels) {
+  PM_API_BODY(ctx, {
+    if (!labels) throw std::runtime_error("null labels");
+    ctx->labels_host.assign(labels, labels + ctx->n);
+    PM_HIP_CHECK(hipMemcpy(ctx->d_labels, labels, ctx->n * sizeof(uint64_t), hipMemcpyHostToDevice));
+  });
+}
+
+int pm_reset(pm_ctx* ctx) {
+  PM_API_BODY(ctx, {
+    pm::reset_state(*ctx);
+    pm::launch_label_match(*ctx);
+    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int pm_lcc_bsp(pm_ctx* ctx, int init_step, uint64_t itr, pm_lcc_stats* out) {
+  (void)itr;
+  PM_API_BODY(ctx, {
+    pm::LccOut lo = pm::lcc_call(*ctx, init_step != 0);
+    if (out) {
+      *out = pm_lcc_stats{};
+      out->supersteps = lo.seconds.size();
+      for (auto t : lo.trav) out->edges_traversed += t;
+      for (auto x : lo.vcount.back()) out->active_vertices += x;
+      for (auto x : lo.ecount.back()) out->active_edges += x;
+      out->not_finished = lo.not_finished ? 1 : 0;
+    }
+  });
+}
+
+int pm_token_passing(pm_ctx* ctx, uint32_t pl, pm_tp_stats* out) {
+  PM_API_BODY(ctx, {
+    if (pl >= ctx->pattern.lines.size()) throw std::runtime_error("NLC line index out of range");
+    const auto& line = ctx->pattern.lines[pl];
+    pm::TpResult r;
+    if (pl >= 4) {
+      std::vector<uint32_t> walks;
+      uint32_t stride = 0;
+      r = pm::run_tds_line(*ctx, line, walks, stride);
+    } else {
+      r = pm::run_path_line(*ctx, line);
+    }
+    if (out) {
+      out->sources = r.sources;
+      out->acked_sources = 0;
+      out->edges_traversed = r.edges;
+      out->tokens = r.tokens;
+      out->walks = r.walks;
+    }
+  });
+}
+
+int pm_post_token_passing(pm_ctx* ctx, uint32_t pl, uint32_t* deleted) {
+  PM_API_BODY(ctx, {
+    if (pl >= ctx->pattern.lines.size()) throw std::runtime_error("NLC line index out of range");
+    const uint32_t d = pm::launch_post_tp(*ctx, ctx->pattern.lines[pl]);
+    if (deleted) *deleted = d;
+  });
+}
+
+int pm_run_beta(pm_ctx* ctx, const char* result_dir, uint64_t max_iterations, pm_run_stats* out) {
+  PM_API_BODY(ctx, { pm::run_beta(*ctx, result_dir ? result_dir : "", max_iterations, out); });
+}
+
+int pm_export_state(pm_ctx* ctx, uint16_t* tpub, uint32_t* mdeg, uint32_t* nbrs, uint64_t* n_edges) {
+  PM_API_BODY(ctx, {
+    std::vector<uint16_t> t;
+    std::vector<uint32_t> d, nb;
+    pm::export_state(*ctx, t, d, nb);
+    if (tpub) std::copy(t.begin(), t.end(), tpub);
+    if (mdeg) std::copy(d.begin(), d.end(), mdeg);
+    if (nbrs) std::copy(nb.begin(), nb.end(), nbrs);
+    if (n_edges) *n_edges = nb.size();
+  });
+}
+
+int pm_rmat_csr(uint64_t scale, uint64_t p_gen, uint64_t** off, uint32_t** col, uint64_t* n) {
+  try {
+    pm::Csr g = pm::build_rmat_csr(scale, p_gen);
+    *n = g.n;
+    *off = static_cast<uint64_t*>(std::malloc(g.off.size() * sizeof(uint64_t)));
+    *col = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, g.col.size()) * sizeof(uint32_t)));
+    std::memcpy(*off, g.off.data(), g.off.size() * sizeof(uint64_t));
+    std::memcpy(*col, g.col.data(), g.col.size() * sizeof(uint32_t));
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+void pm_free_host(void* p) { std::free(p); }
+
+int pm_write_graph(const char* base, uint64_t n, const uint64_t* off, const uint32_t* col, int symmetric,
+                   uint32_t nranks, uint64_t hub_threshold) {
+  try {
+    pm::Csr g;
+    g.n = n;
+    g.off.assign(off, off + n + 1);
+    g.col.assign(col, col + off[n]);
+    g.symmetric = symmetric != 0;
+    pm::write_graph_files(base, g, nranks, hub_threshold);
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n, int* symmetric, uint32_t* nranks,
+                  uint64_t* hub_threshold) {
+  try {
+    uint32_t p = 1;
+    uint64_t h = 0;
+    pm::Csr g = pm::read_graph_files(base, &p, &h);
+    *n = g.n;
+    *off = static_cast<uint64_t*>(std::malloc(g.off.size() * sizeof(uint64_t)));
+    *col = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, g.col.size()) * sizeof(uint32_t)));
+    std::memcpy(*off, g.off.data(), g.off.size() * sizeof(uint64_t));
+    std::memcpy(*col, g.col.data(), g.col.size() * sizeof(uint32_t));
+    if (symmetric) *symmetric = g.symmetric ? 1 : 0;
+    if (nranks) *nranks = p;
+    if (hub_threshold) *hub_threshold = h;
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+const char* pm_build_arch(void) { return "gfx950"; }
+
+int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen) {
+  try {
+    const pm::Pattern p = pm::load_pattern_dir(pattern_dir);
+    std::ostringstream o;
+    auto vec = [&o](const std::vector<uint64_t>& v) {
+      o << "[";
+      for (size_t i = 0; i < v.size(); ++i) o << (i ? "," : "") << v[i];
+      o << "]";
+    };
+    o << "{\"vertex_count\":" << p.graph.vertex_count << ",\"edge_count\":" << p.graph.edge_count
+      << ",\"diameter\":" << p.graph.diameter << ",\"vertices\":";
+    vec(p.graph.vertices);
+    o << ",\"edges\":";
+    vec(p.graph.edges);
+    o << ",\"vertex_data\":";
+    vec(p.graph.vertex_data);
+    o << ",\"adj\":[";
+    for (size_t t = 0; t < p.graph.vertex_data.size(); ++t) o << (t ? "," : "") << p.graph.adj[t];
+    o << "],\"lines\":[";
+    for (size_t i = 0; i < p.lines.size(); ++i) {
+      const auto& l = p.lines[i];
+      o << (i ? "," : "") << "{\"labels\":";
+      vec(l.labels);
+      o << ",\"indices\":";
+      vec(l.indices);
+      o << ",\"C\":" << l.cycle_length << ",\"VC\":" << l.valid_cycle << ",\"IL\":" << l.interleave_lp
+        << ",\"SV\":" << l.selected_vertices << ",\"enumeration\":";
+      vec(l.enumeration);
+      o << "}";
+    }
+    o << "]}";
+    const std::string s = o.str();
+    if (s.size() + 1 > buflen) throw std::runtime_error("summary buffer too small");
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+/*
+ * C-ABI of the MI355X-native label-constrained pattern-matching path.
+ *
+ * The reference exposes this path as C++ templates called from one driver
+ * (no FFI exists upstream).  Each entry point below replaces one of those
+ * in-process interfaces; a caller that used them binds these instead
+ * (INTEGRATION.md shows the ctypes and C++ bindings).
+ *
+ *   pm_create / pm_destroy        graph open + per-pattern containers:
+ *                                 src/run_pattern_matching_beta.cpp:209-223, 307-328, 436-492
+ *   pm_vertex_data_degree         vertex_data_db_degree(graph, labels):
+ *                                 include/havoqgt/vertex_data_db_degree.hpp:133-151 (formula :109)
+ *   pm_vertex_data_set            vertex_data_db(graph, labels, prefix, 10000) (-v):
+ *                                 include/havoqgt/vertex_data_db.hpp:197-257
+ *   pm_lcc_bsp                    label_propagation_pattern_matching_bsp(...):
+ *                                 include/havoqgt/label_propagation_pattern_matching_nonunique_ee.hpp:1029-1153
+ *   pm_token_passing              token_passing_pattern_matching(...) -- nem_1 for pl < 4,
+ *                                 tds_batch_1 for pl >= 4 (switch at beta.cpp:762-767):
+ *                                 include/havoqgt/token_passing_pattern_matching_nonunique_nem_1.hpp:908-939,
+ *                                 include/havoqgt/token_passing_pattern_matching_nonunique_tds_batch_1.hpp:967-1324
+ *   pm_post_token_passing         unacked-source invalidation + state-map erase:
+ *                                 src/run_pattern_matching_beta.cpp:956-1071
+ *   pm_run_beta                   the whole do { LCC; NLCC lines } while loop and every
+ *                                 result file: src/run_pattern_matching_beta.cpp:539-1425
+ *   pm_export_state               vertex_state_map / template_vertices / vertex_active_edges_map
+ *                                 read-out used by the result writers (beta.cpp:1386-1425)
+ *
+ * Conventions: plain C types; int status (0 = OK, negative = error with
+ * pm_last_error()); device memory is owned by the context; host buffers are
+ * owned by the caller; one host thread per context.  There is NO CPU
+ * fallback: pm_create fails when no gfx950 device / HIP kernel image is
+ * available.
+ */
+#ifndef PM_ABI_H_
+#define PM_ABI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pm_ctx pm_ctx;
+
+typedef struct pm_graph_desc {
+  uint64_t n;            /* number of vertex ids (max id + 1)                     */
+  const uint64_t* off;   /* n + 1 CSR row offsets (host memory)                   */
+  const uint32_t* col;   /* off[n] targets, sorted within each row (host memory)  */
+  int32_t symmetric;     /* 1: every (u,v) has a matching (v,u)                    */
+  uint32_t nranks;       /* P used to name per-rank result files (owner rule)      */
+  uint64_t hub_threshold;/* delegate threshold (-d) used by the owner rule         */
+} pm_graph_desc;
+
+typedef struct pm_lcc_stats {
+  uint64_t supersteps;
+  uint64_t edges_traversed;     /* adjacency entries scanned by senders            */
+  uint64_t active_vertices;     /* |S| after the last superstep                     */
+  uint64_t active_edges;        /* sum |M[v]| over S after the last superstep       */
+  uint32_t not_finished;        /* some vertex was removed from S in a verify        */
+  uint32_t reserved;
+} pm_lcc_stats;
+
+typedef struct pm_tp_stats {
+  uint64_t sources;
+  uint64_t acked_sources;
+  uint64_t edges_traversed;     /* adjacency entries scanned by initiators/relays  */
+  uint64_t tokens;              /* tokens / partial walks created                   */
+  uint64_t walks;               /* complete TDS walks (0 for path/cycle lines)      */
+} pm_tp_stats;
+
+typedef struct pm_run_stats {
+  uint64_t iterations;
+  uint32_t terminated;          /* 0 when max_iterations stopped the loop           */
+  uint32_t reserved;
+  uint64_t lcc_edges;
+  uint64_t nlcc_edges;
+  uint64_t tds_edges;
+  uint64_t walks;               /* complete walks of the last TDS line run          */
+  uint64_t final_vertices;
+  uint64_t final_edges;
+  double seconds;               /* pattern_time_start -> pattern_time_end           */
+  double device_seconds;        /* sum of device-event time inside the loop         */
+  double lcc_first_kernel_ms;   /* duration of the fused superstep-0 scan kernel    */
+  uint64_t lcc_first_bytes;     /* algorithmic bytes of that kernel                 */
+} pm_run_stats;
+
+/* Context: uploads the CSR to device `device`, loads <pattern_dir>/0/pattern_*.
+ * Returns NULL on failure (message via pm_last_error(NULL)). */
+pm_ctx* pm_create(const pm_graph_desc* graph, const char* pattern_dir, int device);
+void pm_destroy(pm_ctx* ctx);
+const char* pm_last_error(const pm_ctx* ctx);
+
+/* Labels. */
+int pm_vertex_data_degree(pm_ctx* ctx);
+int pm_vertex_data_set(pm_ctx* ctx, const uint64_t* labels /* n entries, host */);
+
+/* Per-pattern reset: every vertex active, empty state map (beta.cpp:484-492). */
+int pm_reset(pm_ctx* ctx);
+
+/* One LCC call: exactly `diameter` supersteps (nonunique_ee.hpp:1069). */
+int pm_lcc_bsp(pm_ctx* ctx, int init_step, uint64_t itr, pm_lcc_stats* out);
+
+/* One NLC line (index pl): path/cycle walk for pl < 4, TDS for pl >= 4. */
+int pm_token_passing(pm_ctx* ctx, uint32_t pl, pm_tp_stats* out);
+
+/* Post-processing of the last pm_token_passing call; *deleted = any source invalidated. */
+int pm_post_token_passing(pm_ctx* ctx, uint32_t pl, uint32_t* deleted);
+
+/* Whole driver loop + result files under result_dir (must exist; "" = no files).
+ * max_iterations caps the do/while loop (0 = unlimited, as in the reference). */
+int pm_run_beta(pm_ctx* ctx, const char* result_dir, uint64_t max_iterations, pm_run_stats* out);
+
+/* State read-out: tpub[n] (0 = not in S), moff/mlen per vertex and the alive
+ * neighbour ids.  Any pointer may be NULL.  *n_edges receives sum |M[v]| over S;
+ * nbrs must hold that many entries, written row by row in vertex order. */
+int pm_export_state(pm_ctx* ctx, uint16_t* tpub, uint32_t* mdeg, uint32_t* nbrs, uint64_t* n_edges);
+
+/* Host-side input builders (no device needed). */
+int pm_rmat_csr(uint64_t scale, uint64_t p_gen, uint64_t** off, uint32_t** col, uint64_t* n);
+void pm_free_host(void* p);
+int pm_write_graph(const char* base, uint64_t n, const uint64_t* off, const uint32_t* col, int symmetric,
+                   uint32_t nranks, uint64_t hub_threshold);
+int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n, int* symmetric,
+                  uint32_t* nranks, uint64_t* hub_threshold);
+
+/* Parsed pattern directory as JSON text (host only; loader check). */
+int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen);
+
+/* Build info: returns the offload arch the kernels were compiled for ("gfx950"). */
+const char* pm_build_arch(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PM_ABI_H_ */

@@ -1,0 +1,103 @@
+"""CPU tests of the product's host side: C-ABI library, loaders, generator, graph files."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import fuzzypatternmatching_amd as pm
+from fuzzypatternmatching_amd import _abi
+import oracle
+import pmtest
+
+GOLDEN = os.path.join(pmtest.ROOT, "tests", "golden")
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load()
+    header = open(os.path.join(pmtest.ROOT, "include", "pm_abi.h")).read()
+    declared = set(re.findall(r"\b(pm_[a-z_0-9]+)\s*\(", header))
+    assert len(declared) >= 15
+    bound = {name for name, _, _ in _abi.SIGNATURES}
+    assert declared == bound, declared ^ bound
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.pm_build_arch() == b"gfx950"
+
+
+def test_create_without_gpu_fails_loudly(tree_pattern):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    g = pm.Graph.from_edges([0, 1], [1, 0], n=2)
+    with pytest.raises(pm.PMError, match="no HIP device|not gfx950"):
+        pm.PatternMatcher(g, tree_pattern)
+
+
+def test_pattern_loader_tree(tree_pattern):
+    s = pm.pattern_summary(tree_pattern)
+    assert s["vertex_count"] == 7 and s["edge_count"] == 12 and s["diameter"] == 8
+    assert s["vertex_data"] == [3, 4, 7, 2, 3, 5, 7]
+    assert s["vertices"] == [0, 1, 4, 5, 7, 8, 11, 12]
+    assert s["adj"] == [0b10, 0b1101, 0b10, 0b100010, 0b100000, 0b1011000, 0b100000]
+    assert len(s["lines"]) == 5
+    l0, l4 = s["lines"][0], s["lines"][4]
+    assert l0["labels"] == [3, 5, 2, 4, 3] and l0["indices"] == [4, 5, 3, 1, 0]
+    assert (l0["C"], l0["VC"], l0["IL"], l0["SV"]) == (3, 0, 1, 0)
+    assert l4["C"] == 7 and l4["enumeration"] == [0, 1, 2, 1, 4, 5, 6, 5, 8]
+
+
+def test_pattern_loader_errors(tmp_path):
+    d = tmp_path / "p" / "0"
+    d.mkdir(parents=True)
+    (d / "pattern_edge").write_text("0 1\n1 0\n")
+    (d / "pattern_vertex_data").write_text("0 3\n1 4\n")
+    (d / "pattern_stat").write_text("diameter : 2\n")
+    (d / "pattern_nlc").write_text("3 4  3 : 0 1 0 : 1 : 1 : 0 : 0\n")  # double space -> stoull throws
+    (d / "pattern_non_local_constraint").write_text("0 1 0 : 0 1 0 : 0 0 0\n")
+    with pytest.raises(pm.PMError):
+        pm.pattern_summary(str(tmp_path / "p"))
+
+
+@pytest.mark.parametrize("scale,p_gen", [(10, 1), (12, 4)])
+def test_rmat_generator_matches_oracle(scale, p_gen):
+    g = pm.rmat_graph(scale, p_gen)
+    off, col = oracle.rmat_csr(scale, p_gen)
+    assert g.n == 1 << scale and g.nnz == (1 << scale) * 32
+    np.testing.assert_array_equal(g.off, off)
+    np.testing.assert_array_equal(g.col, col)
+
+
+def _grid_edges():
+    rows = [l.split() for l in open(os.path.join(GOLDEN, "grid_graph_weighted_edges.txt")) if l.strip()]
+    return np.array([int(r[0]) for r in rows]), np.array([int(r[1]) for r in rows])
+
+
+def test_grid_fixture_csr_and_delegates(tmp_path):
+    # test/include/input_graph.hpp:9-68 and test_delegate_graph_static.cpp:140-152
+    src, dst = _grid_edges()
+    assert src.size == 44
+    g = pm.Graph.from_edges(src, dst, n=15, nranks=2, hub_threshold=4)
+    assert list(g.degrees()) == [2, 3, 3, 3, 2, 3, 4, 4, 4, 3, 2, 3, 3, 3, 2]
+    assert list(g.off) == [0, 2, 5, 8, 11, 13, 16, 20, 24, 28, 31, 33, 36, 39, 42, 44]
+    assert g.symmetric
+    # graph files: delegates {6,7,8} at -d 4, round trip of the sorted edge list
+    base = str(tmp_path / "grid")
+    pm.write_graph(base, g, nranks=2)
+    assert os.path.exists(base + "_0_of_2") and os.path.exists(base + "_1_of_2")
+    h = pm.read_graph(base)
+    assert h.nranks == 2 and h.hub_threshold == 4
+    np.testing.assert_array_equal(h.off, g.off)
+    np.testing.assert_array_equal(h.col, g.col)
+    hubs = [v for v in range(15) if g.degrees()[v] >= 4]
+    assert hubs == [6, 7, 8]
+
+
+def test_graph_file_roundtrip_rmat(tmp_path):
+    g = pm.rmat_graph(11, 2, nranks=3)
+    base = str(tmp_path / "rmat")
+    pm.write_graph(base, g)
+    h = pm.read_graph(base)
+    np.testing.assert_array_equal(h.off, g.off)
+    np.testing.assert_array_equal(h.col, g.col)
+    assert h.nranks == 3 and h.symmetric

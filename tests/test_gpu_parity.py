@@ -1,0 +1,121 @@
+"""GPU parity tests: the HIP path (via the C-ABI) against the CPU oracle on the same inputs."""
+import os
+
+import numpy as np
+import pytest
+
+import fuzzypatternmatching_amd as pm
+import oracle
+import pmtest
+
+pytestmark = pytest.mark.gpu
+
+PATTERNS = {
+    "tree": os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern"),
+    "cycle": os.path.join(pmtest.ROOT, "patterns", "rmat_log2_cycle4_pattern"),
+}
+
+# (pattern, scale, P_gen, label alphabet or None for degree labels, nranks)
+RMAT_CASES = [
+    ("tree", 10, 1, None, 1),
+    ("tree", 16, 4, None, 1),
+    ("tree", 16, 4, None, 4),
+    ("cycle", 14, 4, None, 1),
+    ("cycle", 10, 1, 8, 1),
+    ("cycle", 12, 4, 8, 3),
+    ("tree", 10, 1, 16, 1),
+    ("tree", 9, 2, 8, 2),
+]
+
+
+def _run_both(off, col, pattern, tmp_path, labels=None, nranks=1, max_iterations=100):
+    a, b = tmp_path / "oracle", tmp_path / "gpu"
+    so = oracle.run(off, col, pattern, str(a), labels=labels, nranks=nranks, max_iterations=max_iterations)
+    g = pm.Graph(off, col, True, nranks)
+    m = pm.PatternMatcher(g, pattern, labels=labels)
+    sg = m.run_beta(str(b), max_iterations=max_iterations)
+    m.close()
+    return so, sg, pmtest.compare_result_dirs(str(a), str(b), nranks)
+
+
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks", RMAT_CASES)
+def test_rmat_matches_oracle(pat, scale, p_gen, alphabet, nranks, tmp_path):
+    g = pm.rmat_graph(scale, p_gen)
+    labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, labels, nranks)
+    assert diffs == []
+    assert sg["iterations"] == so["iterations"] and sg["terminated"] == so["terminated"]
+    assert sg["final_vertices"] == so["final_vertices"] and sg["final_edges"] == so["final_edges"]
+    # edges-traversed counters are defined identically on both sides
+    assert sg["lcc_edges"] == so["lcc_edges"]
+    assert sg["nlcc_edges"] == so["nlcc_edges"]
+    assert sg["tds_edges"] == so["tds_edges"]
+    assert sg["walks"] == so["paths"]
+
+
+def _tree_pairs():
+    return [(0, 1), (1, 2), (1, 3), (3, 5), (4, 5), (5, 6)], np.array([3, 4, 7, 2, 3, 5, 7], np.uint64)
+
+
+def test_known_answer_single_embedding(tmp_path):
+    pairs, labels = _tree_pairs()
+    off, col = pmtest.symmetric_csr(pairs, 7)
+    so, sg, diffs = _run_both(off, col, PATTERNS["tree"], tmp_path, labels)
+    assert diffs == []
+    assert sg["final_vertices"] == 7 and sg["final_edges"] == 12 and sg["walks"] == 1
+    lines = open(tmp_path / "gpu/0/all_ranks_subgraphs/subgraphs_4_0").read().split("\n")
+    assert lines[0] == "[0], 0, 1, 2, 1, 3, 5, 4, 5, 6, [6]"
+
+
+def test_known_answer_shared_label3_vertex(tmp_path):
+    pairs = [(0, 1), (1, 2), (1, 3), (3, 5), (0, 5), (5, 6)]
+    labels = np.array([3, 4, 7, 2, 99, 5, 7], np.uint64)
+    off, col = pmtest.symmetric_csr(pairs, 7)
+    so, sg, diffs = _run_both(off, col, PATTERNS["tree"], tmp_path, labels)
+    assert diffs == []
+    assert sg["final_vertices"] == 0
+
+
+def test_empty_and_isolated_inputs(tmp_path):
+    # no edges at all, and a graph whose labels match nothing
+    off = np.zeros(9, np.uint64)
+    col = np.zeros(0, np.uint32)
+    so, sg, diffs = _run_both(off, col, PATTERNS["tree"], tmp_path / "a", np.full(8, 3, np.uint64))
+    assert diffs == [] and sg["final_vertices"] == 0
+    off2, col2 = pmtest.symmetric_csr([(0, 1), (1, 2), (2, 0), (2, 2)], 3)  # includes a self loop
+    so, sg, diffs = _run_both(off2, col2, PATTERNS["cycle"], tmp_path / "b", np.array([3, 4, 5], np.uint64))
+    assert diffs == []
+
+
+def test_duplicate_edges_and_self_loops(tmp_path):
+    pairs, labels = _tree_pairs()
+    pairs = pairs + [(1, 2), (1, 2), (5, 5), (3, 3), (0, 1)]  # multiplicity + self loops
+    off, col = pmtest.symmetric_csr(pairs, 7)
+    so, sg, diffs = _run_both(off, col, PATTERNS["tree"], tmp_path, labels)
+    assert diffs == []
+    assert sg["lcc_edges"] == so["lcc_edges"]
+
+
+def test_step_api_matches_driver():
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    m = pm.PatternMatcher(g, PATTERNS["cycle"], labels=labels)
+    m.reset()
+    s = m.lcc_bsp(True)
+    assert s["supersteps"] == 4
+    tp = m.token_passing(0)
+    assert tp["sources"] > 0 and tp["edges_traversed"] > 0
+    m.post_token_passing(0)
+    tpub, mdeg, nbrs = m.export_state()
+    assert int(mdeg.sum()) == nbrs.shape[0]
+    assert np.all(mdeg[tpub == 0] == 0)
+    m.close()
+
+
+def test_iteration_cap_reports_non_termination(tmp_path):
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS["cycle"], tmp_path, labels, max_iterations=1)
+    assert sg["iterations"] == so["iterations"] == 1
+    assert sg["terminated"] == so["terminated"] == 0
+    assert diffs == []
