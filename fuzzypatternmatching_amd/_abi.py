@@ -89,6 +89,7 @@ SIGNATURES = [
     ("pm_read_graph", ctypes.c_int, [c_char_p, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_u64),
                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_u32), ctypes.POINTER(c_u64)]),
     ("pm_pattern_summary", ctypes.c_int, [c_char_p, c_char_p, c_u64]),
+    ("pm_debug_time_lcc_first", ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     ("pm_build_arch", c_char_p, []),
 ]
 

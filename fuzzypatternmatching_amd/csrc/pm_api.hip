@@ -97,6 +97,7 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   }
   c->d_labels = dalloc<uint64_t>(c->n);
   c->d_tl = dalloc<uint16_t>(c->n);
+  c->d_tlbits = dalloc<uint64_t>((c->n + 63) / 64 + 1);
   c->d_tpub[0] = dalloc<uint16_t>(c->n);
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
@@ -109,12 +110,22 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   c->d_nS = dalloc<uint32_t>(1);
   c->d_flags = dalloc<uint32_t>(4);
   c->d_tsm = dalloc<uint8_t>(c->n);
+  if (c->nranks > 64) throw std::runtime_error("more than 64 ranks for result-file attribution");
+  c->d_part = dalloc<uint64_t>(uint64_t(kPartGridMax) * slot_words(*c));
+  {
+    const uint64_t chunks = (c->n + 63) / 64;
+    c->d_cmask = dalloc<uint64_t>(chunks + 1);
+    c->d_cbase = dalloc<uint64_t>(chunks + 1);
+    c->scan_tmp_bytes = slist_scan_tmp_bytes(c->n);
+    c->d_scan_tmp = dalloc<char>(c->scan_tmp_bytes);
+  }
   size_t free_b = 0, total_b = 0;
   PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
   size_t arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
   arena = std::max<size_t>(arena, size_t(64) << 20);
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
+  c->k1_resident_blocks = query_k1_resident_blocks(device);
   // default labels = degree labels
   launch_degree_labels(*c);
   c->labels_host.assign(c->n, 0);
@@ -126,9 +137,9 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
 static void destroy_ctx(pm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_off, c->d_col, c->d_labels, c->d_hubs, c->d_tl, c->d_tpub[0], c->d_tpub[1], c->d_tst,
+  void* ptrs[] = {c->d_off, c->d_col, c->d_labels, c->d_hubs, c->d_tl, c->d_tlbits, c->d_tpub[0], c->d_tpub[1], c->d_tst,
                   c->d_mcol, c->d_mst, c->d_mlen, c->d_malive, c->d_slist, c->d_sources, c->d_nS, c->d_flags,
-                  c->d_tsm, c->d_counts, c->arena.base};
+                  c->d_tsm, c->d_counts, c->d_part, c->d_cmask, c->d_cbase, c->d_scan_tmp, c->arena.base};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -160,24 +171,22 @@ struct LccOut {
 static void ensure_counts(Ctx& c, size_t slots) {
   if (c.counts_slots >= slots) return;
   if (c.d_counts) (void)hipFree(c.d_counts);
-  c.d_counts = dalloc<uint64_t>(slots * (2 * c.nranks + 2));
+  c.d_counts = dalloc<uint64_t>(slots * slot_words(c));
   c.counts_slots = slots;
 }
 
 // label_propagation_pattern_matching_bsp (nonunique_ee.hpp:1033-1153).
 static LccOut lcc_call(Ctx& c, bool init_step) {
   const uint64_t D = c.pattern.graph.diameter;
-  const uint64_t slot_words = 2 * c.nranks + 2;
+  const uint64_t W = slot_words(c);
+  const uint64_t P = c.nranks <= 1 ? 1 : c.nranks;
   ensure_counts(c, D);
-  PM_HIP_CHECK(hipMemsetAsync(c.d_counts, 0, D * slot_words * sizeof(uint64_t), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(c.d_flags, 0, 2 * sizeof(uint32_t), c.stream));
   std::vector<hipEvent_t> ev(D + 1);
   for (auto& e : ev) PM_HIP_CHECK(hipEventCreate(&e));
   PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
   hipEvent_t k_beg = nullptr, k_end = nullptr;
   for (uint64_t ss = 0; ss < D; ++ss) {
-    uint64_t* slot = c.d_counts + ss * slot_words;
-    uint64_t* trav = slot + 2 * c.nranks;
+    uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
       launch_label_match(c);
@@ -185,33 +194,35 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       PM_HIP_CHECK(hipEventCreate(&k_beg));
       PM_HIP_CHECK(hipEventCreate(&k_end));
       PM_HIP_CHECK(hipEventRecord(k_beg, c.stream));
-      launch_lcc_first(c, slot, trav);
+      launch_lcc_first(c, slot);
       PM_HIP_CHECK(hipEventRecord(k_end, c.stream));
       PM_HIP_CHECK(hipMemcpyAsync(&c.nS_host, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
       PM_HIP_CHECK(hipStreamSynchronize(c.stream));
       c.lcc_started = true;
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
-      launch_lcc_step(c, slot, trav);
+      launch_lcc_step(c, slot);
     }
     PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
-  std::vector<uint64_t> host(D * slot_words);
-  uint32_t flags[2] = {0, 0};
+  std::vector<uint64_t> host(D * W);
   PM_HIP_CHECK(hipMemcpyAsync(host.data(), c.d_counts, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipMemcpyAsync(flags, c.d_flags, sizeof(flags), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   LccOut out;
+  bool asym = false;
   for (uint64_t ss = 0; ss < D; ++ss) {
+    const uint64_t* h = host.data() + ss * W;
     std::vector<uint64_t> vc(c.nranks), ec(c.nranks);
     for (uint32_t r = 0; r < c.nranks; ++r) {
-      vc[r] = host[ss * slot_words + 2 * r];
-      ec[r] = host[ss * slot_words + 2 * r + 1];
+      vc[r] = h[r];
+      ec[r] = h[P + r];
     }
     out.vcount.push_back(vc);
     out.ecount.push_back(ec);
-    out.trav.push_back(host[ss * slot_words + 2 * c.nranks]);
-    if (ss == 0 && init_step) out.matching_rows = host[ss * slot_words + 2 * c.nranks + 1];
+    out.trav.push_back(h[2 * P]);
+    if (ss == 0 && init_step) out.matching_rows = h[2 * P + 1];
+    if (h[2 * P + 2]) out.not_finished = true;
+    if (h[2 * P + 3]) asym = true;
     float ms = 0.f;
     PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[ss], ev[ss + 1]));
     out.seconds.push_back(ms * 1e-3);
@@ -225,8 +236,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     (void)hipEventDestroy(k_end);
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
-  out.not_finished = flags[0] != 0;
-  if (flags[1])
+  if (asym)
     throw std::runtime_error(
         "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message); "
         "the push-form LCC kernel needed for this case is not implemented yet");
@@ -259,16 +269,18 @@ static void add_count_lines(Ctx& c, DriverFiles& f, uint64_t itr, const char* ta
 
 static void count_state(Ctx& c, std::vector<uint64_t>& vc, std::vector<uint64_t>& ec) {
   ensure_counts(c, 1);
-  PM_HIP_CHECK(hipMemsetAsync(c.d_counts, 0, (2 * c.nranks + 2) * sizeof(uint64_t), c.stream));
+  const uint64_t W = slot_words(c);
+  const uint64_t P = c.nranks <= 1 ? 1 : c.nranks;
+  PM_HIP_CHECK(hipMemsetAsync(c.d_counts, 0, W * sizeof(uint64_t), c.stream));
   if (c.nS_host) launch_count_state(c, c.d_counts);
-  std::vector<uint64_t> host(2 * c.nranks);
+  std::vector<uint64_t> host(W);
   PM_HIP_CHECK(hipMemcpyAsync(host.data(), c.d_counts, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   vc.assign(c.nranks, 0);
   ec.assign(c.nranks, 0);
   for (uint32_t r = 0; r < c.nranks; ++r) {
-    vc[r] = host[2 * r];
-    ec[r] = host[2 * r + 1];
+    vc[r] = host[r];
+    ec[r] = host[P + r];
   }
 }
 
@@ -653,6 +665,33 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
 }
 
 const char* pm_build_arch(void) { return "gfx950"; }
+
+// Diagnostics: times `reps` launches of a superstep-0 kernel variant on the
+// current labels (state is reset first; variants != 0 produce wrong output).
+int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
+  PM_API_BODY(ctx, {
+    pm::reset_state(*ctx);
+    pm::launch_label_match(*ctx);
+    hipEvent_t a, b;
+    PM_HIP_CHECK(hipEventCreate(&a));
+    PM_HIP_CHECK(hipEventCreate(&b));
+    // variant >= 100: same kernel (variant - 100) with one 64-vertex chunk per wave
+    const unsigned grid = variant >= 100 ? static_cast<unsigned>(std::min<uint64_t>((ctx->n + 255) / 256, 1u << 20))
+                                         : pm::lcc_first_grid(*ctx);
+    if (variant >= 100) variant -= 100;
+    pm::launch_lcc_first_kernel(*ctx, variant, grid);  // warm
+    PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
+    for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, variant, grid);
+    PM_HIP_CHECK(hipEventRecord(b, ctx->stream));
+    PM_HIP_CHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    PM_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    if (ms_out) *ms_out = ms / std::max(1, reps);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    pm::reset_state(*ctx);
+  });
+}
 
 int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen) {
   try {

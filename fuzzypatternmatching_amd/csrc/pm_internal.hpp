@@ -77,6 +77,7 @@ struct Ctx {
 
   // vertex state (device)
   uint16_t* d_tl = nullptr;       // template bits matching the vertex label
+  uint64_t* d_tlbits = nullptr;   // 1 bit per vertex: tl != 0
   uint16_t* d_tpub[2] = {nullptr, nullptr};  // template_vertices (T_pub), 0 = not in S
   int cur = 0;
   uint16_t* d_tst = nullptr;      // vertex_state.template_vertices (T_state)
@@ -88,6 +89,13 @@ struct Ctx {
   uint32_t* d_nS = nullptr;       // device count of d_slist
   uint32_t* d_flags = nullptr;    // [0] not_finished, [1] asymmetric edge state, [2] deleted
   uint64_t* d_counts = nullptr;   // per-slot per-rank counts (vertices, edges) + traversed
+  uint64_t* d_part = nullptr;     // per-block counter partials (kMaxGrid x slot_words)
+  uint64_t* d_cmask = nullptr;    // superstep-0 survivor mask per 64-vertex chunk
+  uint64_t* d_cbase = nullptr;    // exclusive scan of the chunk popcounts
+  void* d_scan_tmp = nullptr;     // hipcub scan workspace for the slist build
+  size_t scan_tmp_bytes = 0;
+  uint64_t last_acked = 0;
+  unsigned k1_resident_blocks = 0;
   uint8_t* d_tsm = nullptr;       // token source map: 0 none, 1 unacked source, 2 acked
   size_t counts_slots = 0;
 
@@ -112,9 +120,17 @@ struct Ctx {
 // Kernel launchers (pm_kernels.hip).
 void launch_degree_labels(Ctx& c);
 void launch_label_match(Ctx& c);
-void launch_lcc_first(Ctx& c, uint64_t* d_slot_counts, uint64_t* d_trav);
-void launch_lcc_step(Ctx& c, uint64_t* d_slot_counts, uint64_t* d_trav);
-void launch_count_state(Ctx& c, uint64_t* d_slot_counts);
+// Counter slots: W = slot_words(c) u64 = [vertices per rank | edges per rank |
+// traversed | matching rows | removed flag | asymmetry flag].
+uint32_t slot_words(const Ctx& c);
+void launch_lcc_first(Ctx& c, uint64_t* d_slot);
+void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid);  // variant != 0: ablation builds
+unsigned lcc_first_grid(const Ctx& c);
+unsigned query_k1_resident_blocks(int device);
+void launch_lcc_step(Ctx& c, uint64_t* d_slot);
+void launch_count_state(Ctx& c, uint64_t* d_slot);
+size_t slist_scan_tmp_bytes(uint64_t n);
+static constexpr unsigned kPartGridMax = 2048;
 
 struct TpResult {
   uint64_t sources = 0, acked = 0, edges = 0, tokens = 0, walks = 0;

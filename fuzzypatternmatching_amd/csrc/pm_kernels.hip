@@ -33,6 +33,14 @@ static constexpr int kWave = 64;
 static constexpr int kBlock = 256;
 static constexpr int kWpb = kBlock / kWave;
 static constexpr uint32_t kNone = 0xFFFFFFFFu;
+static constexpr unsigned kMaxGrid = 1024;  // persistent-style grids: 4 blocks per CU
+static constexpr int kU = 8;                // strip unroll: independent loads in flight per lane
+
+struct PopcOp {
+  __host__ __device__ uint64_t operator()(unsigned long long m) const {
+    return static_cast<uint64_t>(__builtin_popcountll(m));
+  }
+};
 
 // ---------------------------------------------------------------------------
 // helpers
@@ -103,6 +111,87 @@ __device__ __forceinline__ uint32_t seg_scan_orsum(uint32_t x, int row) {
   return x;
 }
 
+// Per-block counter partials (no same-address global atomics: a wave-level
+// atomic per chunk on one word serialises at one L2 channel).  Layout of one
+// block's W = 2P + 4 words: [vertices per rank | edges per rank | traversed |
+// matching rows | removed flag | asymmetry flag]; k_reduce_partials sums them.
+static constexpr int kMaxRanks = 64;
+struct BlockAcc {
+  uint64_t trav = 0, match = 0, vs = 0, es = 0;
+  uint32_t removed = 0, asym = 0;
+};
+
+__device__ __forceinline__ void acc_owner(unsigned long long* s_hist, const OwnerArgs& oa, uint64_t v,
+                                          uint64_t edges) {
+  const uint32_t r = owner_of(v, oa);
+  atomicAdd(&s_hist[r], 1ull);
+  atomicAdd(&s_hist[oa.nranks + r], static_cast<unsigned long long>(edges));
+}
+
+// All threads of the block must call this (after their loops).
+__device__ __forceinline__ void flush_block(BlockAcc a, const OwnerArgs& oa, unsigned long long* s_hist,
+                                            unsigned long long* s_red, unsigned long long* __restrict__ part) {
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const uint64_t v[6] = {wave_sum(a.trav), wave_sum(a.match), wave_sum(a.vs), wave_sum(a.es),
+                         wave_sum(a.removed), wave_sum(a.asym)};
+  if (lane == 0)
+    for (int i = 0; i < 6; ++i) s_red[w * 6 + i] = v[i];
+  __syncthreads();
+  const uint32_t P = oa.nranks <= 1 ? 1 : oa.nranks;
+  const uint32_t W = 2 * P + 4;
+  unsigned long long* out = part + uint64_t(blockIdx.x) * W;
+  if (threadIdx.x < 6) {
+    unsigned long long t = 0;
+    for (int i = 0; i < kWpb; ++i) t += s_red[i * 6 + threadIdx.x];
+    const int j = threadIdx.x;
+    if (j == 0) out[2 * P] = t;
+    if (j == 1) out[2 * P + 1] = t;
+    if (j == 4) out[2 * P + 2] = t;
+    if (j == 5) out[2 * P + 3] = t;
+    if (oa.nranks <= 1) {
+      if (j == 2) out[0] = t;
+      if (j == 3) out[1] = t;
+    }
+  }
+  if (oa.nranks > 1)
+    for (uint32_t i = threadIdx.x; i < 2 * P; i += blockDim.x) out[i] = s_hist[i];
+}
+
+// Block-aggregated global add: one atomic per block (all threads must call).
+__device__ __forceinline__ void block_atomic_add(unsigned long long* dst, uint64_t v) {
+  __shared__ unsigned long long s_b[kWpb];
+  v = wave_sum(v);
+  if (lane_id() == 0) s_b[threadIdx.x / kWave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int i = 0; i < kWpb; ++i) t += s_b[i];
+    if (t) atomicAdd(dst, t);
+  }
+  __syncthreads();
+}
+
+// One block: thread t sums blocks t, t+256, ... of every word (independent
+// loads in flight), then a wave + LDS reduction per word.
+__global__ __launch_bounds__(kBlock) void k_reduce_partials(const unsigned long long* __restrict__ part,
+                                                            uint32_t nblocks, uint32_t W,
+                                                            unsigned long long* __restrict__ slot) {
+  __shared__ unsigned long long s_w[kWpb];
+  for (uint32_t j = 0; j < W; ++j) {
+    unsigned long long t = 0;
+    for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) t += part[uint64_t(b) * W + j];
+    t = wave_sum(t);
+    if (lane_id() == 0) s_w[threadIdx.x / kWave] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long s = 0;
+      for (int i = 0; i < kWpb; ++i) s += s_w[i];
+      slot[j] = s;
+    }
+    __syncthreads();
+  }
+}
+
 // Last row r (0..63) of a wave's strip space whose start <= j.
 __device__ __forceinline__ int find_row(const uint64_t* rs, uint64_t j) {
   int lo = 0, hi = kWave - 1;
@@ -124,13 +213,26 @@ __global__ void k_degree_labels(const uint64_t* __restrict__ off, uint64_t n, ui
 }
 
 // lppm_visitor::visit first-superstep label match (nonunique_ee.hpp:523-537).
-__global__ void k_label_match(const uint64_t* __restrict__ labels, uint64_t n, PatArgs pa, uint16_t* __restrict__ tl) {
-  for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < n; v += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t lab = labels[v];
+// Also writes a 1-bit-per-vertex "matches some template" bitmap: superstep 0
+// probes it before gathering Tl (V/8 bytes stay L2-resident, and only a
+// minority of scanned entries point at matching vertices on R-MAT).
+__global__ void k_label_match(const uint64_t* __restrict__ labels, uint64_t n, PatArgs pa, uint16_t* __restrict__ tl,
+                              unsigned long long* __restrict__ tlbits) {
+  const uint64_t nwords = (n + kWave - 1) / kWave;
+  const int lane = lane_id();
+  const uint64_t wave = (blockIdx.x * uint64_t(blockDim.x) + threadIdx.x) / kWave;
+  const uint64_t nwaves = uint64_t(gridDim.x) * blockDim.x / kWave;
+  for (uint64_t wd = wave; wd < nwords; wd += nwaves) {
+    const uint64_t v = wd * kWave + lane;
     uint16_t t = 0;
-    for (int i = 0; i < pa.K; ++i)
-      if (pa.plabel[i] == lab) t |= static_cast<uint16_t>(1u << i);
-    tl[v] = t;
+    if (v < n) {
+      const uint64_t lab = labels[v];
+      for (int i = 0; i < pa.K; ++i)
+        if (pa.plabel[i] == lab) t |= static_cast<uint16_t>(1u << i);
+      tl[v] = t;
+    }
+    const unsigned long long m = __ballot(t != 0);
+    if (lane == 0) tlbits[wd] = m;
   }
 }
 
@@ -146,12 +248,19 @@ __global__ void k_label_match(const uint64_t* __restrict__ labels, uint64_t n, P
 //   M[u]  = distinct contributing v (first occurrence in the sorted row);
 //   T_state = keep_bits(Tl(u), TN); empty -> removed (sets not_finished).
 // Survivors get T_pub = T_state, |M[u]| and a slot in slist.
+// MODE (ablation only, 0 in the product): bit0 skips the M writes, bit1 the
+// bitmap/Tl gathers, bit2 the segmented scans (diagnostic builds, wrong output).
+template <int MODE, int KU = kU>
 __global__ __launch_bounds__(kBlock) void k_lcc_first(
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ col, const uint16_t* __restrict__ tl,
-    uint64_t n, PatArgs pa, OwnerArgs oa, uint16_t* __restrict__ tst, uint16_t* __restrict__ tpub,
+    const unsigned long long* __restrict__ tlbits, uint64_t n, PatArgs pa, OwnerArgs oa, uint16_t* __restrict__ tst, uint16_t* __restrict__ tpub,
     uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst, uint32_t* __restrict__ mlen,
-    uint32_t* __restrict__ malive, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS,
-    uint32_t* __restrict__ flags, unsigned long long* __restrict__ counts, unsigned long long* __restrict__ trav) {
+    uint32_t* __restrict__ malive, unsigned long long* __restrict__ cmask, unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+  BlockAcc acc;
   __shared__ uint64_t s_rs[kWpb][kWave];
   __shared__ uint64_t s_beg[kWpb][kWave];
   __shared__ uint32_t s_acc[kWpb][kWave];  // TN | (contributing distinct count << 16), carried across strips
@@ -159,17 +268,27 @@ __global__ __launch_bounds__(kBlock) void k_lcc_first(
   __shared__ uint16_t s_nm[kWpb][kWave];
   const int lane = lane_id(), w = threadIdx.x / kWave;
   const uint64_t nchunks = (n + kWave - 1) / kWave;
-  for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb) {
+  const uint64_t cstride = uint64_t(gridDim.x) * kWpb;
+  // Vertex data of the next chunk is loaded one iteration ahead (software
+  // pipelining): Tl and the two row offsets come from independent, coalesced
+  // loads (off[u+1] via a lane shuffle) so no HBM round trip sits between chunks.
+  uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w;
+  uint16_t pf_t = 0;
+  uint64_t pf_o = 0, pf_o63 = 0;
+  auto prefetch = [&](uint64_t c) {
+    const uint64_t u = c * kWave + lane;
+    pf_t = (c < nchunks && u < n) ? tl[u] : uint16_t(0);
+    pf_o = (c < nchunks) ? off[u < n ? u : n] : 0;
+    pf_o63 = (c < nchunks && lane == kWave - 1) ? off[(u + 1) < n ? (u + 1) : n] : 0;
+  };
+  prefetch(chunk);
+  for (; chunk < nchunks; chunk += cstride) {
     const uint64_t u = chunk * kWave + lane;
-    uint16_t Tu = 0;
-    uint64_t beg = 0, deg = 0;
-    if (u < n) {
-      Tu = tl[u];
-      if (Tu) {
-        beg = off[u];
-        deg = off[u + 1] - beg;
-      }
-    }
+    const uint16_t Tu = pf_t;
+    const uint64_t o_next = __shfl_down(pf_o, 1, kWave);
+    const uint64_t beg = pf_o;
+    const uint64_t deg = Tu ? ((lane == kWave - 1 ? pf_o63 : o_next) - beg) : 0;
+    prefetch(chunk + cstride);
     const uint64_t incl = wave_incl_scan(deg);
     const uint64_t total = __shfl(incl, kWave - 1, kWave);
     s_rs[w][lane] = incl - deg;
@@ -178,44 +297,71 @@ __global__ __launch_bounds__(kBlock) void k_lcc_first(
     s_acc[w][lane] = 0;
     s_cnt[w][lane] = 0;
     __builtin_amdgcn_wave_barrier();
-    for (uint64_t j0 = 0; j0 < total; j0 += kWave) {
-      const uint64_t j = j0 + lane;
-      const bool valid = j < total;
-      int r = kWave;  // sentinel row for idle lanes
-      uint32_t v = kNone;
-      uint64_t e = 0, rel = 0;
-      if (valid) {
-        r = find_row(s_rs[w], j);
-        rel = j - s_rs[w][r];
-        e = s_beg[w][r] + rel;
-        v = col[e];
-      }
-      const uint32_t vprev = __shfl_up(v, 1, kWave);
-      const int rprev = __shfl_up(r, 1, kWave);
-      uint32_t x = 0;
-      if (valid) {
-        bool first = true;
-        if (rel > 0) first = ((lane > 0 && rprev == r) ? vprev : col[e - 1]) != v;
-        const uint16_t Tv = tl[v];
-        const bool cm = (Tv & s_nm[w][r]) != 0;
-        x = (cm ? Tv : 0u) | ((cm && first) ? (1u << 16) : 0u);
-      }
-      const uint32_t inc = seg_scan_orsum(x, r);
-      const int rnext = __shfl_down(r, 1, kWave);
-      if (valid) {
-        if (x >> 16) {
-          // exclusive position of this distinct contributor inside u's row
-          const uint32_t pos = s_cnt[w][r] + (inc >> 16) - 1;
-          const uint64_t dst = s_beg[w][r] + pos;
-          mcol[dst] = v;
-          mst[dst] = 1;
-        }
-        if (lane == kWave - 1 || rnext != r) {
-          s_acc[w][r] |= inc & 0xFFFFu;
-          s_cnt[w][r] += inc >> 16;
+    // Strips of kU x 64 entries: every lane issues kU independent adjacency
+    // loads, then kU independent Tl gathers, before any reduction (memory-level
+    // parallelism; a single 64-entry strip per iteration is latency bound).
+    for (uint64_t j0 = 0; j0 < total; j0 += uint64_t(kWave) * KU) {
+      int r[KU];
+      uint64_t rel[KU], e[KU];
+      uint32_t v[KU];
+#pragma unroll
+      for (int q = 0; q < KU; ++q) {
+        const uint64_t j = j0 + uint64_t(q) * kWave + lane;
+        r[q] = kWave;  // sentinel row for idle lanes
+        rel[q] = 0;
+        e[q] = 0;
+        v[q] = kNone;
+        if (j < total) {
+          r[q] = find_row(s_rs[w], j);
+          rel[q] = j - s_rs[w][r[q]];
+          e[q] = s_beg[w][r[q]] + rel[q];
+          v[q] = col[e[q]];
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      uint32_t pv0 = kNone;
+      if (lane == 0 && r[0] < kWave && rel[0] > 0) pv0 = col[e[0] - 1];
+      bool hit[KU];
+      uint16_t tv[KU];
+      if (MODE & 2) {
+#pragma unroll
+        for (int q = 0; q < KU; ++q) tv[q] = static_cast<uint16_t>(v[q] & 0x1Fu);
+      } else {
+#pragma unroll
+        for (int q = 0; q < KU; ++q) hit[q] = (r[q] < kWave) && ((tlbits[v[q] >> 6] >> (v[q] & 63)) & 1ull);
+#pragma unroll
+        for (int q = 0; q < KU; ++q) tv[q] = hit[q] ? tl[v[q]] : uint16_t(0);
+      }
+#pragma unroll
+      for (int q = 0; q < KU; ++q) {
+        // predecessor entry j-1 (same row whenever rel > 0): lane-1 of this
+        // slice, lane 63 of the previous slice, or loaded before the strip.
+        uint32_t pv = __shfl_up(v[q], 1, kWave);
+        const uint32_t carry = q ? __shfl(v[q ? q - 1 : 0], kWave - 1, kWave) : pv0;
+        if (lane == 0) pv = carry;
+        const bool valid = r[q] < kWave;
+        uint32_t x = 0;
+        if (valid) {
+          const bool first = (rel[q] == 0) || (pv != v[q]);
+          const bool cm = (tv[q] & s_nm[w][r[q]]) != 0;
+          x = (cm ? tv[q] : 0u) | ((cm && first) ? (1u << 16) : 0u);
+        }
+        const uint32_t inc = (MODE & 4) ? x : seg_scan_orsum(x, r[q]);
+        const int rnext = __shfl_down(r[q], 1, kWave);
+        if (valid) {
+          if ((x >> 16) && !(MODE & 1)) {
+            // exclusive position of this distinct contributor inside u's row
+            const uint32_t pos = s_cnt[w][r[q]] + (inc >> 16) - 1;
+            const uint64_t dst = s_beg[w][r[q]] + pos;
+            mcol[dst] = v[q];
+            mst[dst] = 1;
+          }
+          if (lane == kWave - 1 || rnext != r[q]) {
+            s_acc[w][r[q]] |= inc & 0xFFFFu;
+            s_cnt[w][r[q]] += inc >> 16;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     }
     // finalize row `lane`
     bool survivor = false, removed = false;
@@ -237,31 +383,122 @@ __global__ __launch_bounds__(kBlock) void k_lcc_first(
       }
     }
     const uint64_t smask = __ballot(survivor);
-    const uint64_t rmask = __ballot(removed);
-    uint32_t base = 0;
-    if (lane == 0 && smask) base = atomicAdd(nS, static_cast<uint32_t>(__popcll(smask)));
-    base = __shfl(base, 0, kWave);
-    if (survivor) {
-      const uint32_t rank_in_wave = __popcll(smask & ((1ull << lane) - 1ull));
-      slist[base + rank_in_wave] = static_cast<uint32_t>(u);
-    }
-    if (lane == 0 && rmask) atomicOr(&flags[0], 1u);
+    if (lane == 0) cmask[chunk] = smask;  // slist is built from these masks (k_slist_write)
     // counts: vertices/edges per rank (owner rule) and traversed entries
-    const uint64_t tot_deg = wave_sum(deg);
-    if (oa.nranks <= 1) {
-      const uint64_t vs = __popcll(smask), es = wave_sum(survivor ? cnt : 0);
-      if (lane == 0) {
-        if (vs) atomicAdd(&counts[0], static_cast<unsigned long long>(vs));
-        if (es) atomicAdd(&counts[1], static_cast<unsigned long long>(es));
+    acc.trav += deg;
+    acc.match += Tu != 0;
+    acc.removed |= removed;
+    if (survivor) {
+      if (oa.nranks <= 1) {
+        acc.vs += 1;
+        acc.es += cnt;
+      } else {
+        acc_owner(s_hist, oa, u, cnt);
       }
-    } else if (survivor) {
-      const uint32_t r = owner_of(u, oa);
-      atomicAdd(&counts[2 * r], 1ull);
-      atomicAdd(&counts[2 * r + 1], static_cast<unsigned long long>(cnt));
     }
-    if (lane == 0 && tot_deg) atomicAdd(trav, static_cast<unsigned long long>(tot_deg));
-    const uint64_t nmatch = __popcll(__ballot(Tu != 0));
-    if (lane == 0 && nmatch) atomicAdd(trav + 1, static_cast<unsigned long long>(nmatch));
+  }
+  flush_block(acc, oa, s_hist, s_red, part);
+}
+
+// Alternative superstep-0 kernel (ablation): one lane per row, serial scan of
+// the row with kU-way unrolled independent loads; no LDS, no shuffles.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_lcc_first_lpr(
+    const uint64_t* __restrict__ off, const uint32_t* __restrict__ col, const uint16_t* __restrict__ tl,
+    const unsigned long long* __restrict__ tlbits, uint64_t n, PatArgs pa, OwnerArgs oa,
+    uint16_t* __restrict__ tst, uint16_t* __restrict__ tpub, uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst,
+    uint32_t* __restrict__ mlen, uint32_t* __restrict__ malive, unsigned long long* __restrict__ cmask,
+    unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+  BlockAcc acc;
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const uint64_t nchunks = (n + kWave - 1) / kWave;
+  for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb) {
+    const uint64_t u = chunk * kWave + lane;
+    uint16_t Tu = 0;
+    uint64_t beg = 0, deg = 0;
+    if (u < n) {
+      Tu = tl[u];
+      if (Tu) {
+        beg = off[u];
+        deg = off[u + 1] - beg;
+      }
+    }
+    const uint16_t NM = nbr_mask(Tu, pa);
+    uint32_t TN = 0, cnt = 0, prev = kNone;
+    for (uint64_t i0 = 0; i0 < deg; i0 += kU) {
+      uint32_t v[kU];
+      uint16_t tv[kU];
+#pragma unroll
+      for (int q = 0; q < kU; ++q) v[q] = (i0 + q < deg) ? col[beg + i0 + q] : kNone;
+#pragma unroll
+      for (int q = 0; q < kU; ++q) {
+        const bool hit = v[q] != kNone && ((tlbits[v[q] >> 6] >> (v[q] & 63)) & 1ull);
+        tv[q] = hit ? tl[v[q]] : uint16_t(0);
+      }
+#pragma unroll
+      for (int q = 0; q < kU; ++q) {
+        if (v[q] == kNone) break;
+        const bool cm = (tv[q] & NM) != 0;
+        if (cm) {
+          TN |= tv[q];
+          if (v[q] != prev) {
+            if (!(MODE & 1)) {
+              mcol[beg + cnt] = v[q];
+              mst[beg + cnt] = 1;
+            }
+            ++cnt;
+          }
+        }
+        prev = v[q];
+      }
+    }
+    bool survivor = false, removed = false;
+    if (Tu && TN) {
+      const uint16_t T = keep_bits(Tu, static_cast<uint16_t>(TN), pa);
+      if (T) {
+        survivor = true;
+        tst[u] = T;
+        tpub[u] = T;
+        mlen[u] = cnt;
+        malive[u] = cnt;
+      } else {
+        removed = true;
+      }
+    }
+    const uint64_t smask = __ballot(survivor);
+    if (lane == 0) cmask[chunk] = smask;
+    acc.trav += deg;
+    acc.match += Tu != 0;
+    acc.removed |= removed;
+    if (survivor) {
+      if (oa.nranks <= 1) {
+        acc.vs += 1;
+        acc.es += cnt;
+      } else {
+        acc_owner(s_hist, oa, u, cnt);
+      }
+    }
+  }
+  flush_block(acc, oa, s_hist, s_red, part);
+}
+
+// slist from the superstep-0 survivor masks: an exclusive scan of the
+// per-chunk popcounts (hipcub) gives each chunk's base.
+__global__ void k_slist_write(const unsigned long long* __restrict__ cmask, const uint64_t* __restrict__ base,
+                              uint64_t nchunks, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
+  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < nchunks; c += uint64_t(gridDim.x) * blockDim.x) {
+    unsigned long long m = cmask[c];
+    uint64_t o = base[c];
+    while (m) {
+      const int b = __ffsll(static_cast<long long>(m)) - 1;
+      m &= m - 1;
+      slist[o++] = static_cast<uint32_t>(c * kWave + b);
+    }
+    if (c == nchunks - 1) *nS = static_cast<uint32_t>(o);
   }
 }
 
@@ -281,8 +518,12 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t* __restrict__ off, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, const uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
-    uint32_t* __restrict__ malive, uint32_t* __restrict__ flags, unsigned long long* __restrict__ counts,
-    unsigned long long* __restrict__ trav) {
+    uint32_t* __restrict__ malive, unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+  BlockAcc acc;
   __shared__ uint64_t s_rs[kWpb][kWave];
   __shared__ uint64_t s_beg[kWpb][kWave];
   __shared__ uint32_t s_acc[kWpb][kWave];
@@ -317,32 +558,46 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     s_cnt[w][lane] = 0;
     __builtin_amdgcn_wave_barrier();
     bool asym = false;
-    for (uint64_t j0 = 0; j0 < total; j0 += kWave) {
-      const uint64_t j = j0 + lane;
-      const bool valid = j < total;
-      int r = kWave;
-      uint32_t x = 0;
-      if (valid) {
-        r = find_row(s_rs[w], j);
-        const uint64_t e = s_beg[w][r] + (j - s_rs[w][r]);
-        const uint8_t st = mst[e];
-        if (st & 1u) {
-          const uint32_t v = mcol[e];
-          const uint16_t Tv = tcur[v];
-          const bool ok = (Tv & s_nm[w][r]) != 0;
-          const bool flag = ok || (st & 2u);
-          mst[e] = flag ? 1u : 0u;
-          if ((st & 2u) && !ok && Tv) asym = true;
-          x = (ok ? Tv : 0u) | (flag ? (1u << 16) : 0u);
+    for (uint64_t j0 = 0; j0 < total; j0 += uint64_t(kWave) * kU) {
+      int r[kU];
+      uint64_t e[kU];
+      uint8_t st[kU];
+      uint32_t v[kU];
+#pragma unroll
+      for (int q = 0; q < kU; ++q) {
+        const uint64_t j = j0 + uint64_t(q) * kWave + lane;
+        r[q] = kWave;
+        e[q] = 0;
+        st[q] = 0;
+        v[q] = 0;
+        if (j < total) {
+          r[q] = find_row(s_rs[w], j);
+          e[q] = s_beg[w][r[q]] + (j - s_rs[w][r[q]]);
+          st[q] = mst[e[q]];
+          v[q] = mcol[e[q]];
         }
       }
-      const uint32_t inc = seg_scan_orsum(x, r);
-      const int rnext = __shfl_down(r, 1, kWave);
-      if (valid && (lane == kWave - 1 || rnext != r)) {
-        s_acc[w][r] |= inc & 0xFFFFu;
-        s_cnt[w][r] += inc >> 16;
+      uint16_t tv[kU];
+#pragma unroll
+      for (int q = 0; q < kU; ++q) tv[q] = (st[q] & 1u) ? tcur[v[q]] : uint16_t(0);
+#pragma unroll
+      for (int q = 0; q < kU; ++q) {
+        uint32_t x = 0;
+        if (st[q] & 1u) {
+          const bool ok = (tv[q] & s_nm[w][r[q]]) != 0;
+          const bool flag = ok || (st[q] & 2u);
+          mst[e[q]] = flag ? 1u : 0u;
+          if ((st[q] & 2u) && !ok && tv[q]) asym = true;
+          x = (ok ? tv[q] : 0u) | (flag ? (1u << 16) : 0u);
+        }
+        const uint32_t inc = seg_scan_orsum(x, r[q]);
+        const int rnext = __shfl_down(r[q], 1, kWave);
+        if (r[q] < kWave && (lane == kWave - 1 || rnext != r[q])) {
+          s_acc[w][r[q]] |= inc & 0xFFFFu;
+          s_cnt[w][r[q]] += inc >> 16;
+        }
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
     }
     bool survivor = false, removed = false;
     uint32_t cnt = 0;
@@ -361,40 +616,45 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         malive[u] = 0;
       }
     }
-    const uint64_t smask = __ballot(survivor);
-    const uint64_t rmask = __ballot(removed);
-    const uint64_t amask = __ballot(asym);
-    if (lane == 0 && rmask) atomicOr(&flags[0], 1u);
-    if (lane == 0 && amask) atomicOr(&flags[1], 1u);
-    const uint64_t sent = wave_sum(alive0);
-    if (oa.nranks <= 1) {
-      const uint64_t vs = __popcll(smask), es = wave_sum(survivor ? cnt : 0);
-      if (lane == 0) {
-        if (vs) atomicAdd(&counts[0], static_cast<unsigned long long>(vs));
-        if (es) atomicAdd(&counts[1], static_cast<unsigned long long>(es));
+    acc.trav += alive0;
+    acc.removed |= removed;
+    acc.asym |= asym;
+    if (survivor) {
+      if (oa.nranks <= 1) {
+        acc.vs += 1;
+        acc.es += cnt;
+      } else {
+        acc_owner(s_hist, oa, u, cnt);
       }
-    } else if (survivor) {
-      const uint32_t r = owner_of(u, oa);
-      atomicAdd(&counts[2 * r], 1ull);
-      atomicAdd(&counts[2 * r + 1], static_cast<unsigned long long>(cnt));
     }
-    if (lane == 0 && sent) atomicAdd(trav, static_cast<unsigned long long>(sent));
   }
+  flush_block(acc, oa, s_hist, s_red, part);
 }
 
 // Counts of the current state (after token-passing post-processing).
-__global__ void k_count_state(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
-                              const uint16_t* __restrict__ tpub, const uint32_t* __restrict__ malive, OwnerArgs oa,
-                              unsigned long long* __restrict__ counts) {
+__global__ __launch_bounds__(kBlock) void k_count_state(const uint32_t* __restrict__ slist,
+                                                        const uint32_t* __restrict__ nSp,
+                                                        const uint16_t* __restrict__ tpub,
+                                                        const uint32_t* __restrict__ malive, OwnerArgs oa,
+                                                        unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+  BlockAcc acc;
   const uint32_t nS = *nSp;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS + 0ull;
        i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = slist[i];
     if (!tpub[u]) continue;
-    const uint32_t r = owner_of(u, oa);
-    atomicAdd(&counts[2 * r], 1ull);
-    atomicAdd(&counts[2 * r + 1], static_cast<unsigned long long>(malive[u]));
+    if (oa.nranks <= 1) {
+      acc.vs += 1;
+      acc.es += malive[u];
+    } else {
+      acc_owner(s_hist, oa, u, malive[u]);
+    }
   }
+  flush_block(acc, oa, s_hist, s_red, part);
 }
 
 // ---------------------------------------------------------------------------
@@ -422,34 +682,100 @@ void launch_degree_labels(Ctx& c) {
 
 void launch_label_match(Ctx& c) {
   hipLaunchKernelGGL(k_label_match, dim3(grid_for(c.n, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_labels, c.n,
-                     c.pa, c.d_tl);
+                     c.pa, c.d_tl, reinterpret_cast<unsigned long long*>(c.d_tlbits));
   PM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_lcc_first(Ctx& c, uint64_t* d_slot_counts, uint64_t* d_trav) {
+uint32_t slot_words(const Ctx& c) { return 2 * (c.nranks <= 1 ? 1 : c.nranks) + 4; }
+
+static void reduce_into(Ctx& c, unsigned grid, uint64_t* d_slot) {
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, c.stream,
+                     reinterpret_cast<const unsigned long long*>(c.d_part), grid, slot_words(c),
+                     reinterpret_cast<unsigned long long*>(d_slot));
+  PM_HIP_CHECK(hipGetLastError());
+}
+
+// variant: 0 = product (strip kernel); 1..7 = strip ablation MODE; 16+ = lane-per-row (MODE = variant-16)
+void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid) {
+#define PM_K1_ARGS                                                                                                 \
+  dim3(grid), dim3(kBlock), 0, c.stream, c.d_off, c.d_col, c.d_tl,                                                \
+      reinterpret_cast<const unsigned long long*>(c.d_tlbits), c.n, c.pa, owner_args(c), c.d_tst, c.d_tpub[c.cur], \
+      c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, reinterpret_cast<unsigned long long*>(c.d_cmask),                   \
+      reinterpret_cast<unsigned long long*>(c.d_part)
+  switch (variant) {
+    case 0: hipLaunchKernelGGL(k_lcc_first<0>, PM_K1_ARGS); break;
+    case 1: hipLaunchKernelGGL(k_lcc_first<1>, PM_K1_ARGS); break;
+    case 2: hipLaunchKernelGGL(k_lcc_first<2>, PM_K1_ARGS); break;
+    case 3: hipLaunchKernelGGL(k_lcc_first<3>, PM_K1_ARGS); break;
+    case 4: hipLaunchKernelGGL(k_lcc_first<4>, PM_K1_ARGS); break;
+    case 7: hipLaunchKernelGGL(k_lcc_first<7>, PM_K1_ARGS); break;
+    case 8: hipLaunchKernelGGL((k_lcc_first<0, 4>), PM_K1_ARGS); break;
+    case 9: hipLaunchKernelGGL((k_lcc_first<0, 16>), PM_K1_ARGS); break;
+    case 16: hipLaunchKernelGGL(k_lcc_first_lpr<0>, PM_K1_ARGS); break;
+    case 17: hipLaunchKernelGGL(k_lcc_first_lpr<1>, PM_K1_ARGS); break;
+    default: throw std::runtime_error("unknown superstep-0 kernel variant");
+  }
+#undef PM_K1_ARGS
+  PM_HIP_CHECK(hipGetLastError());
+}
+
+unsigned lcc_first_grid(const Ctx& c) {
+  return grid_for((c.n + kWave - 1) / kWave, kWpb, c.k1_resident_blocks ? c.k1_resident_blocks : kMaxGrid);
+}
+
+// Resident 256-thread blocks of the superstep-0 kernel on the whole chip
+// (occupancy query minus one block per CU: the API over-reports by one for
+// SGPR-heavy 256-thread kernels, MI355X_MICROARCH.md "Residency").
+unsigned query_k1_resident_blocks(int device) {
+  int per_cu = 0;
+  PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lcc_first<0>, kBlock, 0));
+  hipDeviceProp_t prop;
+  PM_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+  per_cu = std::max(1, per_cu - 1);
+  return static_cast<unsigned>(per_cu * prop.multiProcessorCount);
+}
+
+void launch_lcc_first(Ctx& c, uint64_t* d_slot) {
   const uint64_t chunks = (c.n + kWave - 1) / kWave;
-  hipLaunchKernelGGL(k_lcc_first, dim3(grid_for(chunks, kWpb, 16384)), dim3(kBlock), 0, c.stream, c.d_off, c.d_col,
-                     c.d_tl, c.n, c.pa, owner_args(c), c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mst, c.d_mlen,
-                     c.d_malive, c.d_slist, c.d_nS, c.d_flags,
-                     reinterpret_cast<unsigned long long*>(d_slot_counts), reinterpret_cast<unsigned long long*>(d_trav));
+  const unsigned grid = lcc_first_grid(c);
+  launch_lcc_first_kernel(c, 0, grid);
+  reduce_into(c, grid, d_slot);
+  // slist = survivors in id order
+  hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(
+      reinterpret_cast<const unsigned long long*>(c.d_cmask), PopcOp());
+  size_t tmp = c.scan_tmp_bytes;
+  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_cbase, static_cast<int>(chunks), c.stream));
+  hipLaunchKernelGGL(k_slist_write, dim3(grid_for(chunks, kBlock, 4096)), dim3(kBlock), 0, c.stream,
+                     reinterpret_cast<const unsigned long long*>(c.d_cmask), c.d_cbase, chunks, c.d_slist, c.d_nS);
   PM_HIP_CHECK(hipGetLastError());
 }
 
-void launch_lcc_step(Ctx& c, uint64_t* d_slot_counts, uint64_t* d_trav) {
+size_t slist_scan_tmp_bytes(uint64_t n) {
+  const uint64_t chunks = (n + kWave - 1) / kWave;
+  hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(nullptr, PopcOp());
+  size_t tmp = 0;
+  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, static_cast<uint64_t*>(nullptr),
+                                                static_cast<int>(std::max<uint64_t>(chunks, 1)), hipStream_t(0)));
+  return tmp;
+}
+
+void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
-  hipLaunchKernelGGL(k_lcc_step, dim3(grid_for(chunks, kWpb, 16384)), dim3(kBlock), 0, c.stream, c.d_off, c.d_slist,
-                     c.d_nS, c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mst,
-                     c.d_mlen, c.d_malive, c.d_flags, reinterpret_cast<unsigned long long*>(d_slot_counts),
-                     reinterpret_cast<unsigned long long*>(d_trav));
+  const unsigned grid = grid_for(chunks, kWpb, kMaxGrid);
+  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_off, c.d_slist, c.d_nS,
+                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mst, c.d_mlen,
+                     c.d_malive, reinterpret_cast<unsigned long long*>(c.d_part));
   PM_HIP_CHECK(hipGetLastError());
+  reduce_into(c, grid, d_slot);
   c.cur ^= 1;
 }
 
-void launch_count_state(Ctx& c, uint64_t* d_slot_counts) {
-  hipLaunchKernelGGL(k_count_state, dim3(grid_for(c.nS_host, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_slist,
-                     c.d_nS, c.d_tpub[c.cur], c.d_malive, owner_args(c),
-                     reinterpret_cast<unsigned long long*>(d_slot_counts));
+void launch_count_state(Ctx& c, uint64_t* d_slot) {
+  const unsigned grid = grid_for(c.nS_host, kBlock, kMaxGrid);
+  hipLaunchKernelGGL(k_count_state, dim3(grid), dim3(kBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tpub[c.cur],
+                     c.d_malive, owner_args(c), reinterpret_cast<unsigned long long*>(c.d_part));
   PM_HIP_CHECK(hipGetLastError());
+  reduce_into(c, grid, d_slot);
 }
 
 // ===========================================================================
@@ -484,21 +810,24 @@ __device__ __forceinline__ bool pos_ok(uint16_t T, int k, const LineArgs& la) {
 }
 
 // Source selection, nem_1.hpp:387-479 / tds_batch_1.hpp:1067-1135 (over S:
-// T_pub != 0 only for members of S).
-__global__ void k_tp_sources(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
-                             const uint16_t* __restrict__ tpub, LineArgs la, int tds, uint8_t* __restrict__ tsm,
-                             uint32_t* __restrict__ sources, unsigned long long* __restrict__ nsrc) {
-  const uint32_t nS = *nSp;
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS + 0ull;
-       i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t u = slist[i];
+// T_pub != 0 only for members of S).  Stream compaction of slist (hipcub).
+struct SourcePred {
+  const uint16_t* tpub;
+  LineArgs la;
+  int tds;
+  __device__ bool operator()(uint32_t u) const {
     const uint16_t T = tpub[u];
-    if (!T || !pos_ok(T, 0, la)) continue;
-    if (!tds && !la.VC && !((T >> la.ilast) & 1u)) continue;
-    tsm[u] = 1;
-    const unsigned long long p = atomicAdd(nsrc, 1ull);
-    sources[p] = u;
+    if (!T || !pos_ok(T, 0, la)) return false;
+    if (!tds && !la.VC && !((T >> la.ilast) & 1u)) return false;
+    return true;
   }
+};
+
+__global__ void k_mark_sources(const uint32_t* __restrict__ sources, const int* __restrict__ nsrc,
+                               uint8_t* __restrict__ tsm) {
+  const uint64_t n = static_cast<uint64_t>(*nsrc);
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    tsm[sources[i]] = 1;
 }
 
 // Number of alive entries of M[u] (excluding `skip`) -> outputs per item.
@@ -585,6 +914,7 @@ __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, con
                                   const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
                                   const uint32_t* __restrict__ malive, uint32_t* __restrict__ cnt,
                                   unsigned long long* __restrict__ trav) {
+  uint64_t t = 0;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nf; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = static_cast<uint32_t>(fk[i] & 0xFFFFFFFFull);
     const uint32_t x = fx[i];
@@ -593,8 +923,9 @@ __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, con
     for (uint64_t e = b; e < b + L; ++e)
       if ((mst[e] & 1u) && mcol[e] != x) ++c;
     cnt[i] = c;
-    atomicAdd(trav, static_cast<unsigned long long>(malive[u]));
+    t += malive[u];
   }
+  block_atomic_add(trav, t);
 }
 
 __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, const uint32_t* __restrict__ fx,
@@ -688,6 +1019,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive,
                              uint32_t* __restrict__ cnt, const uint64_t* __restrict__ obase,
                              uint32_t* __restrict__ wout, unsigned long long* __restrict__ trav) {
+  uint64_t t = 0;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nw; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t* w = win + i * stride;
     const uint32_t u = w[k];
@@ -717,10 +1049,11 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
         }
         ++c;
       }
-      if (!PASS) atomicAdd(trav, static_cast<unsigned long long>(malive[u]));
+      if (!PASS) t += malive[u];
     }
     if (!PASS) cnt[i] = c;
   }
+  if (!PASS) block_atomic_add(trav, t);
 }
 
 // Terminal position C+1 (tds_batch_1.hpp:641-758).
@@ -749,12 +1082,12 @@ __global__ void k_tds_terminal(const uint32_t* __restrict__ win, uint64_t nw, in
 
 // Post-processing of unacked sources (beta.cpp:964-1000).
 __global__ void k_tp_post(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint8_t* __restrict__ tsm,
-                          uint16_t* __restrict__ tpub, int i0, uint32_t* __restrict__ flags,
-                          unsigned long long* __restrict__ acked) {
+                          uint16_t* __restrict__ tpub, int i0, unsigned long long* __restrict__ out) {
+  uint64_t acked = 0, deleted = 0;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
     if (tsm[s] == 2) {
-      atomicAdd(acked, 1ull);
+      ++acked;
       continue;
     }
     uint16_t T = tpub[s];
@@ -763,8 +1096,10 @@ __global__ void k_tp_post(const uint32_t* __restrict__ sources, uint64_t nsrc, c
       T &= static_cast<uint16_t>(~(1u << i0));
       tpub[s] = T;  // T == 0: vertex_active = false and erased from the state map
     }
-    atomicOr(&flags[2], 1u);
+    ++deleted;
   }
+  block_atomic_add(&out[0], acked);
+  block_atomic_add(&out[1], deleted);
 }
 
 __global__ void k_clear_tsm(const uint32_t* __restrict__ sources, uint64_t nsrc, uint8_t* __restrict__ tsm) {
@@ -800,14 +1135,24 @@ static void ensure_sources(Ctx& c, const LineArgs& la, int tds, unsigned long lo
     hipLaunchKernelGGL(k_clear_tsm, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
                        c.nsources, c.d_tsm);
   }
-  PM_HIP_CHECK(hipMemsetAsync(d_nsrc, 0, sizeof(unsigned long long), c.stream));
-  hipLaunchKernelGGL(k_tp_sources, dim3(grid_for(c.nS_host, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_slist,
-                     c.d_nS, c.d_tpub[c.cur], la, tds, c.d_tsm, c.d_sources, d_nsrc);
-  PM_HIP_CHECK(hipGetLastError());
-  unsigned long long ns = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(&ns, d_nsrc, sizeof(ns), hipMemcpyDeviceToHost, c.stream));
+  (void)d_nsrc;
+  SourcePred pred{c.d_tpub[c.cur], la, tds};
+  int* d_ns = arena_alloc<int>(c, 1);
+  size_t tmp = 0;
+  const int nitems = static_cast<int>(std::max<uint32_t>(c.nS_host, 1));
+  PM_HIP_CHECK(hipMemsetAsync(d_ns, 0, sizeof(int), c.stream));
+  if (c.nS_host) {
+    PM_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
+    void* d_tmp = c.arena.get(tmp);
+    PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
+    hipLaunchKernelGGL(k_mark_sources, dim3(grid_for(c.nS_host, kBlock, 1024)), dim3(kBlock), 0, c.stream,
+                       c.d_sources, d_ns, c.d_tsm);
+    PM_HIP_CHECK(hipGetLastError());
+  }
+  int ns = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&ns, d_ns, sizeof(ns), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  c.nsources = ns;
+  c.nsources = static_cast<uint64_t>(ns);
 }
 
 TpResult run_path_line(Ctx& c, const NlcLine& line) {
@@ -840,7 +1185,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   const int C = la.C;
   for (int k = 1; k <= C && ntok > 0; ++k) {
     auto* keys = arena_alloc<unsigned long long>(c, ntok);
-    hipLaunchKernelGGL(k_tp_filter, dim3(grid_for(ntok, kBlock, 16384)), dim3(kBlock), 0, c.stream, tu, ts, ntok, k,
+    hipLaunchKernelGGL(k_tp_filter, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, ntok, k,
                        la, tpub, keys);
     auto* keys_s = arena_alloc<unsigned long long>(c, ntok);
     auto* par_s = arena_alloc<uint32_t>(c, ntok);
@@ -852,7 +1197,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
                                                     64, c.stream));
     auto* head = arena_alloc<uint8_t>(c, ntok);
     auto* excl = arena_alloc<uint32_t>(c, ntok);
-    hipLaunchKernelGGL(k_tp_unique, dim3(grid_for(ntok, kBlock, 16384)), dim3(kBlock), 0, c.stream, keys_s, par_s,
+    hipLaunchKernelGGL(k_tp_unique, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, keys_s, par_s,
                        ntok, seen, head, excl);
     // compact heads (stable: keeps keys sorted)
     auto* fk = arena_alloc<unsigned long long>(c, ntok);
@@ -877,21 +1222,21 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
       break;
     }
     auto* ecnt = arena_alloc<uint32_t>(c, nf);
-    hipLaunchKernelGGL(k_tp_expand_count, dim3(grid_for(nf, kBlock, 16384)), dim3(kBlock), 0, c.stream, fk, fx, nf,
+    hipLaunchKernelGGL(k_tp_expand_count, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf,
                        c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, ecnt, d_trav);
     auto* eb = arena_alloc<uint64_t>(c, nf + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, ecnt, eb, nf);
     tu = arena_alloc<uint32_t>(c, nnext);
     ts = arena_alloc<uint32_t>(c, nnext);
     tp = arena_alloc<uint32_t>(c, nnext);
-    hipLaunchKernelGGL(k_tp_expand_write, dim3(grid_for(nf, kBlock, 16384)), dim3(kBlock), 0, c.stream, fk, fx, nf, eb,
+    hipLaunchKernelGGL(k_tp_expand_write, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf, eb,
                        c.d_off, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
     PM_HIP_CHECK(hipGetLastError());
     ntok = nnext;
     res.tokens += ntok;
   }
   if (ntok > 0) {
-    hipLaunchKernelGGL(k_tp_terminal, dim3(grid_for(ntok, kBlock, 16384)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
+    hipLaunchKernelGGL(k_tp_terminal, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
                        la, tpub, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_tsm);
     PM_HIP_CHECK(hipGetLastError());
   }
@@ -932,14 +1277,14 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   res.tokens += nw;
   for (int k = 1; k <= C && nw > 0; ++k) {
     auto* wc = arena_alloc<uint32_t>(c, nw);
-    hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 16384)), dim3(kBlock), 0, c.stream, walks, nw, k,
+    hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
                        stride, la, tpub, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc,
                        static_cast<const uint64_t*>(nullptr), static_cast<uint32_t*>(nullptr), d_trav);
     auto* wb = arena_alloc<uint64_t>(c, nw + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
     auto* wn = arena_alloc<uint32_t>(c, nnext * stride);
     if (nnext) {
-      hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(nw, kBlock, 16384)), dim3(kBlock), 0, c.stream, walks, nw, k,
+      hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
                          stride, la, tpub, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
       PM_HIP_CHECK(hipGetLastError());
     }
@@ -949,7 +1294,7 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   }
   if (nw > 0) {
     auto* keep = arena_alloc<uint8_t>(c, nw);
-    hipLaunchKernelGGL(k_tds_terminal, dim3(grid_for(nw, kBlock, 16384)), dim3(kBlock), 0, c.stream, walks, nw, stride,
+    hipLaunchKernelGGL(k_tds_terminal, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, stride,
                        la, tpub, c.d_tsm, keep);
     PM_HIP_CHECK(hipGetLastError());
     std::vector<uint32_t> all(nw * stride);
@@ -970,16 +1315,16 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
 
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line) {
   if (c.nsources == 0) return 0;
-  auto* acked = arena_alloc<unsigned long long>(c, 1);
-  PM_HIP_CHECK(hipMemsetAsync(acked, 0, sizeof(unsigned long long), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(c.d_flags + 2, 0, sizeof(uint32_t), c.stream));
-  hipLaunchKernelGGL(k_tp_post, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, c.d_tsm, c.d_tpub[c.cur], static_cast<int>(line.indices[0]), c.d_flags, acked);
+  auto* out = arena_alloc<unsigned long long>(c, 2);
+  PM_HIP_CHECK(hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), c.stream));
+  hipLaunchKernelGGL(k_tp_post, dim3(grid_for(c.nsources, kBlock, 1024)), dim3(kBlock), 0, c.stream, c.d_sources,
+                     c.nsources, c.d_tsm, c.d_tpub[c.cur], static_cast<int>(line.indices[0]), out);
   PM_HIP_CHECK(hipGetLastError());
-  uint32_t deleted = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(&deleted, c.d_flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+  unsigned long long h[2] = {0, 0};
+  PM_HIP_CHECK(hipMemcpyAsync(h, out, sizeof(h), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  return deleted;
+  c.last_acked = h[0];
+  return h[1] ? 1u : 0u;
 }
 
 }  // namespace pm

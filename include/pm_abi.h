@@ -126,6 +126,10 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
 /* Parsed pattern directory as JSON text (host only; loader check). */
 int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen);
 
+/* Diagnostics: average time of `reps` launches of superstep-0 kernel variant
+ * (0 = product kernel; others are ablation builds used by tools/ubench.py). */
+int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out);
+
 /* Build info: returns the offload arch the kernels were compiled for ("gfx950"). */
 const char* pm_build_arch(void);
 
