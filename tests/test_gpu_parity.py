@@ -119,3 +119,26 @@ def test_iteration_cap_reports_non_termination(tmp_path):
     assert sg["iterations"] == so["iterations"] == 1
     assert sg["terminated"] == so["terminated"] == 0
     assert diffs == []
+
+
+def test_cli_end_to_end_matches_oracle(tmp_path):
+    import subprocess
+    binp = os.path.join(pmtest.ROOT, "fuzzypatternmatching_amd", "csrc", "tools", "bin")
+    base = str(tmp_path / "g")
+    assert subprocess.run([os.path.join(binp, "generate_rmat"), "-s", "12", "-n", "4", "-o", base]).returncode == 0
+    # -v label files (prefix matching: every file named lab.* in the directory)
+    g = pm.read_graph(base)
+    labels = pmtest.hash_labels(g.n, 8)
+    half = g.n // 2
+    with open(tmp_path / "lab.0", "w") as f:
+        f.write("".join(f"{v} {labels[v]}\n" for v in range(half)))
+    with open(tmp_path / "lab.1", "w") as f:
+        f.write("".join(f"{v} {labels[v]}\n" for v in range(half, g.n)))
+    out = tmp_path / "gpu"
+    out.mkdir()
+    r = subprocess.run([os.path.join(binp, "run_pattern_matching_beta"), "-i", base, "-v", str(tmp_path / "lab"),
+                        "-p", PATTERNS["cycle"], "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    ora = tmp_path / "oracle"
+    oracle.run(g.off, g.col, PATTERNS["cycle"], str(ora), labels=labels, nranks=4)
+    assert pmtest.compare_result_dirs(str(ora), str(out), 4) == []
