@@ -86,23 +86,27 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
     if (l.selected_vertices) throw std::runtime_error("pattern_nlc selected_vertices=1 is not supported yet");
   for (uint64_t v = 0; v < c->n; ++v)
     if (g->off[v + 1] - g->off[v] >= c->hub_threshold) c->hubs_host.push_back(v);
-  // device graph + state
+  // device graph + state; padded slot count (label independent)
+  c->nq = 0;
+  for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(g->off[v + 1] - g->off[v]);
   c->d_off = dalloc<uint64_t>(c->n + 1);
-  c->d_col = dalloc<uint32_t>(c->nnz);
+  c->d_offp = dalloc<uint64_t>(c->n + 1);
+  c->d_offr = dalloc<uint64_t>(c->n + 1);
+  c->d_colp = dalloc<uint32_t>(c->nq);
+  c->d_perm = dalloc<uint32_t>(c->n);
+  c->d_pos = dalloc<uint32_t>(c->n);
+  c->d_labs = dalloc<uint64_t>(c->n);
   PM_HIP_CHECK(hipMemcpy(c->d_off, g->off, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
-  PM_HIP_CHECK(hipMemcpy(c->d_col, g->col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
   if (!c->hubs_host.empty()) {
     c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
     PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   }
   c->d_labels = dalloc<uint64_t>(c->n);
-  c->d_tl = dalloc<uint16_t>(c->n);
-  c->d_tlbits = dalloc<uint64_t>((c->n + 63) / 64 + 1);
   c->d_tpub[0] = dalloc<uint16_t>(c->n);
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
-  c->d_mcol = dalloc<uint32_t>(c->nnz);
-  c->d_mst = dalloc<uint8_t>(c->nnz);
+  c->d_mcol = dalloc<uint32_t>(c->nq);
+  c->d_mst = dalloc<uint8_t>(c->nq);
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
   c->d_slist = dalloc<uint32_t>(c->n);
@@ -112,24 +116,20 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   c->d_tsm = dalloc<uint8_t>(c->n);
   if (c->nranks > 64) throw std::runtime_error("more than 64 ranks for result-file attribution");
   c->d_part = dalloc<uint64_t>(uint64_t(kPartGridMax) * slot_words(*c));
-  {
-    const uint64_t chunks = (c->n + 63) / 64;
-    c->d_cmask = dalloc<uint64_t>(chunks + 1);
-    c->d_cbase = dalloc<uint64_t>(chunks + 1);
-    c->scan_tmp_bytes = slist_scan_tmp_bytes(c->n);
-    c->d_scan_tmp = dalloc<char>(c->scan_tmp_bytes);
-  }
   size_t free_b = 0, total_b = 0;
   PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
   size_t arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
   arena = std::max<size_t>(arena, size_t(64) << 20);
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
-  c->k1_resident_blocks = query_k1_resident_blocks(device);
-  // default labels = degree labels
+  // default labels = degree labels; the id-major adjacency is staged in the
+  // M column buffer and permuted into the label-major d_colp
+  PM_HIP_CHECK(hipMemcpy(c->d_mcol, g->col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
   launch_degree_labels(*c);
   c->labels_host.assign(c->n, 0);
   for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(g->off[v + 1] - g->off[v]);
+  build_label_layout(*c, c->d_mcol, false, c->d_colp);
+  build_tiling(*c);
   PM_HIP_CHECK(hipStreamSynchronize(c->stream));
   return c.release();
 }
@@ -137,13 +137,23 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
 static void destroy_ctx(pm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_off, c->d_col, c->d_labels, c->d_hubs, c->d_tl, c->d_tlbits, c->d_tpub[0], c->d_tpub[1], c->d_tst,
-                  c->d_mcol, c->d_mst, c->d_mlen, c->d_malive, c->d_slist, c->d_sources, c->d_nS, c->d_flags,
-                  c->d_tsm, c->d_counts, c->d_part, c->d_cmask, c->d_cbase, c->d_scan_tmp, c->arena.base};
+  void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
+                  c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
+                  c->d_mst, c->d_mlen, c->d_malive, c->d_slist, c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
+                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// New labels: rebuild the label-major layout from the current one (the M
+// column buffer is free between searches and receives the new adjacency).
+static void relayout(Ctx& c) {
+  build_label_layout(c, c.d_colp, true, c.d_mcol);
+  std::swap(c.d_colp, c.d_mcol);
+  build_tiling(c);
+  c.lcc_started = false;
 }
 
 static void reset_state(Ctx& c) {
@@ -189,7 +199,6 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
-      launch_label_match(c);
       PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
       PM_HIP_CHECK(hipEventCreate(&k_beg));
       PM_HIP_CHECK(hipEventCreate(&k_end));
@@ -220,7 +229,12 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     out.vcount.push_back(vc);
     out.ecount.push_back(ec);
     out.trav.push_back(h[2 * P]);
-    if (ss == 0 && init_step) out.matching_rows = h[2 * P + 1];
+    if (ss == 0 && init_step) {
+      // superstep 0 visits only label-matching rows; their adjacency size is
+      // a property of the layout (build_tiling), identical to the reference's count
+      out.trav.back() = c.ss0_trav;
+      out.matching_rows = c.ss0_rows;
+    }
     if (h[2 * P + 2]) out.not_finished = true;
     if (h[2 * P + 3]) asym = true;
     float ms = 0.f;
@@ -244,12 +258,13 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
 }
 
 // Algorithmic bytes of the fused superstep-0 kernel (roofline):
-// every vertex: Tl (2 B) ; matching rows: 2 offsets (16 B) + per entry 4 B id
-// + 2 B Tl gather + 1 B edge state ; survivors: T_state/T_pub/mlen/malive/slist (16 B)
-// + 4 B per distinct contributing neighbour written.
+// matching rows: row offset (8 B); per scanned entry: 4 B neighbour id + 2 B
+// Tl gather; survivors: perm (4 B) + T_state, T_pub (2+2 B) + mlen, malive
+// (4+4 B); per distinct contributing neighbour: 4 B id + 1 B state written.
 static uint64_t lcc_first_bytes(const Ctx& c, uint64_t scanned, uint64_t survivors, uint64_t edges,
                                 uint64_t matching_rows) {
-  return c.n * 2 + matching_rows * 16 + scanned * (4 + 2) + survivors * 16 + edges * (4 + 1);
+  (void)c;
+  return matching_rows * 8 + scanned * (4 + 2) + survivors * 16 + edges * (4 + 1);
 }
 
 struct DriverFiles {
@@ -293,35 +308,43 @@ static uint32_t owner_host(const Ctx& c, uint64_t v) {
   return static_cast<uint32_t>(v % c.nranks);
 }
 
+// State by vertex id: T_pub, |M[v]| and the alive M entries (neighbour ids,
+// rows in vertex-id order, entries in the row's id order).
 static void export_state(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32_t>& mdeg,
                          std::vector<uint32_t>& nbrs) {
-  tpub.resize(c.n);
-  PM_HIP_CHECK(hipMemcpy(tpub.data(), c.d_tpub[c.cur], c.n * sizeof(uint16_t), hipMemcpyDeviceToHost));
-  std::vector<uint32_t> mlen(c.n), malive(c.n);
-  PM_HIP_CHECK(hipMemcpy(mlen.data(), c.d_mlen, c.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  PM_HIP_CHECK(hipMemcpy(malive.data(), c.d_malive, c.n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  std::vector<uint64_t> off(c.n + 1);
-  PM_HIP_CHECK(hipMemcpy(off.data(), c.d_off, (c.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  mdeg.assign(c.n, 0);
+  const uint64_t n = c.n;
+  std::vector<uint16_t> tp(n);
+  std::vector<uint32_t> mlen(n), malive(n);
+  std::vector<uint64_t> off(n + 1);
+  PM_HIP_CHECK(hipMemcpy(tp.data(), c.d_tpub[c.cur], n * sizeof(uint16_t), hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(mlen.data(), c.d_mlen, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(malive.data(), c.d_malive, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(off.data(), c.d_offp, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> pos(n);
+  for (uint64_t i = 0; i < n; ++i) pos[c.perm_host[i]] = static_cast<uint32_t>(i);
+  tpub.assign(n, 0);
+  mdeg.assign(n, 0);
   nbrs.clear();
   std::vector<uint32_t> rowc;
   std::vector<uint8_t> rows;
-  for (uint64_t v = 0; v < c.n; ++v) {
-    if (!tpub[v]) continue;
-    mdeg[v] = malive[v];
-    const uint32_t L = mlen[v];
+  for (uint64_t v = 0; v < n; ++v) {
+    const uint32_t p = pos[v];
+    if (!tp[p]) continue;
+    tpub[v] = tp[p];
+    mdeg[v] = malive[p];
+    const uint32_t L = mlen[p];
     if (!L) continue;
     rowc.resize(L);
     rows.resize(L);
-    PM_HIP_CHECK(hipMemcpy(rowc.data(), c.d_mcol + off[v], L * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    PM_HIP_CHECK(hipMemcpy(rows.data(), c.d_mst + off[v], L, hipMemcpyDeviceToHost));
+    PM_HIP_CHECK(hipMemcpy(rowc.data(), c.d_mcol + off[p], L * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    PM_HIP_CHECK(hipMemcpy(rows.data(), c.d_mst + off[p], L, hipMemcpyDeviceToHost));
     uint32_t k = 0;
     for (uint32_t i = 0; i < L; ++i)
       if (rows[i] & 1u) {
-        nbrs.push_back(rowc[i]);
+        nbrs.push_back(c.perm_host[rowc[i]]);
         ++k;
       }
-    if (k != malive[v]) throw std::runtime_error("internal: alive count mismatch in export");
+    if (k != malive[p]) throw std::runtime_error("internal: alive count mismatch in export");
   }
 }
 
@@ -402,11 +425,11 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           s.tds_edges += tr.edges;
           s.walks = tr.walks;
           for (uint64_t i = 0; i < tr.walks; ++i) {
-            const uint32_t* w = walks.data() + i * stride;
-            const uint32_t last = w[stride - 1];
+            const uint32_t* w = walks.data() + i * stride;  // positions
+            const uint32_t last = c.perm_host[w[stride - 1]];
             const uint32_t r = owner_host(c, last);
             std::string l = "[" + std::to_string(r) + "], ";
-            for (uint32_t p = 0; p < stride; ++p) l += std::to_string(w[p]) + ", ";
+            for (uint32_t p = 0; p < stride; ++p) l += std::to_string(c.perm_host[w[p]]) + ", ";
             l += "[" + std::to_string(last) + "]";
             subgraphs[pl][r].push_back(std::move(l));
           }
@@ -530,6 +553,7 @@ int pm_vertex_data_degree(pm_ctx* ctx) {
     PM_HIP_CHECK(hipMemcpy(off.data(), ctx->d_off, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (uint64_t v = 0; v < ctx->n; ++v) ctx->labels_host[v] = pm::degree_label(off[v + 1] - off[v]);
     PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    pm::relayout(*ctx);
   });
 }
 
@@ -538,14 +562,13 @@ int pm_vertex_data_set(pm_ctx* ctx, const uint64_t* labels) {
     if (!labels) throw std::runtime_error("null labels");
     ctx->labels_host.assign(labels, labels + ctx->n);
     PM_HIP_CHECK(hipMemcpy(ctx->d_labels, labels, ctx->n * sizeof(uint64_t), hipMemcpyHostToDevice));
+    pm::relayout(*ctx);
   });
 }
 
 int pm_reset(pm_ctx* ctx) {
   PM_API_BODY(ctx, {
     pm::reset_state(*ctx);
-    pm::launch_label_match(*ctx);
-    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   });
 }
 
@@ -666,22 +689,22 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
 
 const char* pm_build_arch(void) { return "gfx950"; }
 
-// Diagnostics: times `reps` launches of a superstep-0 kernel variant on the
-// current labels (state is reset first; variants != 0 produce wrong output).
+// Diagnostics: times `reps` launches of the superstep-0 kernel on the current
+// labels (state is reset first).  variant < 16: diagnostic MODE of the
+// kernel on the default grid; variant >= 16: the product kernel on a grid of
+// `variant` blocks.
 int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
   PM_API_BODY(ctx, {
     pm::reset_state(*ctx);
-    pm::launch_label_match(*ctx);
     hipEvent_t a, b;
     PM_HIP_CHECK(hipEventCreate(&a));
     PM_HIP_CHECK(hipEventCreate(&b));
-    // variant >= 100: same kernel (variant - 100) with one 64-vertex chunk per wave
-    const unsigned grid = variant >= 100 ? static_cast<unsigned>(std::min<uint64_t>((ctx->n + 255) / 256, 1u << 20))
-                                         : pm::lcc_first_grid(*ctx);
-    if (variant >= 100) variant -= 100;
-    pm::launch_lcc_first_kernel(*ctx, variant, grid);  // warm
+    const unsigned grid = variant >= 16 ? std::min<unsigned>(static_cast<unsigned>(variant), pm::kPartGridMax)
+                                        : ctx->k1_grid;
+    const int mode = variant >= 16 ? 0 : variant;
+    pm::launch_lcc_first_kernel(*ctx, mode, grid);  // warm
     PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
-    for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, variant, grid);
+    for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, mode, grid);
     PM_HIP_CHECK(hipEventRecord(b, ctx->stream));
     PM_HIP_CHECK(hipEventSynchronize(b));
     float ms = 0.f;

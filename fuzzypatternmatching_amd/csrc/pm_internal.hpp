@@ -27,10 +27,20 @@ struct PatArgs {
 };
 
 // Per-rank counter attribution (owner rule of delegate_partitioned_graph).
+// Device state is indexed by label-major position; perm maps back to ids.
 struct OwnerArgs {
   const uint64_t* hubs;  // sorted hub ids (device), may be null
+  const uint32_t* perm;  // position -> vertex id
   uint32_t nhubs;
   uint32_t nranks;
+};
+
+// Position runs of the pattern's distinct labels in the label-major order:
+// a vertex at position p carries template bits tu[l] iff lo[l] <= p < hi[l].
+struct LabelRuns {
+  uint32_t lo[16], len[16];
+  uint16_t tu[16];
+  int32_t n;
 };
 
 // NLC line constants for the token-passing kernels.
@@ -57,6 +67,46 @@ struct Arena {
   void reset() { used = 0; }
 };
 
+// Superstep-0 tiling of the padded label-major CSR (DESIGN.md "Data
+// layout"): one entry per (pattern label, degree class) run of rows.  kind
+// 0..10: rows of degree in (G/2, G], G = 1 << kind, stored in G padded slots,
+// so the run is a dense rows x G array and a tile is kTileEntries (G for
+// G > kTileEntries) consecutive slots; kind 11: rows above kHeavyDeg (stored
+// unpadded), one kHeavyDeg-entry segment per tile (HSeg list).
+struct KRange {
+  uint64_t qbase;       // first slot of the run
+  uint32_t tile0;       // first tile of the run
+  uint32_t start, end;  // row positions [start, end)
+  uint32_t aux;         // kind 11: first HSeg index
+  uint16_t tu, nm;      // template bits of the label and their neighbour mask
+  uint32_t kind;
+  // label runs whose template bits meet nm (the only neighbours that can
+  // contribute), first four inline (len 0 = unused); nrel > 4 adds a scan of
+  // all LabelRuns
+  uint32_t rlo[4], rlen[4];
+  uint16_t rtu[4];
+  uint32_t nrel;
+};
+struct HSeg {
+  uint32_t row;   // row position
+  uint32_t seg;   // segment index inside the row
+  uint32_t h;     // heavy-row ordinal (scratch slot)
+  uint32_t nseg;  // segments of the row
+};
+static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
+static constexpr uint32_t kTileEntries = 64 * kSub; // 512
+static constexpr uint32_t kHeavyDeg = 1024;
+static constexpr int kHeavyKind = 11;
+static constexpr int kMaxRanges = 16 * 12 + 1;
+// Padded row length: nextpow2(degree) up to kHeavyDeg, the degree above.
+__host__ __device__ inline uint64_t padded_degree(uint64_t d) {
+  if (d <= 1) return d;
+  if (d > kHeavyDeg) return d;
+  uint64_t g = 1;
+  while (g < d) g <<= 1;
+  return g;
+}
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -68,20 +118,40 @@ struct Ctx {
   Pattern pattern;
   PatArgs pa{};
 
-  // graph (device)
-  uint64_t* d_off = nullptr;
-  uint32_t* d_col = nullptr;
-  uint64_t* d_labels = nullptr;
+  // graph (device), renumbered label-major whenever the labels change:
+  // vertex positions ordered by (label, degree, id); every device array below
+  // is indexed by position and the adjacency holds neighbour positions (each
+  // row keeps the id order of the input, so duplicates stay adjacent).
+  uint64_t* d_off = nullptr;      // id-major offsets (degrees), V+1
+  uint64_t nq = 0;                // padded slots (label independent)
+  uint64_t* d_offp = nullptr;     // label-major padded row starts, V+1
+  uint64_t* d_offr = nullptr;     // label-major unpadded offsets (degree sums), V+1
+  uint32_t* d_colp = nullptr;     // padded adjacency (neighbour positions, kNone pad), nq
+  uint32_t* d_perm = nullptr;     // position -> vertex id
+  uint32_t* d_pos = nullptr;      // vertex id -> position
+  uint64_t* d_labs = nullptr;     // labels in position order
+  std::vector<uint32_t> perm_host;
+  LabelRuns lr{};
+  uint64_t* d_labels = nullptr;   // labels by vertex id
   uint64_t* d_hubs = nullptr;
   std::vector<uint64_t> labels_host;  // for result files
 
-  // vertex state (device)
-  uint16_t* d_tl = nullptr;       // template bits matching the vertex label
-  uint64_t* d_tlbits = nullptr;   // 1 bit per vertex: tl != 0
+  // superstep-0 tiling for the current labels and pattern
+  std::vector<KRange> ktab;
+  KRange* d_ktab = nullptr;
+  uint32_t ntiles = 0;
+  bool k1_wide = false;           // some range has more than four relevant label runs
+  HSeg* d_hseg = nullptr;
+  uint32_t nheavy = 0;            // heavy rows (scratch slots)
+  uint32_t* d_hscr = nullptr;     // 3 x nheavy: TN, distinct count, segments done
+  uint64_t ss0_trav = 0;          // adjacency entries of label-matching rows
+  uint64_t ss0_rows = 0;          // label-matching rows with degree > 0
+
+  // vertex state (device, by position)
   uint16_t* d_tpub[2] = {nullptr, nullptr};  // template_vertices (T_pub), 0 = not in S
   int cur = 0;
   uint16_t* d_tst = nullptr;      // vertex_state.template_vertices (T_state)
-  uint32_t* d_mcol = nullptr;     // active-edge rows, stored at the vertex's CSR offset
+  uint32_t* d_mcol = nullptr;     // active-edge rows (neighbour positions) at the vertex's row start, nq
   uint8_t* d_mst = nullptr;       // per entry: bit0 alive, bit1 flag (cycle mark)
   uint32_t* d_mlen = nullptr;     // entries written in the row (alive or dead)
   uint32_t* d_malive = nullptr;   // |M[v]|
@@ -89,13 +159,14 @@ struct Ctx {
   uint32_t* d_nS = nullptr;       // device count of d_slist
   uint32_t* d_flags = nullptr;    // [0] not_finished, [1] asymmetric edge state, [2] deleted
   uint64_t* d_counts = nullptr;   // per-slot per-rank counts (vertices, edges) + traversed
-  uint64_t* d_part = nullptr;     // per-block counter partials (kMaxGrid x slot_words)
-  uint64_t* d_cmask = nullptr;    // superstep-0 survivor mask per 64-vertex chunk
-  uint64_t* d_cbase = nullptr;    // exclusive scan of the chunk popcounts
+  uint64_t* d_part = nullptr;     // per-block counter partials (kPartGridMax x slot_words)
+  uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile
+  uint64_t* d_tbase = nullptr;    // exclusive scan of the mask popcounts
   void* d_scan_tmp = nullptr;     // hipcub scan workspace for the slist build
   size_t scan_tmp_bytes = 0;
+  uint64_t tmask_words = 0;
   uint64_t last_acked = 0;
-  unsigned k1_resident_blocks = 0;
+  unsigned k1_grid = 0;
   uint8_t* d_tsm = nullptr;       // token source map: 0 none, 1 unacked source, 2 acked
   size_t counts_slots = 0;
 
@@ -119,17 +190,21 @@ struct Ctx {
 
 // Kernel launchers (pm_kernels.hip).
 void launch_degree_labels(Ctx& c);
-void launch_label_match(Ctx& c);
+// Label-major layout: sorts the vertices by (label, degree, id) and writes the
+// renumbered adjacency into dst (E entries).  src_col holds neighbour ids at
+// src_start[id] (the id-major input), or, when relabelling, is the current
+// d_colp (neighbour positions, translated in place first).
+void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst);
+void build_tiling(Ctx& c);
 // Counter slots: W = slot_words(c) u64 = [vertices per rank | edges per rank |
 // traversed | matching rows | removed flag | asymmetry flag].
 uint32_t slot_words(const Ctx& c);
 void launch_lcc_first(Ctx& c, uint64_t* d_slot);
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid);  // variant != 0: ablation builds
 unsigned lcc_first_grid(const Ctx& c);
-unsigned query_k1_resident_blocks(int device);
 void launch_lcc_step(Ctx& c, uint64_t* d_slot);
 void launch_count_state(Ctx& c, uint64_t* d_slot);
-size_t slist_scan_tmp_bytes(uint64_t n);
+size_t slist_scan_tmp_bytes(uint64_t words);
 static constexpr unsigned kPartGridMax = 2048;
 
 struct TpResult {

@@ -1,23 +1,25 @@
 // HIP kernels (gfx950 / CDNA4) for the label-constrained pattern-matching path.
 //
-// Layout in HBM (see DESIGN.md "Data layout"):
-//   off[V+1] u64, col[E] u32      CSR, rows sorted by target (duplicates adjacent)
-//   tl[V] u16                     template bits whose label equals the vertex label
+// Layout in HBM (see DESIGN.md "Data layout").  Vertices are renumbered
+// label-major when the labels are loaded: position order = (label, degree,
+// id), so every pattern label owns one contiguous run of positions and the
+// template bits of a neighbour follow from its position alone (LabelRuns).
+//   offp[V+1] u64, colp[E] u32    CSR by position; entries are neighbour
+//                                 positions, each row in input (id) order so
+//                                 duplicates stay adjacent
+//   perm[V], pos[V] u32           position <-> vertex id (output, owner rule)
 //   tpub[2][V] u16                template_vertices (T_pub), ping-pong per superstep;
 //                                 0 <=> vertex not in the state map S
 //   tst[V] u16                    vertex_state.template_vertices (T_state)
 //   mcol[E] u32, mst[E] u8        active-edge map M[v], stored in v's own CSR slot
-//                                 [off[v], off[v]+mlen[v]) so no prefix scan is needed;
+//                                 [offp[v], offp[v]+mlen[v]) so no prefix scan is needed;
 //                                 mst bit0 = alive, bit1 = edge flag
 //   mlen[V], malive[V] u32        written length / alive count of M[v]
-//   slist[nS] u32                 vertices that entered S in superstep 0 (S only shrinks)
+//   slist[nS] u32                 positions that entered S in superstep 0 (S only shrinks)
 //
-// Every LCC kernel is row-per-lane scheduled through "strips": a wave owns 64
-// consecutive rows (vertices or slist entries), prefix-sums their lengths and
-// then walks the concatenated entries 64 at a time, one entry per lane, so the
-// adjacency reads are coalesced regardless of degree; per-row OR / count
-// reductions are segmented wave scans (no LDS or global atomics per entry).
-// This is an irregular gather: no MFMA (north_star).
+// Superstep 0 (k_lcc_first) visits only the label-matching runs, tiled by
+// degree class; later supersteps (k_lcc_step) are row-per-lane scheduled
+// through "strips" over M.  Irregular integer work: no MFMA (north_star).
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -34,7 +36,7 @@ static constexpr int kBlock = 256;
 static constexpr int kWpb = kBlock / kWave;
 static constexpr uint32_t kNone = 0xFFFFFFFFu;
 static constexpr unsigned kMaxGrid = 1024;  // persistent-style grids: 4 blocks per CU
-static constexpr int kU = 8;                // strip unroll: independent loads in flight per lane
+static constexpr int kU = 8;                // K2 strip unroll: independent loads in flight per lane
 
 struct PopcOp {
   __host__ __device__ uint64_t operator()(unsigned long long m) const {
@@ -46,11 +48,17 @@ struct PopcOp {
 // helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
-__device__ __forceinline__ uint16_t nbr_mask(uint16_t T, const PatArgs& pa) {
+// Template adjacency is read from an LDS copy (s_adj): a kernel-argument
+// array indexed at run time compiles to a scalar memory load per access.
+__device__ __forceinline__ void load_adj(uint16_t* s_adj, const PatArgs& pa) {
+  if (threadIdx.x < 16) s_adj[threadIdx.x] = pa.adj[threadIdx.x];
+}
+
+__device__ __forceinline__ uint16_t nbr_mask(uint16_t T, const uint16_t* adj) {
   uint16_t m = 0;
   while (T) {
     const int t = __ffs(static_cast<int>(T)) - 1;
-    m |= pa.adj[t];
+    m |= adj[t];
     T &= static_cast<uint16_t>(T - 1);
   }
   return m;
@@ -58,19 +66,21 @@ __device__ __forceinline__ uint16_t nbr_mask(uint16_t T, const PatArgs& pa) {
 
 // global verify_and_update_vertex_state bit test (nonunique_ee.hpp:901-939):
 // keep bit t iff adj[t] != 0 and adj[t] is a subset of TN.
-__device__ __forceinline__ uint16_t keep_bits(uint16_t T, uint16_t TN, const PatArgs& pa) {
+__device__ __forceinline__ uint16_t keep_bits(uint16_t T, uint16_t TN, const uint16_t* adj) {
   uint16_t out = T, x = T;
   while (x) {
     const int t = __ffs(static_cast<int>(x)) - 1;
     x &= static_cast<uint16_t>(x - 1);
-    const uint16_t a = pa.adj[t];
+    const uint16_t a = adj[t];
     if (a == 0 || (a & static_cast<uint16_t>(~TN))) out &= static_cast<uint16_t>(~(1u << t));
   }
   return out;
 }
 
-__device__ __forceinline__ uint32_t owner_of(uint64_t v, const OwnerArgs& oa) {
+// Owner rank of the vertex at position p.
+__device__ __forceinline__ uint32_t owner_of(uint64_t p, const OwnerArgs& oa) {
   if (oa.nranks <= 1) return 0;
+  const uint64_t v = oa.perm[p];
   if (oa.nhubs) {
     uint32_t lo = 0, hi = oa.nhubs;
     while (lo < hi) {
@@ -192,16 +202,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce_partials(const unsigned long 
   }
 }
 
-// Last row r (0..63) of a wave's strip space whose start <= j.
-__device__ __forceinline__ int find_row(const uint64_t* rs, uint64_t j) {
-  int lo = 0, hi = kWave - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (rs[mid] <= j) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
 // ---------------------------------------------------------------------------
 // K0: labels.
 // vertex_data_db_degree.hpp:109  label = ceil(log2(degree + 1)) == bit_width(degree)
@@ -212,27 +212,111 @@ __global__ void k_degree_labels(const uint64_t* __restrict__ off, uint64_t n, ui
   }
 }
 
-// lppm_visitor::visit first-superstep label match (nonunique_ee.hpp:523-537).
-// Also writes a 1-bit-per-vertex "matches some template" bitmap: superstep 0
-// probes it before gathering Tl (V/8 bytes stay L2-resident, and only a
-// minority of scanned entries point at matching vertices on R-MAT).
-__global__ void k_label_match(const uint64_t* __restrict__ labels, uint64_t n, PatArgs pa, uint16_t* __restrict__ tl,
-                              unsigned long long* __restrict__ tlbits) {
-  const uint64_t nwords = (n + kWave - 1) / kWave;
+// ---------------------------------------------------------------------------
+// Label-major padded layout (built when the labels change, outside any search).
+//
+// Vertices are stably sorted by (label, degree); rows of degree <= kHeavyDeg
+// get padded_degree() slots (kNone fill), so every (label, degree class) run
+// is a dense rows x G array whose slot addresses follow from the tile index
+// alone: superstep 0 needs no row-offset loads, one round trip per tile.
+__global__ void k_layout_keys(const uint64_t* __restrict__ off, uint64_t n, uint32_t* __restrict__ dkey,
+                              uint32_t* __restrict__ ids) {
+  for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < n; v += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t d = off[v + 1] - off[v];
+    dkey[v] = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
+    ids[v] = static_cast<uint32_t>(v);
+  }
+}
+
+__global__ void k_gather_labels(const uint64_t* __restrict__ labels, const uint32_t* __restrict__ ids, uint64_t n,
+                                uint64_t* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    out[i] = labels[ids[i]];
+}
+
+// Degrees in position order: padded (pad) and real (real).
+__global__ void k_perm_degrees(const uint64_t* __restrict__ off, const uint32_t* __restrict__ perm, uint64_t n,
+                               uint64_t* __restrict__ pad, uint64_t* __restrict__ real) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t u = perm[i];
+    const uint64_t d = off[u + 1] - off[u];
+    pad[i] = padded_degree(d);
+    real[i] = d;
+  }
+}
+
+__global__ void k_inverse_perm(const uint32_t* __restrict__ perm, uint64_t n, uint32_t* __restrict__ pos) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    pos[perm[i]] = static_cast<uint32_t>(i);
+}
+
+// Relabel, step 1: row starts by vertex id of the current layout, and the
+// adjacency translated back to ids in place (padding stays kNone).
+__global__ void k_row_starts_by_id(const uint64_t* __restrict__ offp, const uint32_t* __restrict__ perm, uint64_t n,
+                                   uint64_t* __restrict__ start) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    start[perm[i]] = offp[i];
+}
+
+__global__ void k_to_ids(uint32_t* __restrict__ col, uint64_t nq, const uint32_t* __restrict__ perm) {
+  for (uint64_t e = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; e < nq; e += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t x = col[e];
+    if (x != kNone) col[e] = perm[x];
+  }
+}
+
+// One wave per destination row: slot j < degree gets pos[src[src_start[id] + j]],
+// the padding kNone.
+__global__ __launch_bounds__(kBlock) void k_copy_rows(const uint32_t* __restrict__ src,
+                                                      const uint64_t* __restrict__ src_start,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint64_t* __restrict__ offp,
+                                                      const uint32_t* __restrict__ perm,
+                                                      const uint32_t* __restrict__ pos, uint64_t n,
+                                                      uint32_t* __restrict__ dst) {
   const int lane = lane_id();
-  const uint64_t wave = (blockIdx.x * uint64_t(blockDim.x) + threadIdx.x) / kWave;
-  const uint64_t nwaves = uint64_t(gridDim.x) * blockDim.x / kWave;
-  for (uint64_t wd = wave; wd < nwords; wd += nwaves) {
-    const uint64_t v = wd * kWave + lane;
-    uint16_t t = 0;
-    if (v < n) {
-      const uint64_t lab = labels[v];
-      for (int i = 0; i < pa.K; ++i)
-        if (pa.plabel[i] == lab) t |= static_cast<uint16_t>(1u << i);
-      tl[v] = t;
+  const uint64_t nw = uint64_t(gridDim.x) * kWpb;
+  for (uint64_t i = blockIdx.x * uint64_t(kWpb) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave); i < n; i += nw) {
+    const uint64_t d0 = offp[i], slots = offp[i + 1] - d0;
+    const uint32_t u = perm[i];
+    const uint64_t deg = off[u + 1] - off[u];
+    const uint64_t s0 = src_start[u];
+    for (uint64_t j = lane; j < slots; j += kWave) dst[d0 + j] = j < deg ? pos[src[s0 + j]] : kNone;
+  }
+}
+
+// Run boundaries for the pattern's distinct labels: out[l*kLB + 0] = first
+// position with the label, [1 + k] = first position with padded degree >=
+// 1 << k (k = 0..10), [12] = first with degree > kHeavyDeg, [13] = one past
+// the last position with the label.
+static constexpr int kLB = 14;
+__global__ void k_label_bounds(const uint64_t* __restrict__ labs, const uint64_t* __restrict__ offp, uint64_t n,
+                               const uint64_t* __restrict__ want, int nl, uint64_t* __restrict__ out) {
+  const int l = threadIdx.x;
+  if (l >= nl) return;
+  const uint64_t L = want[l];
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (labs[m] < L) lo = m + 1; else hi = m;
+  }
+  const uint64_t a = lo;
+  hi = n;
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (labs[m] <= L) lo = m + 1; else hi = m;
+  }
+  const uint64_t b = lo;
+  out[l * kLB + 0] = a;
+  out[l * kLB + 13] = b;
+  for (int k = 0; k <= 11; ++k) {
+    const uint64_t th = k <= 10 ? (1ull << k) : uint64_t(kHeavyDeg) + 1;
+    uint64_t x = a, y = b;
+    while (x < y) {
+      const uint64_t m = (x + y) >> 1;
+      if (offp[m + 1] - offp[m] < th) x = m + 1; else y = m;
     }
-    const unsigned long long m = __ballot(t != 0);
-    if (lane == 0) tlbits[wd] = m;
+    out[l * kLB + 1 + k] = x;
   }
 }
 
@@ -247,259 +331,357 @@ __global__ void k_label_match(const uint64_t* __restrict__ labels, uint64_t n, P
 //   TN(u) = OR of contributing Tl(v); u in S iff TN(u) != 0;
 //   M[u]  = distinct contributing v (first occurrence in the sorted row);
 //   T_state = keep_bits(Tl(u), TN); empty -> removed (sets not_finished).
-// Survivors get T_pub = T_state, |M[u]| and a slot in slist.
-// MODE (ablation only, 0 in the product): bit0 skips the M writes, bit1 the
-// bitmap/Tl gathers, bit2 the segmented scans (diagnostic builds, wrong output).
-template <int MODE, int KU = kU>
-__global__ __launch_bounds__(kBlock) void k_lcc_first(
-    const uint64_t* __restrict__ off, const uint32_t* __restrict__ col, const uint16_t* __restrict__ tl,
-    const unsigned long long* __restrict__ tlbits, uint64_t n, PatArgs pa, OwnerArgs oa, uint16_t* __restrict__ tst, uint16_t* __restrict__ tpub,
-    uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst, uint32_t* __restrict__ mlen,
-    uint32_t* __restrict__ malive, unsigned long long* __restrict__ cmask, unsigned long long* __restrict__ part) {
-  __shared__ unsigned long long s_hist[2 * kMaxRanks];
-  __shared__ unsigned long long s_red[kWpb * 6];
-  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
-  __syncthreads();
-  BlockAcc acc;
-  __shared__ uint64_t s_rs[kWpb][kWave];
-  __shared__ uint64_t s_beg[kWpb][kWave];
-  __shared__ uint32_t s_acc[kWpb][kWave];  // TN | (contributing distinct count << 16), carried across strips
-  __shared__ uint32_t s_cnt[kWpb][kWave];  // running distinct count (can exceed 16 bits)
-  __shared__ uint16_t s_nm[kWpb][kWave];
-  const int lane = lane_id(), w = threadIdx.x / kWave;
-  const uint64_t nchunks = (n + kWave - 1) / kWave;
-  const uint64_t cstride = uint64_t(gridDim.x) * kWpb;
-  // Vertex data of the next chunk is loaded one iteration ahead (software
-  // pipelining): Tl and the two row offsets come from independent, coalesced
-  // loads (off[u+1] via a lane shuffle) so no HBM round trip sits between chunks.
-  uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w;
-  uint16_t pf_t = 0;
-  uint64_t pf_o = 0, pf_o63 = 0;
-  auto prefetch = [&](uint64_t c) {
-    const uint64_t u = c * kWave + lane;
-    pf_t = (c < nchunks && u < n) ? tl[u] : uint16_t(0);
-    pf_o = (c < nchunks) ? off[u < n ? u : n] : 0;
-    pf_o63 = (c < nchunks && lane == kWave - 1) ? off[(u + 1) < n ? (u + 1) : n] : 0;
-  };
-  prefetch(chunk);
-  for (; chunk < nchunks; chunk += cstride) {
-    const uint64_t u = chunk * kWave + lane;
-    const uint16_t Tu = pf_t;
-    const uint64_t o_next = __shfl_down(pf_o, 1, kWave);
-    const uint64_t beg = pf_o;
-    const uint64_t deg = Tu ? ((lane == kWave - 1 ? pf_o63 : o_next) - beg) : 0;
-    prefetch(chunk + cstride);
-    const uint64_t incl = wave_incl_scan(deg);
-    const uint64_t total = __shfl(incl, kWave - 1, kWave);
-    s_rs[w][lane] = incl - deg;
-    s_beg[w][lane] = beg;
-    s_nm[w][lane] = nbr_mask(Tu, pa);
-    s_acc[w][lane] = 0;
-    s_cnt[w][lane] = 0;
-    __builtin_amdgcn_wave_barrier();
-    // Strips of kU x 64 entries: every lane issues kU independent adjacency
-    // loads, then kU independent Tl gathers, before any reduction (memory-level
-    // parallelism; a single 64-entry strip per iteration is latency bound).
-    for (uint64_t j0 = 0; j0 < total; j0 += uint64_t(kWave) * KU) {
-      int r[KU];
-      uint64_t rel[KU], e[KU];
-      uint32_t v[KU];
-#pragma unroll
-      for (int q = 0; q < KU; ++q) {
-        const uint64_t j = j0 + uint64_t(q) * kWave + lane;
-        r[q] = kWave;  // sentinel row for idle lanes
-        rel[q] = 0;
-        e[q] = 0;
-        v[q] = kNone;
-        if (j < total) {
-          r[q] = find_row(s_rs[w], j);
-          rel[q] = j - s_rs[w][r[q]];
-          e[q] = s_beg[w][r[q]] + rel[q];
-          v[q] = col[e[q]];
-        }
-      }
-      uint32_t pv0 = kNone;
-      if (lane == 0 && r[0] < kWave && rel[0] > 0) pv0 = col[e[0] - 1];
-      bool hit[KU];
-      uint16_t tv[KU];
-      if (MODE & 2) {
-#pragma unroll
-        for (int q = 0; q < KU; ++q) tv[q] = static_cast<uint16_t>(v[q] & 0x1Fu);
-      } else {
-#pragma unroll
-        for (int q = 0; q < KU; ++q) hit[q] = (r[q] < kWave) && ((tlbits[v[q] >> 6] >> (v[q] & 63)) & 1ull);
-#pragma unroll
-        for (int q = 0; q < KU; ++q) tv[q] = hit[q] ? tl[v[q]] : uint16_t(0);
-      }
-#pragma unroll
-      for (int q = 0; q < KU; ++q) {
-        // predecessor entry j-1 (same row whenever rel > 0): lane-1 of this
-        // slice, lane 63 of the previous slice, or loaded before the strip.
-        uint32_t pv = __shfl_up(v[q], 1, kWave);
-        const uint32_t carry = q ? __shfl(v[q ? q - 1 : 0], kWave - 1, kWave) : pv0;
-        if (lane == 0) pv = carry;
-        const bool valid = r[q] < kWave;
-        uint32_t x = 0;
-        if (valid) {
-          const bool first = (rel[q] == 0) || (pv != v[q]);
-          const bool cm = (tv[q] & s_nm[w][r[q]]) != 0;
-          x = (cm ? tv[q] : 0u) | ((cm && first) ? (1u << 16) : 0u);
-        }
-        const uint32_t inc = (MODE & 4) ? x : seg_scan_orsum(x, r[q]);
-        const int rnext = __shfl_down(r[q], 1, kWave);
-        if (valid) {
-          if ((x >> 16) && !(MODE & 1)) {
-            // exclusive position of this distinct contributor inside u's row
-            const uint32_t pos = s_cnt[w][r[q]] + (inc >> 16) - 1;
-            const uint64_t dst = s_beg[w][r[q]] + pos;
-            mcol[dst] = v[q];
-            mst[dst] = 1;
-          }
-          if (lane == kWave - 1 || rnext != r[q]) {
-            s_acc[w][r[q]] |= inc & 0xFFFFu;
-            s_cnt[w][r[q]] += inc >> 16;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    // finalize row `lane`
-    bool survivor = false, removed = false;
-    uint32_t cnt = 0;
-    if (u < n && Tu) {
-      const uint16_t TN = static_cast<uint16_t>(s_acc[w][lane] & 0xFFFFu);
-      if (TN) {  // entered the state map
-        const uint16_t T = keep_bits(Tu, TN, pa);
-        if (T) {
-          survivor = true;
-          cnt = s_cnt[w][lane];
-          tst[u] = T;
-          tpub[u] = T;
-          mlen[u] = cnt;
-          malive[u] = cnt;
-        } else {
-          removed = true;
-        }
-      }
-    }
-    const uint64_t smask = __ballot(survivor);
-    if (lane == 0) cmask[chunk] = smask;  // slist is built from these masks (k_slist_write)
-    // counts: vertices/edges per rank (owner rule) and traversed entries
-    acc.trav += deg;
-    acc.match += Tu != 0;
-    acc.removed |= removed;
-    if (survivor) {
-      if (oa.nranks <= 1) {
-        acc.vs += 1;
-        acc.es += cnt;
-      } else {
-        acc_owner(s_hist, oa, u, cnt);
-      }
-    }
+// Survivors get T_pub = T_state, |M[u]| and a bit in the tile survivor mask.
+//
+// Only the label-matching runs of the padded label-major CSR are visited
+// (KRange table, staged in LDS); Tl(v) follows from v's position (LabelRuns).
+// A tile is kTileEntries consecutive slots: every lane issues kSub adjacency
+// loads before any use (one memory round trip per tile).  G <= 64: a sub-tile
+// holds 64/G rows, G lanes each; per-row OR and count come from wave ballots,
+// M positions from a masked popcount.  G = 128..1024: sub-tiles are the
+// consecutive 64-slot slices of G/64-slot rows, reduced in order.  Rows above
+// kHeavyDeg are cut into kHeavyDeg segments (one per tile) whose M stays
+// uncompacted (dead entries keep bit0 = 0); the last segment to finish
+// (ticket counter) runs the verify.  Only neighbour-mask bits of TN are
+// reduced: bits outside NbrMask(Tu) never affect keep_bits.
+__device__ __forceinline__ uint16_t wave_or_bits(uint32_t x, uint16_t nm, int shift, uint64_t gmask) {
+  uint16_t r = 0, b = nm;
+  while (b) {
+    const int t = __ffs(static_cast<int>(b)) - 1;
+    b &= static_cast<uint16_t>(b - 1);
+    const uint64_t bb = __ballot((x >> t) & 1u);
+    if ((bb >> shift) & gmask) r |= static_cast<uint16_t>(1u << t);
   }
-  flush_block(acc, oa, s_hist, s_red, part);
+  return r;
 }
 
-// Alternative superstep-0 kernel (ablation): one lane per row, serial scan of
-// the row with kU-way unrolled independent loads; no LDS, no shuffles.
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_lcc_first_lpr(
-    const uint64_t* __restrict__ off, const uint32_t* __restrict__ col, const uint16_t* __restrict__ tl,
-    const unsigned long long* __restrict__ tlbits, uint64_t n, PatArgs pa, OwnerArgs oa,
-    uint16_t* __restrict__ tst, uint16_t* __restrict__ tpub, uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst,
-    uint32_t* __restrict__ mlen, uint32_t* __restrict__ malive, unsigned long long* __restrict__ cmask,
+struct K1Out {
+  uint16_t* tst;
+  uint16_t* tpub;
+  uint32_t* mcol;
+  uint8_t* mst;
+  uint32_t* mlen;
+  uint32_t* malive;
+};
+
+// Template bits of neighbour position p that can meet the range's nm: four
+// runs held in registers (wave-uniform), the rest (rare) scanned from LDS.
+struct RelRuns {
+  uint32_t lo[4], len[4], tu[4];
+  uint32_t nrel;
+};
+
+__device__ __forceinline__ RelRuns load_rel(const KRange& R) {
+  RelRuns x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x.lo[i] = __builtin_amdgcn_readfirstlane(R.rlo[i]);
+    x.len[i] = __builtin_amdgcn_readfirstlane(R.rlen[i]);
+    x.tu[i] = __builtin_amdgcn_readfirstlane(R.rtu[i]);
+  }
+  x.nrel = __builtin_amdgcn_readfirstlane(R.nrel);
+  return x;
+}
+
+template <bool WIDE>
+__device__ __forceinline__ uint16_t tbits_rel(uint32_t p, const RelRuns& x, const uint32_t* s_runs, int nruns) {
+  uint32_t t = 0;
+  if (WIDE) {  // more than four relevant runs somewhere: scan all runs (LDS)
+    for (int l = 0; l < nruns; ++l)
+      if (p - s_runs[3 * l] < s_runs[3 * l + 1]) t |= s_runs[3 * l + 2];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (p - x.lo[i] < x.len[i]) t |= x.tu[i];
+  }
+  return static_cast<uint16_t>(t);
+}
+
+// Verify of the row at position u by the calling lane; returns survivor.
+__device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t TN, uint32_t len, uint32_t cnt,
+                                              const uint16_t* adj, const OwnerArgs& oa, const K1Out& o, BlockAcc& acc,
+                                              unsigned long long* s_hist) {
+  if (!TN) return false;
+  const uint16_t T = keep_bits(tu, TN, adj);
+  if (!T) {
+    acc.removed = 1;
+    return false;
+  }
+  o.tst[u] = T;
+  o.tpub[u] = T;
+  o.mlen[u] = len;
+  o.malive[u] = cnt;
+  if (oa.nranks <= 1) {
+    acc.vs += 1;
+    acc.es += cnt;
+  } else {
+    acc_owner(s_hist, oa, u, cnt);
+  }
+  return true;
+}
+
+// One 64-slot slice of a row scanned by the whole wave (G >= 64 and heavy
+// segments).  j = slot index of this lane inside the row; carry = the row's
+// previous slot (kNone at the row start).  COMPACT: M position = running
+// distinct count, else the slot itself.
+template <bool COMPACT, int MODE>
+__device__ __forceinline__ void k1_slice(uint32_t v, uint16_t tv, uint32_t j, uint64_t rowbase, uint16_t nm,
+                                         const K1Out& o, uint32_t& cnt, uint32_t& tnacc, uint32_t& carry) {
+  const int lane = lane_id();
+  uint32_t pv = __shfl_up(v, 1, kWave);
+  if (lane == 0) pv = carry;
+  carry = __shfl(v, kWave - 1, kWave);
+  const bool ok = v != kNone;
+  const bool first = ok && (j == 0 || pv != v);
+  const bool cm = ok && (tv & nm) != 0;
+  const bool contrib = cm && first;
+  const uint64_t bal = __ballot(contrib);
+  if (MODE & 9) {
+  } else if (COMPACT) {
+    if (contrib) {
+      const uint64_t dst = rowbase + cnt + __builtin_popcountll(bal & ((1ull << lane) - 1));
+      o.mcol[dst] = v;
+      o.mst[dst] = 1;
+    }
+  } else if (ok) {
+    o.mcol[rowbase + j] = v;
+    o.mst[rowbase + j] = contrib ? 1 : 0;
+  }
+  cnt += static_cast<uint32_t>(__builtin_popcountll(bal));
+  if (cm) tnacc |= tv;
+}
+
+// MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores,
+// bit1 skips G <= 64 tiles, bit2 skips G >= 128 tiles, bit3 drops every
+// store except a checksum of the loaded slots.  WIDE: some range has more
+// than four relevant label runs (tbits_rel scans them all).
+template <int MODE, bool WIDE = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lcc_first(
+    const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
+    const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
+    K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, unsigned long long* __restrict__ tmask,
     unsigned long long* __restrict__ part) {
+  __shared__ KRange s_tab[kMaxRanges];
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
+  __shared__ uint16_t s_adj[16];
+  __shared__ uint32_t s_runs[3 * 16];
+  for (uint32_t i = threadIdx.x; i <= nr; i += blockDim.x) s_tab[i] = ktab[i];
+  load_adj(s_adj, pa);
+  if (threadIdx.x < 16) {
+    const int l = threadIdx.x;
+    s_runs[3 * l] = lr.lo[l];
+    s_runs[3 * l + 1] = l < lr.n ? lr.len[l] : 0u;
+    s_runs[3 * l + 2] = lr.tu[l];
+  }
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   __syncthreads();
   BlockAcc acc;
-  const int lane = lane_id(), w = threadIdx.x / kWave;
-  const uint64_t nchunks = (n + kWave - 1) / kWave;
-  for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb) {
-    const uint64_t u = chunk * kWave + lane;
-    uint16_t Tu = 0;
-    uint64_t beg = 0, deg = 0;
-    if (u < n) {
-      Tu = tl[u];
-      if (Tu) {
-        beg = off[u];
-        deg = off[u + 1] - beg;
+  const int lane = lane_id();
+  const uint32_t W = gridDim.x * kWpb;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform
+  const int nruns = lr.n;
+  uint32_t r = 0;
+  for (uint32_t t = blockIdx.x * kWpb + wid; t < ntiles; t += W) {
+    while (__builtin_amdgcn_readfirstlane(s_tab[r + 1].tile0) <= t) ++r;
+    const uint32_t kind = __builtin_amdgcn_readfirstlane(s_tab[r].kind);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(s_tab[r].start);
+    const uint32_t nrows = __builtin_amdgcn_readfirstlane(s_tab[r].end) - start;
+    const uint32_t rel = t - __builtin_amdgcn_readfirstlane(s_tab[r].tile0);
+    const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(s_tab[r].tu));
+    const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(s_tab[r].nm));
+    const uint64_t qbase = (uint64_t(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase >> 32))) << 32) |
+                           __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase));
+    unsigned long long* tm = tmask + uint64_t(t) * kSub;
+    const RelRuns rel_runs = load_rel(s_tab[r]);
+#define PM_TB(x) ((x) != kNone ? tbits_rel<WIDE>((x), rel_runs, s_runs, nruns) : uint16_t(0))
+    if (kind <= 6) {
+      if (MODE & 2) continue;
+      // ---- G <= 64: G lanes per row, 64/G rows per sub-tile
+      const int lg = static_cast<int>(kind);
+      const int k = lane & ((1 << lg) - 1);
+      const int shift = (lane >> lg) << lg;
+      const uint64_t gmask = lg == 6 ? ~0ull : ((1ull << (1u << lg)) - 1);
+      const uint64_t t0 = uint64_t(rel) * kTileEntries;          // slot offset of the tile in the run
+      const uint64_t tend = uint64_t(nrows) << lg;              // slots of the run
+      uint32_t v[kSub];
+#pragma unroll
+      for (int q = 0; q < kSub; ++q) {
+        const uint64_t s = t0 + q * kWave + lane;
+        v[q] = s < tend ? colp[qbase + s] : kNone;
       }
-    }
-    const uint16_t NM = nbr_mask(Tu, pa);
-    uint32_t TN = 0, cnt = 0, prev = kNone;
-    for (uint64_t i0 = 0; i0 < deg; i0 += kU) {
-      uint32_t v[kU];
-      uint16_t tv[kU];
+      if (MODE & 8) {
 #pragma unroll
-      for (int q = 0; q < kU; ++q) v[q] = (i0 + q < deg) ? col[beg + i0 + q] : kNone;
-#pragma unroll
-      for (int q = 0; q < kU; ++q) {
-        const bool hit = v[q] != kNone && ((tlbits[v[q] >> 6] >> (v[q] & 63)) & 1ull);
-        tv[q] = hit ? tl[v[q]] : uint16_t(0);
+        for (int q = 0; q < kSub; ++q) acc.vs += v[q] ^ PM_TB(v[q]);
+        continue;
       }
+#pragma unroll 1
+      for (int q = 0; q < kSub; ++q) {
+        // rolled loop: the slice in use rotates into v[0] (no dynamic register indexing)
+        const uint32_t vq = v[0];
 #pragma unroll
-      for (int q = 0; q < kU; ++q) {
-        if (v[q] == kNone) break;
-        const bool cm = (tv[q] & NM) != 0;
-        if (cm) {
-          TN |= tv[q];
-          if (v[q] != prev) {
-            if (!(MODE & 1)) {
-              mcol[beg + cnt] = v[q];
-              mst[beg + cnt] = 1;
-            }
-            ++cnt;
+        for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
+        const uint16_t tvq = PM_TB(vq);
+        const uint64_t s = t0 + q * kWave + lane;
+        const uint32_t rr = static_cast<uint32_t>(s >> lg);    // row inside the run
+        const uint32_t pv = __shfl_up(vq, 1, kWave);
+        const bool ok = vq != kNone;
+        const bool first = ok && (k == 0 || pv != vq);
+        const bool cm = ok && (tvq & nm) != 0;
+        const bool contrib = cm && first;
+        const uint64_t g = (__ballot(contrib) >> shift) & gmask;
+        if (contrib && !(MODE & 1)) {
+          const uint64_t dst = qbase + (uint64_t(rr) << lg) + __builtin_popcountll(g & ((1ull << k) - 1));
+          o.mcol[dst] = vq;
+          o.mst[dst] = 1;
+        }
+        const uint16_t TN = wave_or_bits(cm ? tvq : 0u, nm, shift, gmask);
+        bool surv = false;
+        if (k == 0 && rr < nrows) {
+          const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(g));
+          surv = k1_finish_row(start + rr, tu, TN, c, c, s_adj, oa, o, acc, s_hist);
+        }
+        const uint64_t sm = __ballot(surv);
+        if (lane == 0) tm[q] = sm;
+      }
+    } else if (kind <= 10) {
+      if (MODE & 4) continue;
+      // ---- G = 128..1024: consecutive 64-slot slices of one row at a time
+      const int lg = static_cast<int>(kind);
+      const uint32_t spr = 1u << (lg - 6);                       // slices per row
+      const uint32_t te = kTileEntries > (1u << lg) ? kTileEntries : (1u << lg);
+      const uint64_t t0 = uint64_t(rel) * te;
+      const uint64_t tend = uint64_t(nrows) << lg;
+      uint64_t smask = 0;
+      uint32_t cnt = 0, tnacc = 0, carry = kNone;
+      for (uint32_t b0 = 0; b0 < te / kWave; b0 += kSub) {
+        uint32_t v[kSub];
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+          const uint64_t s = t0 + (b0 + q) * kWave + lane;
+          v[q] = s < tend ? colp[qbase + s] : kNone;
+        }
+        if (MODE & 8) {
+#pragma unroll
+          for (int q = 0; q < kSub; ++q) acc.vs += v[q] ^ PM_TB(v[q]);
+          continue;
+        }
+#pragma unroll 1
+        for (int q = 0; q < kSub; ++q) {
+          const uint32_t vq = v[0];
+#pragma unroll
+          for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
+          const uint64_t s0 = t0 + (b0 + q) * kWave;             // first slot of the slice
+          const uint32_t rr = static_cast<uint32_t>(s0 >> lg);
+          const uint32_t sl = (b0 + q) & (spr - 1);
+          if (sl == 0) {
+            cnt = 0;
+            tnacc = 0;
+            carry = kNone;
+          }
+          k1_slice<true, MODE>(vq, PM_TB(vq), sl * kWave + lane, qbase + (uint64_t(rr) << lg), nm, o, cnt, tnacc,
+                               carry);
+          if (sl == spr - 1) {
+            const uint16_t TN = wave_or_bits(tnacc, nm, 0, ~0ull);
+            bool surv = false;
+            if (lane == 0 && rr < nrows) surv = k1_finish_row(start + rr, tu, TN, cnt, cnt, s_adj, oa, o, acc, s_hist);
+            if (__ballot(surv)) smask |= 1ull << (rr - static_cast<uint32_t>(t0 >> lg));
           }
         }
-        prev = v[q];
       }
-    }
-    bool survivor = false, removed = false;
-    if (Tu && TN) {
-      const uint16_t T = keep_bits(Tu, static_cast<uint16_t>(TN), pa);
-      if (T) {
-        survivor = true;
-        tst[u] = T;
-        tpub[u] = T;
-        mlen[u] = cnt;
-        malive[u] = cnt;
-      } else {
-        removed = true;
+      if (lane < kSub && !(MODE & 8)) tm[lane] = lane == 0 ? smask : 0ull;
+    } else {
+      if (MODE & 4) continue;
+      // ---- heavy rows: one kHeavyDeg segment per tile, uncompacted M
+      const HSeg hs = hseg[s_tab[r].aux + rel];
+      const uint64_t b0 = offp[hs.row];
+      const uint32_t deg = static_cast<uint32_t>(offp[hs.row + 1] - b0);
+      const uint32_t j_beg = hs.seg * kHeavyDeg;
+      const uint32_t j_end = min(deg, j_beg + kHeavyDeg);
+      uint32_t cnt = 0, tnacc = 0;
+      uint32_t carry = j_beg ? colp[b0 + j_beg - 1] : kNone;
+      for (uint32_t j0 = j_beg; j0 < j_end; j0 += kSub * kWave) {
+        uint32_t v[kSub];
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+          const uint32_t j = j0 + q * kWave + lane;
+          v[q] = j < j_end ? colp[b0 + j] : kNone;
+        }
+#pragma unroll 1
+        for (int q = 0; q < kSub; ++q) {
+          const uint32_t vq = v[0];
+#pragma unroll
+          for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
+          k1_slice<false, MODE>(vq, PM_TB(vq), j0 + q * kWave + lane, b0, nm, o, cnt, tnacc, carry);
+        }
       }
-    }
-    const uint64_t smask = __ballot(survivor);
-    if (lane == 0) cmask[chunk] = smask;
-    acc.trav += deg;
-    acc.match += Tu != 0;
-    acc.removed |= removed;
-    if (survivor) {
-      if (oa.nranks <= 1) {
-        acc.vs += 1;
-        acc.es += cnt;
-      } else {
-        acc_owner(s_hist, oa, u, cnt);
+      const uint16_t TN = wave_or_bits(tnacc, nm, 0, ~0ull);
+      bool surv = false;
+      if (lane == 0 && !(MODE & 8)) {
+        uint32_t* h_tn = hscr;
+        uint32_t* h_cnt = hscr + nheavy;
+        uint32_t* h_done = hscr + 2 * nheavy;
+        if (TN) atomicOr(&h_tn[hs.h], static_cast<uint32_t>(TN));
+        if (cnt) atomicAdd(&h_cnt[hs.h], cnt);
+        __threadfence();
+        if (atomicAdd(&h_done[hs.h], 1u) == hs.nseg - 1) {
+          __threadfence();
+          const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
+          const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
+          surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, oa, o, acc, s_hist);
+        }
       }
+      if (lane < kSub && !(MODE & 8)) tm[lane] = (lane == 0 && surv) ? 1ull : 0ull;
     }
   }
+#undef PM_TB
   flush_block(acc, oa, s_hist, s_red, part);
 }
 
-// slist from the superstep-0 survivor masks: an exclusive scan of the
-// per-chunk popcounts (hipcub) gives each chunk's base.
-__global__ void k_slist_write(const unsigned long long* __restrict__ cmask, const uint64_t* __restrict__ base,
-                              uint64_t nchunks, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
-  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < nchunks; c += uint64_t(gridDim.x) * blockDim.x) {
-    unsigned long long m = cmask[c];
-    uint64_t o = base[c];
+// slist from the superstep-0 survivor masks: an exclusive scan of the mask
+// popcounts (hipcub) gives each word's base; bits decode to row positions
+// through the tiling.
+__global__ void k_slist_write(const KRange* __restrict__ ktab, uint32_t nr, const HSeg* __restrict__ hseg,
+                              const unsigned long long* __restrict__ tmask, const uint64_t* __restrict__ base,
+                              uint64_t nwords, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
+  for (uint64_t wi = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; wi < nwords; wi += uint64_t(gridDim.x) * blockDim.x) {
+    unsigned long long m = tmask[wi];
+    uint64_t o = base[wi];
+    if (wi == nwords - 1) *nS = static_cast<uint32_t>(o + __builtin_popcountll(m));
+    if (!m) continue;
+    const uint32_t t = static_cast<uint32_t>(wi / kSub), q = static_cast<uint32_t>(wi % kSub);
+    uint32_t lo = 0, hi = nr;  // last range with tile0 <= t
+    while (lo + 1 < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ktab[mid].tile0 <= t) lo = mid; else hi = mid;
+    }
+    const KRange R = ktab[lo];
+    const uint32_t rel = t - R.tile0;
     while (m) {
       const int b = __ffsll(static_cast<long long>(m)) - 1;
       m &= m - 1;
-      slist[o++] = static_cast<uint32_t>(c * kWave + b);
+      uint32_t row;
+      if (R.kind <= 6) {
+        row = R.start + static_cast<uint32_t>((uint64_t(rel) * kTileEntries + q * kWave + b) >> R.kind);
+      } else if (R.kind <= 10) {
+        const uint32_t te = kTileEntries > (1u << R.kind) ? kTileEntries : (1u << R.kind);
+        row = R.start + static_cast<uint32_t>((uint64_t(rel) * te) >> R.kind) + b;
+      } else {
+        row = hseg[R.aux + rel].row;
+      }
+      slist[o++] = row;
     }
-    if (c == nchunks - 1) *nS = static_cast<uint32_t>(o);
   }
+}
+
+// Last row r (0..63) of a wave's strip space whose start <= j.
+__device__ __forceinline__ int find_row(const uint64_t* rs, uint64_t j) {
+  int lo = 0, hi = kWave - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rs[mid] <= j) lo = mid; else hi = mid - 1;
+  }
+  return lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -515,13 +697,15 @@ __global__ void k_slist_write(const unsigned long long* __restrict__ cmask, cons
 // verify without a message; if its neighbour is still in S that breaks the
 // symmetry, which is reported through flags[1] (the host then refuses to go on).
 __global__ __launch_bounds__(kBlock) void k_lcc_step(
-    const uint64_t* __restrict__ off, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
+    const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, const uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, unsigned long long* __restrict__ part) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
+  __shared__ uint16_t s_adj[16];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  load_adj(s_adj, pa);
   __syncthreads();
   BlockAcc acc;
   __shared__ uint64_t s_rs[kWpb][kWave];
@@ -529,7 +713,8 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   __shared__ uint32_t s_acc[kWpb][kWave];
   __shared__ uint32_t s_cnt[kWpb][kWave];
   __shared__ uint16_t s_nm[kWpb][kWave];
-  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t nS = *nSp;
   const uint64_t nchunks = (uint64_t(nS) + kWave - 1) / kWave;
   for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb) {
@@ -542,7 +727,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
       u = slist[i];
       Tu = tcur[u];
       if (Tu) {
-        beg = off[u];
+        beg = offp[u];
         len = mlen[u];
         alive0 = malive[u];
       } else {
@@ -553,7 +738,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t total = __shfl(incl, kWave - 1, kWave);
     s_rs[w][lane] = incl - len;
     s_beg[w][lane] = beg;
-    s_nm[w][lane] = nbr_mask(Tu, pa);
+    s_nm[w][lane] = nbr_mask(Tu, s_adj);
     s_acc[w][lane] = 0;
     s_cnt[w][lane] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -603,7 +788,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     uint32_t cnt = 0;
     if (Tu) {
       const uint16_t TN = static_cast<uint16_t>(s_acc[w][lane] & 0xFFFFu);
-      const uint16_t T = keep_bits(tst[u], TN, pa);
+      const uint16_t T = keep_bits(tst[u], TN, s_adj);
       if (T) {
         survivor = true;
         cnt = s_cnt[w][lane];
@@ -669,6 +854,7 @@ static unsigned grid_for(uint64_t items, unsigned per_block, unsigned cap = 6553
 static OwnerArgs owner_args(const Ctx& c) {
   OwnerArgs oa;
   oa.hubs = c.d_hubs;
+  oa.perm = c.d_perm;
   oa.nhubs = static_cast<uint32_t>(c.hubs_host.size());
   oa.nranks = c.nranks;
   return oa;
@@ -677,12 +863,6 @@ static OwnerArgs owner_args(const Ctx& c) {
 void launch_degree_labels(Ctx& c) {
   hipLaunchKernelGGL(k_degree_labels, dim3(grid_for(c.n, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_off, c.n,
                      c.d_labels);
-  PM_HIP_CHECK(hipGetLastError());
-}
-
-void launch_label_match(Ctx& c) {
-  hipLaunchKernelGGL(k_label_match, dim3(grid_for(c.n, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_labels, c.n,
-                     c.pa, c.d_tl, reinterpret_cast<unsigned long long*>(c.d_tlbits));
   PM_HIP_CHECK(hipGetLastError());
 }
 
@@ -695,74 +875,270 @@ static void reduce_into(Ctx& c, unsigned grid, uint64_t* d_slot) {
   PM_HIP_CHECK(hipGetLastError());
 }
 
-// variant: 0 = product (strip kernel); 1..7 = strip ablation MODE; 16+ = lane-per-row (MODE = variant-16)
+// Sorts the vertices by (label, degree, id) (two stable LSD radix passes:
+// degree, then label) and writes the renumbered adjacency into dst.
+void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst) {
+  const uint64_t n = c.n;
+  c.arena.reset();
+  if (n) {
+    const unsigned g = grid_for(n, kBlock, 8192);
+    auto* src_start = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
+    if (src_is_layout) {
+      hipLaunchKernelGGL(k_row_starts_by_id, dim3(g), dim3(kBlock), 0, c.stream, c.d_offp, c.d_perm, n, src_start);
+      hipLaunchKernelGGL(k_to_ids, dim3(grid_for(c.nq, kBlock, 65535)), dim3(kBlock), 0, c.stream, src_col, c.nq,
+                         c.d_perm);
+    } else {
+      PM_HIP_CHECK(hipMemcpyAsync(src_start, c.d_off, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+    }
+    auto* dkey = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
+    auto* dkey2 = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
+    auto* ids = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
+    auto* ids2 = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
+    auto* lkey = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_layout_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, n, dkey, ids);
+    size_t tmp = 0, tmp2 = 0;
+    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 32,
+                                                    c.stream));
+    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, lkey, c.d_labs, ids2, c.d_perm, static_cast<int>(n),
+                                                    0, 64, c.stream));
+    tmp = std::max(tmp, tmp2);
+    void* d_tmp = c.arena.get(tmp);
+    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 32,
+                                                    c.stream));
+    hipLaunchKernelGGL(k_gather_labels, dim3(g), dim3(kBlock), 0, c.stream, c.d_labels, ids2, n, lkey);
+    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, lkey, c.d_labs, ids2, c.d_perm, static_cast<int>(n), 0,
+                                                    64, c.stream));
+    hipLaunchKernelGGL(k_inverse_perm, dim3(g), dim3(kBlock), 0, c.stream, c.d_perm, n, c.d_pos);
+    // label-major offsets: padded (slots) and real (degree sums)
+    auto* pdeg = lkey;  // reuse
+    auto* rdeg = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_perm_degrees, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, c.d_perm, n, pdeg, rdeg);
+    size_t tmp3 = 0;
+    PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp3, pdeg, c.d_offp + 1, static_cast<int>(n), c.stream));
+    void* d_tmp3 = c.arena.get(tmp3);
+    PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(d_tmp3, tmp3, pdeg, c.d_offp + 1, static_cast<int>(n), c.stream));
+    PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(d_tmp3, tmp3, rdeg, c.d_offr + 1, static_cast<int>(n), c.stream));
+    PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
+    PM_HIP_CHECK(hipMemsetAsync(c.d_offr, 0, sizeof(uint64_t), c.stream));
+    hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, kWpb, 65535)), dim3(kBlock), 0, c.stream, src_col, src_start,
+                       c.d_off, c.d_offp, c.d_perm, c.d_pos, n, dst);
+    PM_HIP_CHECK(hipGetLastError());
+  } else {
+    PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
+    PM_HIP_CHECK(hipMemsetAsync(c.d_offr, 0, sizeof(uint64_t), c.stream));
+  }
+  c.perm_host.resize(n);
+  if (n) PM_HIP_CHECK(hipMemcpyAsync(c.perm_host.data(), c.d_perm, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.arena.reset();
+}
+
+// Superstep-0 tiling for the current layout and pattern (host-side table).
+void build_tiling(Ctx& c) {
+  // distinct pattern labels and their template bits
+  std::vector<uint64_t> labs;
+  std::vector<uint16_t> tus;
+  for (int t = 0; t < c.pa.K; ++t) {
+    auto it = std::find(labs.begin(), labs.end(), c.pa.plabel[t]);
+    if (it == labs.end()) {
+      labs.push_back(c.pa.plabel[t]);
+      tus.push_back(static_cast<uint16_t>(1u << t));
+    } else {
+      tus[it - labs.begin()] |= static_cast<uint16_t>(1u << t);
+    }
+  }
+  const int nl = static_cast<int>(labs.size());
+  std::vector<uint64_t> bounds(std::max(nl, 1) * kLB, 0);
+  if (nl && c.n) {
+    c.arena.reset();
+    auto* d_want = static_cast<uint64_t*>(c.arena.get(nl * sizeof(uint64_t)));
+    auto* d_out = static_cast<uint64_t*>(c.arena.get(nl * kLB * sizeof(uint64_t)));
+    PM_HIP_CHECK(hipMemcpyAsync(d_want, labs.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+    hipLaunchKernelGGL(k_label_bounds, dim3(1), dim3(64), 0, c.stream, c.d_labs, c.d_offp, c.n, d_want, nl, d_out);
+    PM_HIP_CHECK(hipGetLastError());
+    PM_HIP_CHECK(hipMemcpyAsync(bounds.data(), d_out, nl * kLB * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    c.arena.reset();
+  }
+  auto dev_at = [&](const uint64_t* arr, uint64_t i) {
+    uint64_t x = 0;
+    PM_HIP_CHECK(hipMemcpy(&x, arr + i, sizeof(x), hipMemcpyDeviceToHost));
+    return x;
+  };
+  c.lr = LabelRuns{};
+  c.lr.n = nl;
+  for (int l = 0; l < nl; ++l) {
+    c.lr.lo[l] = static_cast<uint32_t>(bounds[l * kLB + 0]);
+    c.lr.len[l] = static_cast<uint32_t>(bounds[l * kLB + 13] - bounds[l * kLB + 0]);
+    c.lr.tu[l] = tus[l];
+  }
+  std::vector<KRange> tab;
+  std::vector<HSeg> hs;
+  uint32_t tiles = 0, nheavy = 0;
+  c.ss0_trav = 0;
+  c.ss0_rows = 0;
+  for (int l = 0; l < nl; ++l) {
+    const uint64_t* B = bounds.data() + l * kLB;
+    const uint16_t tu = tus[l];
+    uint16_t nm = 0;
+    for (int t = 0; t < 16; ++t)
+      if ((tu >> t) & 1u) nm |= c.pa.adj[t];
+    const uint64_t first_nz = B[1], hi = B[13];
+    if (hi <= first_nz) continue;
+    c.ss0_rows += hi - first_nz;
+    c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
+    if (!nm) continue;  // such rows never enter S (TN = 0): scanned by no kernel, counted above
+    // kind k = [B[1+k], B[2+k]) for k = 0..10 (padded degree 1 << k); kind 11 = [B[12], hi)
+    for (int kind = 0; kind <= kHeavyKind; ++kind) {
+      const uint64_t a = B[1 + kind];
+      const uint64_t b = kind == kHeavyKind ? hi : B[2 + kind];
+      if (b <= a) continue;
+      KRange R{};
+      R.tile0 = tiles;
+      R.start = static_cast<uint32_t>(a);
+      R.end = static_cast<uint32_t>(b);
+      R.tu = tu;
+      R.nm = nm;
+      R.kind = static_cast<uint32_t>(kind);
+      R.qbase = dev_at(c.d_offp, a);
+      R.nrel = 0;
+      for (int m = 0; m < nl; ++m) {
+        if (!(tus[m] & nm) || c.lr.len[m] == 0) continue;
+        if (R.nrel < 4) {
+          R.rlo[R.nrel] = c.lr.lo[m];
+          R.rlen[R.nrel] = c.lr.len[m];
+          R.rtu[R.nrel] = tus[m];
+        }
+        ++R.nrel;
+      }
+      uint64_t nt;
+      if (kind < kHeavyKind) {
+        const uint64_t te = std::max<uint64_t>(kTileEntries, 1ull << kind);
+        nt = ((b - a) * (1ull << kind) + te - 1) / te;
+      } else {
+        R.aux = static_cast<uint32_t>(hs.size());
+        std::vector<uint64_t> o(b - a + 1);
+        PM_HIP_CHECK(hipMemcpy(o.data(), c.d_offp + a, o.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        for (uint64_t i = a; i < b; ++i) {
+          const uint64_t deg = o[i - a + 1] - o[i - a];
+          const uint32_t ns = static_cast<uint32_t>((deg + kHeavyDeg - 1) / kHeavyDeg);
+          for (uint32_t sgm = 0; sgm < ns; ++sgm) hs.push_back(HSeg{static_cast<uint32_t>(i), sgm, nheavy, ns});
+          ++nheavy;
+        }
+        nt = hs.size() - R.aux;
+      }
+      if (uint64_t(tiles) + nt >= 0xFFFFFFFFull) throw std::runtime_error("superstep-0 tiling exceeds 2^32 tiles");
+      tiles += static_cast<uint32_t>(nt);
+      tab.push_back(R);
+    }
+  }
+  if (tab.size() + 1 > static_cast<size_t>(kMaxRanges)) throw std::runtime_error("internal: too many tile ranges");
+  KRange sent{};
+  sent.tile0 = tiles;
+  tab.push_back(sent);
+  c.ktab = tab;
+  c.k1_wide = false;
+  for (const auto& R : tab)
+    if (R.nrel > 4) c.k1_wide = true;
+  c.ntiles = tiles;
+  c.nheavy = nheavy;
+  if (c.d_ktab) (void)hipFree(c.d_ktab);
+  if (c.d_hseg) (void)hipFree(c.d_hseg);
+  if (c.d_hscr) (void)hipFree(c.d_hscr);
+  if (c.d_tmask) (void)hipFree(c.d_tmask);
+  if (c.d_tbase) (void)hipFree(c.d_tbase);
+  if (c.d_scan_tmp) (void)hipFree(c.d_scan_tmp);
+  c.d_ktab = nullptr;
+  c.d_hseg = nullptr;
+  c.d_hscr = nullptr;
+  c.d_tmask = c.d_tbase = nullptr;
+  c.d_scan_tmp = nullptr;
+  PM_HIP_CHECK(hipMalloc(&c.d_ktab, tab.size() * sizeof(KRange)));
+  PM_HIP_CHECK(hipMemcpy(c.d_ktab, tab.data(), tab.size() * sizeof(KRange), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMalloc(&c.d_hseg, std::max<size_t>(1, hs.size()) * sizeof(HSeg)));
+  if (!hs.empty()) PM_HIP_CHECK(hipMemcpy(c.d_hseg, hs.data(), hs.size() * sizeof(HSeg), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMalloc(&c.d_hscr, std::max<size_t>(1, 3 * size_t(nheavy)) * sizeof(uint32_t)));
+  c.tmask_words = std::max<uint64_t>(1, uint64_t(tiles) * kSub);
+  PM_HIP_CHECK(hipMalloc(&c.d_tmask, c.tmask_words * sizeof(uint64_t)));
+  PM_HIP_CHECK(hipMalloc(&c.d_tbase, c.tmask_words * sizeof(uint64_t)));
+  c.scan_tmp_bytes = slist_scan_tmp_bytes(c.tmask_words);
+  PM_HIP_CHECK(hipMalloc(&c.d_scan_tmp, std::max<size_t>(1, c.scan_tmp_bytes)));
+  c.k1_grid = lcc_first_grid(c);
+}
+
+static K1Out k1_out(Ctx& c) {
+  return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mst, c.d_mlen, c.d_malive};
+}
+
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid) {
-#define PM_K1_ARGS                                                                                                 \
-  dim3(grid), dim3(kBlock), 0, c.stream, c.d_off, c.d_col, c.d_tl,                                                \
-      reinterpret_cast<const unsigned long long*>(c.d_tlbits), c.n, c.pa, owner_args(c), c.d_tst, c.d_tpub[c.cur], \
-      c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, reinterpret_cast<unsigned long long*>(c.d_cmask),                   \
-      reinterpret_cast<unsigned long long*>(c.d_part)
+  if (c.ntiles == 0) return;
+  if (c.nheavy) PM_HIP_CHECK(hipMemsetAsync(c.d_hscr, 0, 3 * size_t(c.nheavy) * sizeof(uint32_t), c.stream));
+#define PM_K1_ARGS                                                                                                    \
+  dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab, static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,     \
+      c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c), c.d_hscr, c.nheavy,                                  \
+      reinterpret_cast<unsigned long long*>(c.d_tmask), reinterpret_cast<unsigned long long*>(c.d_part)
   switch (variant) {
-    case 0: hipLaunchKernelGGL(k_lcc_first<0>, PM_K1_ARGS); break;
+    case 0:
+      if (c.k1_wide) hipLaunchKernelGGL((k_lcc_first<0, true>), PM_K1_ARGS);
+      else hipLaunchKernelGGL(k_lcc_first<0>, PM_K1_ARGS);
+      break;
     case 1: hipLaunchKernelGGL(k_lcc_first<1>, PM_K1_ARGS); break;
     case 2: hipLaunchKernelGGL(k_lcc_first<2>, PM_K1_ARGS); break;
-    case 3: hipLaunchKernelGGL(k_lcc_first<3>, PM_K1_ARGS); break;
     case 4: hipLaunchKernelGGL(k_lcc_first<4>, PM_K1_ARGS); break;
-    case 7: hipLaunchKernelGGL(k_lcc_first<7>, PM_K1_ARGS); break;
-    case 8: hipLaunchKernelGGL((k_lcc_first<0, 4>), PM_K1_ARGS); break;
-    case 9: hipLaunchKernelGGL((k_lcc_first<0, 16>), PM_K1_ARGS); break;
-    case 16: hipLaunchKernelGGL(k_lcc_first_lpr<0>, PM_K1_ARGS); break;
-    case 17: hipLaunchKernelGGL(k_lcc_first_lpr<1>, PM_K1_ARGS); break;
+    case 8: hipLaunchKernelGGL(k_lcc_first<8>, PM_K1_ARGS); break;
+    case 10: hipLaunchKernelGGL(k_lcc_first<10>, PM_K1_ARGS); break;
+    case 12: hipLaunchKernelGGL(k_lcc_first<12>, PM_K1_ARGS); break;
     default: throw std::runtime_error("unknown superstep-0 kernel variant");
   }
 #undef PM_K1_ARGS
   PM_HIP_CHECK(hipGetLastError());
 }
 
+// Persistent grid: the resident blocks of the whole chip (occupancy query),
+// never more waves than tiles.
 unsigned lcc_first_grid(const Ctx& c) {
-  return grid_for((c.n + kWave - 1) / kWave, kWpb, c.k1_resident_blocks ? c.k1_resident_blocks : kMaxGrid);
-}
-
-// Resident 256-thread blocks of the superstep-0 kernel on the whole chip
-// (occupancy query minus one block per CU: the API over-reports by one for
-// SGPR-heavy 256-thread kernels, MI355X_MICROARCH.md "Residency").
-unsigned query_k1_resident_blocks(int device) {
   int per_cu = 0;
   PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lcc_first<0>, kBlock, 0));
   hipDeviceProp_t prop;
-  PM_HIP_CHECK(hipGetDeviceProperties(&prop, device));
-  per_cu = std::max(1, per_cu - 1);
-  return static_cast<unsigned>(per_cu * prop.multiProcessorCount);
+  PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
+  const uint64_t cap = std::min<uint64_t>(kPartGridMax, uint64_t(std::max(per_cu, 1)) * prop.multiProcessorCount);
+  return grid_for(c.ntiles, kWpb, static_cast<unsigned>(cap));
 }
 
 void launch_lcc_first(Ctx& c, uint64_t* d_slot) {
-  const uint64_t chunks = (c.n + kWave - 1) / kWave;
-  const unsigned grid = lcc_first_grid(c);
+  if (c.ntiles == 0) {
+    PM_HIP_CHECK(hipMemsetAsync(d_slot, 0, slot_words(c) * sizeof(uint64_t), c.stream));
+    PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
+    return;
+  }
+  const unsigned grid = c.k1_grid;
   launch_lcc_first_kernel(c, 0, grid);
   reduce_into(c, grid, d_slot);
-  // slist = survivors in id order
+  // slist = survivors in label-major row order
   hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(
-      reinterpret_cast<const unsigned long long*>(c.d_cmask), PopcOp());
+      reinterpret_cast<const unsigned long long*>(c.d_tmask), PopcOp());
   size_t tmp = c.scan_tmp_bytes;
-  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_cbase, static_cast<int>(chunks), c.stream));
-  hipLaunchKernelGGL(k_slist_write, dim3(grid_for(chunks, kBlock, 4096)), dim3(kBlock), 0, c.stream,
-                     reinterpret_cast<const unsigned long long*>(c.d_cmask), c.d_cbase, chunks, c.d_slist, c.d_nS);
+  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_tbase, static_cast<int>(c.tmask_words),
+                                                c.stream));
+  hipLaunchKernelGGL(k_slist_write, dim3(grid_for(c.tmask_words, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_ktab,
+                     static_cast<uint32_t>(c.ktab.size() - 1), c.d_hseg,
+                     reinterpret_cast<const unsigned long long*>(c.d_tmask), c.d_tbase, c.tmask_words, c.d_slist,
+                     c.d_nS);
   PM_HIP_CHECK(hipGetLastError());
 }
 
-size_t slist_scan_tmp_bytes(uint64_t n) {
-  const uint64_t chunks = (n + kWave - 1) / kWave;
+size_t slist_scan_tmp_bytes(uint64_t words) {
   hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(nullptr, PopcOp());
   size_t tmp = 0;
   PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, static_cast<uint64_t*>(nullptr),
-                                                static_cast<int>(std::max<uint64_t>(chunks, 1)), hipStream_t(0)));
+                                                static_cast<int>(std::max<uint64_t>(words, 1)), hipStream_t(0)));
   return tmp;
 }
 
 void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   const unsigned grid = grid_for(chunks, kWpb, kMaxGrid);
-  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_off, c.d_slist, c.d_nS,
+  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mst, c.d_mlen,
                      c.d_malive, reinterpret_cast<unsigned long long*>(c.d_part));
   PM_HIP_CHECK(hipGetLastError());
@@ -832,7 +1208,7 @@ __global__ void k_mark_sources(const uint32_t* __restrict__ sources, const int* 
 
 // Number of alive entries of M[u] (excluding `skip`) -> outputs per item.
 __global__ void k_row_alive(const uint32_t* __restrict__ items, uint64_t nitems, int stride, int pos,
-                            const uint64_t* __restrict__ off, const uint32_t* __restrict__ malive,
+                            const uint64_t* __restrict__ offp, const uint32_t* __restrict__ malive,
                             uint32_t* __restrict__ out) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nitems; i += uint64_t(gridDim.x) * blockDim.x)
     out[i] = malive[items[i * stride + pos]];
@@ -840,13 +1216,13 @@ __global__ void k_row_alive(const uint32_t* __restrict__ items, uint64_t nitems,
 
 // Level-1 tokens of path/cycle lines: (v, s, parent = s) for v in M[s].
 __global__ void k_tp_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
-                          const uint64_t* __restrict__ off, const uint32_t* __restrict__ mcol,
+                          const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
                           const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
                           uint32_t* __restrict__ tu, uint32_t* __restrict__ ts, uint32_t* __restrict__ tp) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
     uint64_t o = obase[i];
-    const uint64_t b = off[s], L = mlen[s];
+    const uint64_t b = offp[s], L = mlen[s];
     for (uint64_t e = b; e < b + L; ++e) {
       if (!(mst[e] & 1u)) continue;
       tu[o] = mcol[e];
@@ -910,7 +1286,7 @@ __global__ void k_tp_unique(const unsigned long long* __restrict__ keys, const u
 
 // Expansion count: alive entries of M[u] other than the excluded parent.
 __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, const uint32_t* __restrict__ fx,
-                                  uint64_t nf, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mcol,
+                                  uint64_t nf, const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
                                   const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
                                   const uint32_t* __restrict__ malive, uint32_t* __restrict__ cnt,
                                   unsigned long long* __restrict__ trav) {
@@ -918,7 +1294,7 @@ __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, con
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nf; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = static_cast<uint32_t>(fk[i] & 0xFFFFFFFFull);
     const uint32_t x = fx[i];
-    const uint64_t b = off[u], L = mlen[u];
+    const uint64_t b = offp[u], L = mlen[u];
     uint32_t c = 0;
     for (uint64_t e = b; e < b + L; ++e)
       if ((mst[e] & 1u) && mcol[e] != x) ++c;
@@ -929,7 +1305,7 @@ __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, con
 }
 
 __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, const uint32_t* __restrict__ fx,
-                                  uint64_t nf, const uint64_t* __restrict__ obase, const uint64_t* __restrict__ off,
+                                  uint64_t nf, const uint64_t* __restrict__ obase, const uint64_t* __restrict__ offp,
                                   const uint32_t* __restrict__ mcol, const uint8_t* __restrict__ mst,
                                   const uint32_t* __restrict__ mlen, uint32_t* __restrict__ tu,
                                   uint32_t* __restrict__ ts, uint32_t* __restrict__ tp) {
@@ -938,7 +1314,7 @@ __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, con
     const uint32_t s = static_cast<uint32_t>(fk[i] >> 32);
     const uint32_t x = fx[i];
     uint64_t o = obase[i];
-    const uint64_t b = off[u], L = mlen[u];
+    const uint64_t b = offp[u], L = mlen[u];
     for (uint64_t e = b; e < b + L; ++e) {
       if (!(mst[e] & 1u)) continue;
       const uint32_t w = mcol[e];
@@ -955,9 +1331,10 @@ __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, con
 // walk does not end on it; cycle -> mark the source and the closing edge.
 __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts,
                               const uint32_t* __restrict__ tp, uint64_t ntok, LineArgs la,
-                              const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ off,
+                              const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
                               const uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst,
-                              const uint32_t* __restrict__ mlen, uint8_t* __restrict__ tsm) {
+                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ perm,
+                              uint8_t* __restrict__ tsm) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntok; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = tu[i], s = ts[i];
     if (!pos_ok(tpub[u], la.C + 1, la)) continue;
@@ -967,14 +1344,14 @@ __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* _
     } else {
       if (u != s) continue;
       tsm[s] = 2;
-      // mark M[s][parent] (rows are sorted by neighbour id)
-      const uint32_t p = tp[i];
-      uint64_t lo = off[s], hi = off[s] + mlen[s];
+      // mark M[s][parent]: rows hold positions in neighbour-id order
+      const uint32_t p = tp[i], pid = perm[p];
+      uint64_t lo = offp[s], hi = offp[s] + mlen[s];
       while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (mcol[mid] < p) lo = mid + 1; else hi = mid;
+        if (perm[mcol[mid]] < pid) lo = mid + 1; else hi = mid;
       }
-      if (lo < off[s] + mlen[s] && mcol[lo] == p && (mst[lo] & 1u)) mst[lo] = 3;
+      if (lo < offp[s] + mlen[s] && mcol[lo] == p && (mst[lo] & 1u)) mst[lo] = 3;
     }
   }
 }
@@ -994,13 +1371,13 @@ __device__ __forceinline__ bool enum_ok(const uint32_t* w, int pos, uint32_t v, 
 }
 
 __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
-                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ mcol,
+                           const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
                            const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen, int stride,
                            uint32_t* __restrict__ walks) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
     uint64_t o = obase[i];
-    const uint64_t b = off[s], L = mlen[s];
+    const uint64_t b = offp[s], L = mlen[s];
     for (uint64_t e = b; e < b + L; ++e) {
       if (!(mst[e] & 1u)) continue;
       walks[o * stride + 0] = s;
@@ -1014,7 +1391,7 @@ __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, 
 // neighbour.  pass 0 counts, pass 1 writes.
 template <int PASS>
 __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int k, int stride, LineArgs la,
-                             const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ off,
+                             const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
                              const uint32_t* __restrict__ mcol, const uint8_t* __restrict__ mst,
                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive,
                              uint32_t* __restrict__ cnt, const uint64_t* __restrict__ obase,
@@ -1026,7 +1403,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
     uint32_t c = 0;
     if (pos_ok(tpub[u], k, la) && enum_ok(w, k, u, la)) {
       const uint32_t s = w[0];
-      const uint64_t b = off[u], L = mlen[u];
+      const uint64_t b = offp[u], L = mlen[u];
       uint64_t o = PASS ? obase[i] : 0;
       for (uint64_t e = b; e < b + L; ++e) {
         if (!(mst[e] & 1u)) continue;
@@ -1170,14 +1547,14 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
   auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
   hipLaunchKernelGGL(k_row_alive, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, 1, 0, c.d_off, c.d_malive, cnt);
+                     c.nsources, 1, 0, c.d_offp, c.d_malive, cnt);
   uint64_t ntok = exclusive_scan_u32_to_u64(c, cnt, obase, c.nsources);
   uint64_t trav_init = ntok;  // sources scan all of M[s]
   auto* tu = arena_alloc<uint32_t>(c, ntok);
   auto* ts = arena_alloc<uint32_t>(c, ntok);
   auto* tp = arena_alloc<uint32_t>(c, ntok);
   hipLaunchKernelGGL(k_tp_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
+                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += ntok;
   SeenSet seen{};
@@ -1223,21 +1600,21 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     }
     auto* ecnt = arena_alloc<uint32_t>(c, nf);
     hipLaunchKernelGGL(k_tp_expand_count, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf,
-                       c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, ecnt, d_trav);
+                       c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, ecnt, d_trav);
     auto* eb = arena_alloc<uint64_t>(c, nf + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, ecnt, eb, nf);
     tu = arena_alloc<uint32_t>(c, nnext);
     ts = arena_alloc<uint32_t>(c, nnext);
     tp = arena_alloc<uint32_t>(c, nnext);
     hipLaunchKernelGGL(k_tp_expand_write, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf, eb,
-                       c.d_off, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
+                       c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
     PM_HIP_CHECK(hipGetLastError());
     ntok = nnext;
     res.tokens += ntok;
   }
   if (ntok > 0) {
     hipLaunchKernelGGL(k_tp_terminal, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
-                       la, tpub, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_tsm);
+                       la, tpub, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_perm, c.d_tsm);
     PM_HIP_CHECK(hipGetLastError());
   }
   unsigned long long trav = 0;
@@ -1267,25 +1644,25 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
   auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
   hipLaunchKernelGGL(k_row_alive, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, 1, 0, c.d_off, c.d_malive, cnt);
+                     c.nsources, 1, 0, c.d_offp, c.d_malive, cnt);
   uint64_t nw = exclusive_scan_u32_to_u64(c, cnt, obase, c.nsources);
   const uint64_t trav_init = nw;
   auto* walks = arena_alloc<uint32_t>(c, nw * stride);
   hipLaunchKernelGGL(k_tds_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, stride, walks);
+                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, stride, walks);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += nw;
   for (int k = 1; k <= C && nw > 0; ++k) {
     auto* wc = arena_alloc<uint32_t>(c, nw);
     hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                       stride, la, tpub, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc,
+                       stride, la, tpub, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc,
                        static_cast<const uint64_t*>(nullptr), static_cast<uint32_t*>(nullptr), d_trav);
     auto* wb = arena_alloc<uint64_t>(c, nw + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
     auto* wn = arena_alloc<uint32_t>(c, nnext * stride);
     if (nnext) {
       hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                         stride, la, tpub, c.d_off, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
+                         stride, la, tpub, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
       PM_HIP_CHECK(hipGetLastError());
     }
     walks = wn;

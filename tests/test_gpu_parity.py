@@ -96,6 +96,32 @@ def test_duplicate_edges_and_self_loops(tmp_path):
     assert sg["lcc_edges"] == so["lcc_edges"]
 
 
+def test_heavy_rows_segment_boundaries(tmp_path):
+    # Two hubs of degree > 1024 (split into 1024-entry segments by superstep 0)
+    # with duplicate entries straddling the segment boundary, plus rows of
+    # 65..1024 entries.  Cycle pattern labels: A=3, leaves 4, C=5, closers 6.
+    n_leaf, n_close = 1100, 3
+    A, C = 0, 1
+    leaves = list(range(2, 2 + n_leaf))
+    closers = list(range(2 + n_leaf, 2 + n_leaf + n_close))
+    pairs = [(A, v) for v in leaves] + [(C, v) for v in leaves]
+    pairs += [(A, v) for v in leaves[1000:1050]] * 2  # multiplicity across entry 1024 of A's row
+    pairs += [(C, w) for w in closers] + [(A, w) for w in closers]
+    mid = 2 + n_leaf + n_close  # a row of 200 entries (65..1024 class)
+    pairs += [(mid, v) for v in leaves[:200]]
+    n = mid + 1
+    labels = np.zeros(n, np.uint64)
+    labels[A], labels[C] = 3, 5
+    labels[leaves] = 4
+    labels[closers] = 6
+    labels[mid] = 3
+    off, col = pmtest.symmetric_csr(pairs, n)
+    so, sg, diffs = _run_both(off, col, PATTERNS["cycle"], tmp_path, labels)
+    assert diffs == []
+    assert sg["lcc_edges"] == so["lcc_edges"] and sg["tds_edges"] == so["tds_edges"]
+    assert sg["walks"] == so["paths"] and sg["walks"] > 0
+
+
 def test_step_api_matches_driver():
     g = pm.rmat_graph(12, 4)
     labels = pmtest.hash_labels(g.n, 8)

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 SCALE=${SCALE:-22}
 VAR=${VAR:-0}
 i=0
-for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr"; do
+for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT" "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-include-regex "k_lcc_first" --output-format csv \
     -d gpurun_out/sq_$i -o run -- python3 tools/ubench.py $SCALE $VAR > gpurun_out/sq_$i.log 2>&1
