@@ -11,6 +11,7 @@
 #include <bitset>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -122,6 +123,7 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   arena = std::max<size_t>(arena, size_t(64) << 20);
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
+  if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
   // default labels = degree labels; the id-major adjacency is staged in the
   // M column buffer and permuted into the label-major d_colp
   PM_HIP_CHECK(hipMemcpy(c->d_mcol, g->col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -143,6 +145,8 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  free_line_buffers(*c);
+  for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -191,22 +195,26 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   const uint64_t W = slot_words(c);
   const uint64_t P = c.nranks <= 1 ? 1 : c.nranks;
   ensure_counts(c, D);
-  std::vector<hipEvent_t> ev(D + 1);
-  for (auto& e : ev) PM_HIP_CHECK(hipEventCreate(&e));
+  while (c.events.size() < D + 3) {
+    hipEvent_t e;
+    PM_HIP_CHECK(hipEventCreate(&e));
+    c.events.push_back(e);
+  }
+  std::vector<hipEvent_t>& ev = c.events;  // [0..D] superstep bounds, [D+1], [D+2] superstep-0 kernel
   PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
-  hipEvent_t k_beg = nullptr, k_end = nullptr;
+  bool k_timed = false;
   for (uint64_t ss = 0; ss < D; ++ss) {
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
       PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
-      PM_HIP_CHECK(hipEventCreate(&k_beg));
-      PM_HIP_CHECK(hipEventCreate(&k_end));
-      PM_HIP_CHECK(hipEventRecord(k_beg, c.stream));
+      PM_HIP_CHECK(hipEventRecord(ev[D + 1], c.stream));
       launch_lcc_first(c, slot);
-      PM_HIP_CHECK(hipEventRecord(k_end, c.stream));
-      PM_HIP_CHECK(hipMemcpyAsync(&c.nS_host, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-      PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+      PM_HIP_CHECK(hipEventRecord(ev[D + 2], c.stream));
+      k_timed = true;
+      // |slist| is read back with the counters at the end of the call; until
+      // then later supersteps size their grids by its upper bound
+      c.nS_host = static_cast<uint32_t>(std::min<uint64_t>(c.ss0_rows, 0xFFFFFFFFull));
       c.lcc_started = true;
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
@@ -214,9 +222,12 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     }
     PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
+  uint32_t nS = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&nS, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
   std::vector<uint64_t> host(D * W);
   PM_HIP_CHECK(hipMemcpyAsync(host.data(), c.d_counts, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.nS_host = nS;
   LccOut out;
   bool asym = false;
   for (uint64_t ss = 0; ss < D; ++ss) {
@@ -242,14 +253,11 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     out.seconds.push_back(ms * 1e-3);
     c.device_seconds += ms * 1e-3;
   }
-  if (k_beg) {
+  if (k_timed) {
     float ms = 0.f;
-    PM_HIP_CHECK(hipEventElapsedTime(&ms, k_beg, k_end));
+    PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[D + 1], ev[D + 2]));
     c.lcc_first_ms = ms;
-    (void)hipEventDestroy(k_beg);
-    (void)hipEventDestroy(k_end);
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
   if (asym)
     throw std::runtime_error(
         "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message); "
@@ -373,6 +381,10 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
   };
   bool init_step = true, nf = false, terminated = true;
+  // PM_PHASE_TIMES=1: per-phase host wall time on stderr (diagnostics)
+  const bool phase_times = std::getenv("PM_PHASE_TIMES") != nullptr;
+  double ph_lcc = 0, ph_tp = 0, ph_post = 0, ph_count = 0;
+  auto tick = [] { return std::chrono::steady_clock::now(); };
   uint64_t itr = 0;
   uint64_t first_scanned = 0, first_surv = 0, first_edges = 0, first_matching = 0;
   uint64_t last_v = 0, last_e = 0;
@@ -382,12 +394,16 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     for (auto x : vc) last_v += x;
     for (auto x : ec) last_e += x;
   };
+  // active vertex / edge counts per rank after the latest step
+  std::vector<uint64_t> cur_vc(c.nranks, 0), cur_ec(c.nranks, 0);
   auto record_lcc = [&](const LccOut& lo, uint64_t itr_) {
     for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
       f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
       add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
       s.lcc_edges += lo.trav[ss];
       totals(lo.vcount[ss], lo.ecount[ss]);
+      cur_vc = lo.vcount[ss];
+      cur_ec = lo.ecount[ss];
     }
   };
   do {
@@ -399,7 +415,9 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     const auto t_itr = std::chrono::steady_clock::now();
     const auto t_lp = std::chrono::steady_clock::now();
     const bool was_init = init_step;
+    auto t0 = tick();
     LccOut lo = lcc_call(c, init_step);
+    ph_lcc += since(t0);
     if (was_init) {
       first_scanned = lo.trav[0];
       first_matching = lo.matching_rows;
@@ -418,13 +436,43 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         for (auto& r : subgraphs[pl]) r.clear();  // reopened with truncation (beta.cpp:713-717)
         const auto t_tp = std::chrono::steady_clock::now();
         TpResult tr;
-        if (pl >= 4) {  // beta.cpp:762-767
-          std::vector<uint32_t> walks;
-          uint32_t stride = 0;
-          tr = run_tds_line(c, line, walks, stride);
+        uint32_t deleted = 0;
+        std::vector<uint64_t> vc, ec;
+        std::vector<uint32_t> walks;
+        uint32_t stride = 0;
+        FusedLineOut fo;
+        auto t1 = tick();
+        if (c.fused_lines && run_line_fused(c, pl, files, fo)) {
+          tr = fo.tr;
+          deleted = fo.deleted;
+          vc = cur_vc;
+          ec = cur_ec;
+          for (uint32_t r = 0; r < c.nranks; ++r) {
+            vc[r] -= fo.rm_v[r];
+            ec[r] -= fo.rm_e[r];
+          }
+          walks.swap(fo.walks);
+          stride = fo.stride;
+          ph_tp += since(t1);
+        } else {
+          // exact-count path (one launch + sync per position)
+          if (pl >= 4) {  // beta.cpp:762-767
+            tr = run_tds_line(c, line, walks, stride);
+          } else {
+            tr = run_path_line(c, line);
+          }
+          ph_tp += since(t1);
+          auto t2 = tick();
+          deleted = launch_post_tp(c, line);
+          ph_post += since(t2);
+          auto t3 = tick();
+          count_state(c, vc, ec);
+          ph_count += since(t3);
+        }
+        if (pl >= 4) {
           s.tds_edges += tr.edges;
           s.walks = tr.walks;
-          for (uint64_t i = 0; i < tr.walks; ++i) {
+          for (uint64_t i = 0; i < walks.size() / std::max<uint32_t>(stride, 1); ++i) {
             const uint32_t* w = walks.data() + i * stride;  // positions
             const uint32_t last = c.perm_host[w[stride - 1]];
             const uint32_t r = owner_host(c, last);
@@ -434,16 +482,14 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
             subgraphs[pl][r].push_back(std::move(l));
           }
         } else {
-          tr = run_path_line(c, line);
           s.nlcc_edges += tr.edges;
         }
-        const uint32_t deleted = launch_post_tp(c, line);
         if (deleted) nf = true;
         f.superstep.push_back(std::to_string(itr) + ", TP, " + std::to_string(pl) + ", " + fmt_double(since(t_tp)));
-        std::vector<uint64_t> vc, ec;
-        count_state(c, vc, ec);
         add_count_lines(c, f, itr, "TP", pl, vc, ec, tr.edges);
         totals(vc, ec);
+        cur_vc = vc;
+        cur_ec = ec;
         if (deleted && line.interleave_lp) {  // beta.cpp:1163-1197
           const auto t_lpi = std::chrono::steady_clock::now();
           LccOut li = lcc_call(c, false);
@@ -460,6 +506,9 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   } while (nf);
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   const double secs = since(t_pattern);
+  if (phase_times)
+    std::fprintf(stderr, "[pm] run_beta %.3f ms: lcc %.3f, token passing %.3f, post %.3f, counts %.3f, device %.3f\n",
+                 secs * 1e3, ph_lcc * 1e3, ph_tp * 1e3, ph_post * 1e3, ph_count * 1e3, c.device_seconds * 1e3);
   s.iterations = itr;
   s.terminated = terminated ? 1 : 0;
   s.seconds = secs;

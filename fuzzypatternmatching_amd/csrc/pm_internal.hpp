@@ -107,6 +107,15 @@ __host__ __device__ inline uint64_t padded_degree(uint64_t d) {
   return g;
 }
 
+// Outputs of one fused NLC-line kernel (pm_lines.hip), device resident.
+struct LineStats {
+  unsigned long long nsrc, trav, tokens, acked, deleted, walks, ftotal;
+  unsigned long long wn[20];    // TDS walks per position (1..C+1)
+  unsigned long long wbase[20]; // TDS: slot offset of each position's walks
+  unsigned int overflow, pad;
+  unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -171,8 +180,19 @@ struct Ctx {
   size_t counts_slots = 0;
 
   Arena arena;
+  std::vector<hipEvent_t> events;  // LCC call timing, created once
   uint32_t nS_host = 0;     // size of d_slist (host copy, valid after superstep 0)
   bool lcc_started = false; // superstep 0 of the first call done
+
+  // fused NLC lines (pm_lines.hip)
+  LineStats* d_lstats = nullptr;
+  unsigned long long* d_hkey = nullptr;  // (source, vertex) hash table, persistent
+  unsigned long long* d_hval = nullptr;
+  uint64_t hcap = 0;
+  uint32_t* d_front = nullptr;    // slots inserted by a fused path line (cleared by it)
+  unsigned* d_gbar = nullptr;     // grid barrier state of the fused line kernels
+  unsigned line_grid = 0;
+  bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
 
   // last token-passing call
   uint32_t* d_sources = nullptr;
@@ -211,6 +231,22 @@ struct TpResult {
   uint64_t sources = 0, acked = 0, edges = 0, tokens = 0, walks = 0;
 };
 TpResult run_path_line(Ctx& c, const NlcLine& line);
+// One fused kernel per line (token passing + post-processing).  Returns false
+// when a capacity overflowed (no terminal or post effect has happened;
+// c.nsources names the marked sources): the caller reruns the line through
+// run_path_line / run_tds_line, launch_post_tp and count_state.  Otherwise
+// rm_v / rm_e are the vertices / edges per rank that left S in
+// post-processing (the active counts after the line are the counts before it
+// minus these: token passing itself changes neither T_pub nor |M|).
+struct FusedLineOut {
+  TpResult tr;
+  uint32_t deleted = 0;
+  std::vector<uint64_t> rm_v, rm_e;
+  std::vector<uint32_t> walks;  // kept TDS walks (positions), when requested
+  uint32_t stride = 0;
+};
+bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out);
+void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);
 

@@ -1,0 +1,653 @@
+// Fused token passing: one cooperative kernel per NLC line.
+//
+// The level-synchronous formulation of pm_kernels.hip ("Token passing")
+// executed as a single grid-wide kernel whose phases are separated by grid
+// barriers, so a line costs one launch and one host synchronisation instead of
+// a launch + sync per position:
+//   P1 source selection over slist (nem_1.hpp:387-479 / tds_batch_1.hpp:1067-1135)
+//      fused with the position-1 tokens of each selected source
+//   P2.. one phase per walk position (nem_1.hpp:131-297, :540-791 /
+//      tds_batch_1.hpp:284-302, :622-758)
+//   Pp post-processing of unacked sources (beta.cpp:964-1000), reporting the
+//      vertices / edges that leave S per rank (the active counts after the
+//      line follow from the counts before it), and hash-slot cleanup
+// Barriers: C + 1 per path line, C + 2 per TDS line (tree_barrier: a
+// two-level arrival counter, ~6 us at one 1024-thread block per CU against
+// ~30 us for cooperative_groups grid.sync, tools/ubench_src/coop_barrier.hip).
+//
+// Path / cycle lines (nem_1) deduplicate (source, vertex) arrivals in an
+// open-addressing hash table: value = (position << 32) | parent, the parent
+// turning into kMulti when a second distinct parent arrives at the same
+// position -- the rule of the sort-based path (lowest position wins; a single
+// parent is excluded from forwarding, several parents exclude none).
+// Capacities are fixed per call; an overflow is detected before any terminal
+// effect and the caller reruns the line through the exact-count path.
+// Stale token-source-map entries need no cleanup: only sources are read in
+// post-processing and P1 resets every source's entry.
+//
+// Memory ordering: phases exchange data through global memory across CUs.
+// Reads of data written by another CU in an earlier phase whose cache line
+// this CU may already hold (frontier lists, hash slots, source list) go
+// through ld_acq (L1-bypassing atomic loads); TDS walk regions are fresh,
+// 128-B aligned memory per position.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "pm_device.hpp"
+#include "pm_internal.hpp"
+
+namespace pm {
+
+static constexpr unsigned long long kEmpty = ~0ull;
+static constexpr uint32_t kMulti = 0xFFFFFFFEu;
+static constexpr int kMaxProbe = 128;
+
+template <typename T>
+__device__ __forceinline__ T ld_acq(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+struct LineKernelArgs {
+  // graph / state (positions)
+  const uint64_t* offp;
+  const uint32_t* mcol;
+  uint8_t* mst;
+  const uint32_t* mlen;
+  const uint32_t* malive;
+  uint16_t* tpub;
+  const uint32_t* perm;
+  uint8_t* tsm;
+  const uint32_t* slist;
+  const uint32_t* nS;
+  uint32_t* sources;
+  OwnerArgs oa;
+  LineArgs la;
+  int i0;  // pattern_indices[0] (post-processing bit)
+  unsigned* gbar;  // grid barrier state
+  // hash table (path lines), persistent, clean between lines
+  unsigned long long* hkey;
+  unsigned long long* hval;
+  uint64_t hmask;
+  uint32_t* front;  // inserted slots, position segments
+  uint64_t fcap;
+  // walk storage (TDS lines): positions laid out one after the other
+  uint32_t* wbuf;
+  uint64_t wcap;  // u32 slots
+  uint8_t* keep;  // terminal keep flags
+  uint64_t kcap;
+  LineStats* st;
+};
+
+// Wave-aggregated reservation of n slots on a global counter; returns the
+// lane's first slot.  All lanes of the wave must call it.
+__device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, uint32_t n) {
+  const uint64_t incl = wave_incl_scan(n);
+  const uint64_t total = __shfl(incl, kWave - 1, kWave);
+  unsigned long long base = 0;
+  if (lane_id() == 0 && total) base = atomicAdd(ctr, static_cast<unsigned long long>(total));
+  base = __shfl(base, 0, kWave);
+  return base + incl - n;
+}
+
+__device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
+  x = wave_sum(x);
+  if (lane_id() == 0 && x) atomicAdd(ctr, static_cast<unsigned long long>(x));
+}
+
+// Value update of hash slot h for an arrival at position `level` from
+// `parent`; true for the first arrival (the slot joins the position's frontier).
+__device__ __forceinline__ bool ht_arrive(unsigned long long* hval, uint64_t h, uint32_t level, uint32_t parent) {
+  const unsigned long long want = (static_cast<unsigned long long>(level) << 32) | parent;
+  unsigned long long old = ld_acq(&hval[h]);
+  while (true) {
+    if (old == kEmpty) {
+      const unsigned long long prev = atomicCAS(&hval[h], kEmpty, want);
+      if (prev == kEmpty) return true;
+      old = prev;
+      continue;
+    }
+    if ((old >> 32) < level) return false;  // reached at a lower position: dropped
+    const uint32_t par = static_cast<uint32_t>(old);
+    if (par == parent || par == kMulti) return false;
+    const unsigned long long prev =
+        atomicCAS(&hval[h], old, (static_cast<unsigned long long>(level) << 32) | kMulti);
+    if (prev == old) return false;
+    old = prev;
+  }
+}
+
+// Insert (s, u) at `level` from `parent`; returns the slot on a first
+// arrival, kEmpty otherwise (and on overflow, flagged in st).
+__device__ __forceinline__ uint64_t ht_insert(const LineKernelArgs& a, uint32_t s, uint32_t u, uint32_t level,
+                                              uint32_t parent) {
+  const unsigned long long key = (static_cast<unsigned long long>(s) << 32) | u;
+  uint64_t h = mix64(key) & a.hmask;
+  for (int probe = 0; probe < kMaxProbe; ++probe) {
+    unsigned long long k = ld_acq(&a.hkey[h]);
+    if (k == kEmpty) {
+      const unsigned long long prev = atomicCAS(&a.hkey[h], kEmpty, key);
+      k = prev == kEmpty ? key : prev;
+    }
+    if (k == key) return ht_arrive(a.hval, h, level, parent) ? h : kEmpty;
+    h = (h + 1) & a.hmask;
+  }
+  atomicOr(&a.st->overflow, 1u);
+  return kEmpty;
+}
+
+// Terminal position C+1 of a path / cycle line (nem_1.hpp:661-791).
+__device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t p) {
+  const LineArgs& la = a.la;
+  if (!pos_ok(a.tpub[u], la.C + 1, la)) return;
+  if (!la.VC) {
+    if (u == s) return;
+    if (a.tpub[s]) a.tsm[s] = 2;  // ack visitor needs an active source (nem_1.hpp:101, :326-336)
+  } else {
+    if (u != s) return;
+    a.tsm[s] = 2;
+    // mark M[s][p]: rows hold positions in neighbour-id order
+    const uint32_t pid = a.perm[p];
+    const uint64_t b = a.offp[s], e = b + a.mlen[s];
+    uint64_t lo = b, hi = e;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (a.perm[a.mcol[mid]] < pid) lo = mid + 1; else hi = mid;
+    }
+    if (lo < e && a.mcol[lo] == p && (a.mst[lo] & 1u)) a.mst[lo] = 3;
+  }
+}
+
+// Forwarding from u (token of source s at position k, excluded parent excl):
+// every alive w in M[u] other than excl goes to position k + 1 (terminal
+// action at C + 1, else arrival filter + hash insert).  All lanes of the wave
+// must call it; returns the lane's emitted token count.
+__device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t excl,
+                                               int k, bool active) {
+  uint32_t emitted = 0;
+  const LineArgs& la = a.la;
+  uint64_t b = 0, L = 0;
+  if (active) {
+    b = a.offp[u];
+    L = a.mlen[u];
+  }
+  uint64_t Lmax = L;
+  for (int d = kWave / 2; d > 0; d >>= 1) Lmax = max(Lmax, static_cast<uint64_t>(__shfl_xor(Lmax, d, kWave)));
+  for (uint64_t j = 0; j < Lmax; ++j) {
+    uint64_t slot = kEmpty;
+    if (j < L && (a.mst[b + j] & 1u)) {
+      const uint32_t w = a.mcol[b + j];
+      if (w != excl) {
+        ++emitted;
+        if (k + 1 == la.C + 1) {
+          tp_terminal(a, w, s, u);
+        } else if (w != s && pos_ok(a.tpub[w], k + 1, la)) {
+          slot = ht_insert(a, s, w, static_cast<uint32_t>(k + 1), u);
+        }
+      }
+    }
+    const uint32_t is_new = slot != kEmpty ? 1u : 0u;
+    if (__ballot(is_new)) {
+      const uint64_t pos = wave_reserve(&a.st->ftotal, is_new);
+      if (is_new) {
+        if (pos < a.fcap) a.front[pos] = static_cast<uint32_t>(slot);
+        else atomicOr(&a.st->overflow, 1u);
+      }
+    }
+  }
+  return emitted;
+}
+
+// Grid barrier for co-resident blocks (cooperative launch): blocks arrive on
+// per-group counters (16 blocks, own 128-B lines), the last of a group on the
+// top counter, the last group bumps the generation word everyone waits on.
+// Counters reset themselves; the generation only grows.
+__device__ __forceinline__ void tree_barrier(unsigned* bar) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nb = gridDim.x;
+    const unsigned ngroups = (nb + 15) / 16;
+    const unsigned grp = blockIdx.x / 16;
+    const unsigned gsize = min(16u, nb - grp * 16);
+    unsigned* gen = bar;
+    unsigned* top = bar + 32;
+    unsigned* gc = bar + 64 + grp * 32;
+    const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    if (atomicAdd(gc, 1u) == gsize - 1) {
+      __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (atomicAdd(top, 1u) == ngroups - 1) {
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) __builtin_amdgcn_s_sleep(1);
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  }
+  __syncthreads();
+}
+static constexpr unsigned kGbarWords = 64 + 32 * 64;  // up to 1024 blocks
+
+static constexpr int kLineBlock = 1024;
+struct GridIdx {
+  uint64_t tid, nth, gw, nw;
+};
+__device__ __forceinline__ GridIdx grid_idx() {
+  GridIdx g;
+  const uint32_t wpb = blockDim.x / kWave;
+  g.tid = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  g.nth = uint64_t(gridDim.x) * blockDim.x;
+  g.gw = blockIdx.x * uint64_t(wpb) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  g.nw = uint64_t(gridDim.x) * wpb;
+  return g;
+}
+
+// P1 for one 64-entry chunk of slist: returns the lane's source (ok) after
+// appending it to the source list and marking the token source map.
+__device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t i, uint32_t nS, bool tds,
+                                              uint32_t& s) {
+  bool ok = false;
+  s = 0;
+  if (i < nS) {
+    s = a.slist[i];
+    const uint16_t T = a.tpub[s];
+    ok = T && pos_ok(T, 0, a.la);
+    if (ok && !tds && !a.la.VC && !((T >> a.la.ilast) & 1u)) ok = false;
+  }
+  const uint64_t pos = wave_reserve(&a.st->nsrc, ok ? 1u : 0u);
+  if (ok) {
+    a.sources[pos] = s;
+    a.tsm[s] = 1;
+  }
+  return ok;
+}
+
+// Pp: post-processing of unacked sources (k_tp_post), reporting the vertices
+// and edges (|M|) per rank whose T_pub becomes empty.
+__device__ __forceinline__ void line_post(const LineKernelArgs& a, const GridIdx& g, unsigned long long* s_hist) {
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+  const uint64_t nsrc = ld_acq(&a.st->nsrc);
+  uint64_t acked = 0, deleted = 0, rv = 0, re = 0;
+  for (uint64_t i = g.tid; i < nsrc; i += g.nth) {
+    const uint32_t s = ld_acq(&a.sources[i]);
+    if (ld_acq(&a.tsm[s]) == 2) {
+      ++acked;
+      continue;
+    }
+    uint16_t T = a.tpub[s];
+    if (!T) continue;
+    if ((T >> a.i0) & 1u) {
+      T &= static_cast<uint16_t>(~(1u << a.i0));
+      a.tpub[s] = T;  // T == 0: vertex_active = false and erased from the state map
+      if (!T) {
+        if (a.oa.nranks <= 1) {
+          rv += 1;
+          re += a.malive[s];
+        } else {
+          acc_owner(s_hist, a.oa, s, a.malive[s]);
+        }
+      }
+    }
+    ++deleted;
+  }
+  wave_add(&a.st->acked, acked);
+  wave_add(&a.st->deleted, deleted);
+  if (a.oa.nranks <= 1) {
+    wave_add(&a.st->removed[0], rv);
+    wave_add(&a.st->removed[1], re);
+  } else {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 2 * a.oa.nranks; i += blockDim.x)
+      if (s_hist[i]) atomicAdd(&a.st->removed[i], s_hist[i]);
+  }
+}
+
+// ---- path / cycle lines (nem_1) ----------------------------------------
+__global__ __launch_bounds__(kLineBlock) void k_path_line(LineKernelArgs a) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  const GridIdx g = grid_idx();
+  LineStats* st = a.st;
+  uint64_t trav = 0, tokens = 0;
+  // P1 + position 1: (v, s, parent = s) for v in M[s]
+  const uint32_t nS = *a.nS;
+  for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
+    uint32_t s;
+    const bool ok = select_source(a, i0 + lane_id(), nS, false, s);
+    if (ok) trav += a.malive[s];
+    tokens += tp_forward(a, s, s, kNone, 0, ok);
+  }
+  tree_barrier(a.gbar);
+  uint64_t lo = 0;
+  for (int k = 1; k <= a.la.C; ++k) {
+    if (ld_acq(&st->overflow)) break;  // same value in every wave after the barrier
+    const uint64_t hi = ld_acq(&st->ftotal);
+    for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
+      const uint64_t i = i0 + lane_id();
+      const bool act = i < hi;
+      uint32_t s = 0, u = 0, excl = kNone;
+      if (act) {
+        const uint32_t h = ld_acq(&a.front[i]);
+        const unsigned long long key = ld_acq(&a.hkey[h]);
+        const uint32_t par = static_cast<uint32_t>(ld_acq(&a.hval[h]));
+        s = static_cast<uint32_t>(key >> 32);
+        u = static_cast<uint32_t>(key);
+        excl = par == kMulti ? kNone : par;
+        trav += a.malive[u];
+      }
+      tokens += tp_forward(a, u, s, excl, k, act);
+    }
+    lo = hi;
+    tree_barrier(a.gbar);
+  }
+  wave_add(&st->trav, trav);
+  wave_add(&st->tokens, tokens);
+  if (ld_acq(&st->overflow)) return;  // every block returns; the host clears the table
+  line_post(a, g, s_hist);
+  // hash cleanup: no insert happens after the last barrier
+  const uint64_t nf = ld_acq(&st->ftotal);
+  for (uint64_t i = g.tid; i < nf; i += g.nth) {
+    const uint32_t h = ld_acq(&a.front[i]);
+    a.hkey[h] = kEmpty;
+    a.hval[h] = kEmpty;
+  }
+}
+
+// ---- TDS lines (tds_batch_1) -------------------------------------------
+// Walks of position L (L+1 vertices) are stored from st->wbase[L] on, stride
+// C+2 u32, each position in fresh memory (no cache line is reused across
+// phases).  Sender-side checks follow k_tds_expand.
+__device__ __forceinline__ uint32_t tds_children(const LineKernelArgs& a, const uint32_t* w, int k, uint64_t b,
+                                                 uint64_t L, uint32_t* out, int stride) {
+  const LineArgs& la = a.la;
+  const uint32_t s = w[0];
+  uint32_t c = 0;
+  for (uint64_t e = b; e < b + L; ++e) {
+    if (!(a.mst[e] & 1u)) continue;
+    const uint32_t nb = a.mcol[e];
+    if (k == la.C) {
+      if (la.VC) {
+        if (nb != s) continue;
+      } else {
+        if (nb == s) continue;
+        if (!enum_ok(w, k + 1, nb, la)) continue;
+      }
+    } else {
+      if (!enum_ok(w, k + 1, nb, la)) continue;
+    }
+    if (out) {
+      uint32_t* d = out + uint64_t(c) * stride;
+      for (int p = 0; p <= k; ++p) d[p] = w[p];
+      d[k + 1] = nb;
+    }
+    ++c;
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(kLineBlock) void k_tds_line(LineKernelArgs a) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  const GridIdx g = grid_idx();
+  LineStats* st = a.st;
+  const LineArgs& la = a.la;
+  const int stride = la.C + 2;
+  uint64_t trav = 0, tokens = 0;
+  // P1 + position 1 walks [s, w]; region 1 starts at slot 0
+  const uint32_t nS = *a.nS;
+  for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
+    uint32_t s;
+    const bool ok = select_source(a, i0 + lane_id(), nS, true, s);
+    uint32_t cnt = 0;
+    uint64_t b = 0, L = 0;
+    if (ok) {
+      b = a.offp[s];
+      L = a.mlen[s];
+      cnt = a.malive[s];
+      trav += cnt;
+    }
+    const uint64_t pos = wave_reserve(&st->wn[1], cnt);
+    if (cnt) {
+      if ((pos + cnt) * stride <= a.wcap) {
+        uint64_t o = pos;
+        for (uint64_t e = b; e < b + L; ++e) {
+          if (!(a.mst[e] & 1u)) continue;
+          a.wbuf[o * stride + 0] = s;
+          a.wbuf[o * stride + 1] = a.mcol[e];
+          ++o;
+        }
+      } else {
+        atomicOr(&st->overflow, 1u);
+      }
+    }
+  }
+  tree_barrier(a.gbar);
+  uint64_t in_base = 0;
+  for (int k = 1; k <= la.C; ++k) {
+    if (ld_acq(&st->overflow)) break;
+    const uint64_t nin = ld_acq(&st->wn[k]);
+    // next region: 32-slot (128 B) aligned after this one (fresh cache lines)
+    const uint64_t out_base = (in_base + nin * stride + 31) & ~uint64_t(31);
+    if (g.tid == 0) {
+      st->wbase[k] = in_base;
+      st->wbase[k + 1] = out_base;
+    }
+    tokens += g.tid == 0 ? nin : 0;
+    const uint32_t* win = a.wbuf + in_base;
+    for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
+      const uint64_t i = i0 + lane_id();
+      const bool act = i < nin;
+      const uint32_t* w = win + (act ? i : 0) * stride;
+      uint32_t cnt = 0;
+      uint64_t b = 0, L = 0;
+      if (act) {
+        const uint32_t u = w[k];
+        if (pos_ok(a.tpub[u], k, la) && enum_ok(w, k, u, la)) {
+          b = a.offp[u];
+          L = a.mlen[u];
+          trav += a.malive[u];
+          cnt = tds_children(a, w, k, b, L, nullptr, stride);
+        }
+      }
+      const uint64_t pos = wave_reserve(&st->wn[k + 1], cnt);
+      if (cnt) {
+        if (out_base + (pos + cnt) * stride <= a.wcap)
+          tds_children(a, w, k, b, L, a.wbuf + out_base + pos * stride, stride);
+        else
+          atomicOr(&st->overflow, 1u);
+      }
+    }
+    in_base = out_base;
+    tree_barrier(a.gbar);
+  }
+  // terminal keep flags must fit before any terminal effect happens
+  if (ld_acq(&st->overflow) || ld_acq(&st->wn[la.C + 1]) > a.kcap) {
+    if (g.tid == 0) atomicOr(&st->overflow, 1u);
+    wave_add(&st->trav, trav);
+    return;
+  }
+  // terminal position C+1 (tds_batch_1.hpp:641-758)
+  {
+    const int k = la.C + 1;
+    const uint64_t nw = ld_acq(&st->wn[k]);
+    tokens += g.tid == 0 ? nw : 0;
+    uint64_t kept = 0;
+    for (uint64_t i = g.tid; i < nw; i += g.nth) {
+      const uint32_t* w = a.wbuf + in_base + i * stride;
+      const uint32_t u = w[k], s = w[0];
+      uint8_t kp = 0;
+      if (pos_ok(a.tpub[u], k, la)) {
+        if (!la.VC) {
+          if (u != s) {
+            kp = 1;
+            if (a.tpub[s]) a.tsm[s] = 2;
+          }
+        } else if (u == s) {
+          kp = 1;
+          a.tsm[s] = 2;
+        }
+      }
+      a.keep[i] = kp;
+      kept += kp;
+    }
+    wave_add(&st->walks, kept);
+  }
+  wave_add(&st->trav, trav);
+  wave_add(&st->tokens, tokens);
+  tree_barrier(a.gbar);
+  line_post(a, g, s_hist);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+template <typename T>
+static T* dmalloc(uint64_t n) {
+  T* p = nullptr;
+  PM_HIP_CHECK(hipMalloc(&p, std::max<uint64_t>(1, n) * sizeof(T)));
+  return p;
+}
+
+static void ensure_hash(Ctx& c, uint64_t want) {
+  uint64_t cap = 1ull << 16;
+  while (cap < want && cap < (1ull << 31)) cap <<= 1;
+  if (c.hcap >= cap) return;
+  if (c.d_hkey) (void)hipFree(c.d_hkey);
+  if (c.d_hval) (void)hipFree(c.d_hval);
+  if (c.d_front) (void)hipFree(c.d_front);
+  c.d_hkey = dmalloc<unsigned long long>(cap);
+  c.d_hval = dmalloc<unsigned long long>(cap);
+  c.d_front = dmalloc<uint32_t>(cap / 2);
+  PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, cap * sizeof(unsigned long long), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, cap * sizeof(unsigned long long), c.stream));
+  c.hcap = cap;
+}
+
+void free_line_buffers(Ctx& c) {
+  void* ptrs[] = {c.d_lstats, c.d_hkey, c.d_hval, c.d_front, c.d_gbar};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  c.d_lstats = nullptr;
+  c.d_hkey = c.d_hval = nullptr;
+  c.d_front = nullptr;
+  c.d_gbar = nullptr;
+  c.hcap = 0;
+}
+
+bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
+  const NlcLine& line = c.pattern.lines[pl];
+  const bool tds = pl >= 4;  // beta.cpp:762-767
+  const LineArgs la = make_line_args(c, line);
+  const int stride = la.C + 2;
+  if (tds && line.enumeration.size() < static_cast<size_t>(stride))
+    throw std::runtime_error("pattern_non_local_constraint enumeration shorter than the TDS walk");
+  if (la.C + 2 > 18) return false;
+  if (!c.d_lstats) {
+    c.d_lstats = dmalloc<LineStats>(1);
+    c.d_gbar = dmalloc<unsigned>(kGbarWords);
+    PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, kGbarWords * sizeof(unsigned), c.stream));
+  }
+  if (!c.line_grid) {
+    int per_cu = 0, per_cu2 = 0;
+    PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_path_line, kLineBlock, 0));
+    PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_tds_line, kLineBlock, 0));
+    hipDeviceProp_t prop;
+    PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
+    if (std::min(per_cu, per_cu2) < 1) throw std::runtime_error("fused line kernels cannot be resident");
+    // one block per CU: the barrier cost grows with the number of blocks
+    c.line_grid = static_cast<unsigned>(std::min<int>(prop.multiProcessorCount, 1024));
+  }
+  // the table is sized from the superstep-0 matching rows (upper bound of |S|)
+  ensure_hash(c, std::max<uint64_t>(1ull << 16, 4 * c.ss0_rows));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_lstats, 0, sizeof(LineStats), c.stream));
+  LineKernelArgs a{};
+  a.offp = c.d_offp;
+  a.mcol = c.d_mcol;
+  a.mst = c.d_mst;
+  a.mlen = c.d_mlen;
+  a.malive = c.d_malive;
+  a.tpub = c.d_tpub[c.cur];
+  a.perm = c.d_perm;
+  a.tsm = c.d_tsm;
+  a.slist = c.d_slist;
+  a.nS = c.d_nS;
+  a.sources = c.d_sources;
+  a.oa.hubs = c.d_hubs;
+  a.oa.perm = c.d_perm;
+  a.oa.nhubs = static_cast<uint32_t>(c.hubs_host.size());
+  a.oa.nranks = c.nranks;
+  a.la = la;
+  a.i0 = static_cast<int>(line.indices[0]);
+  a.gbar = c.d_gbar;
+  a.hkey = c.d_hkey;
+  a.hval = c.d_hval;
+  a.hmask = c.hcap - 1;
+  a.front = c.d_front;
+  a.fcap = c.hcap / 2;
+  a.st = c.d_lstats;
+  if (tds) {
+    c.arena.reset();
+    const uint64_t room = c.arena.cap - 8192;
+    a.kcap = room / (8 * (4 * uint64_t(stride) + 1));  // final walks whose keep flag fits
+    a.keep = static_cast<uint8_t*>(c.arena.get(a.kcap));
+    a.wcap = (c.arena.cap - c.arena.used - 4096) / sizeof(uint32_t);
+    a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
+  }
+  void* args[] = {&a};
+  PM_HIP_CHECK(hipLaunchCooperativeKernel(tds ? reinterpret_cast<const void*>(k_tds_line)
+                                              : reinterpret_cast<const void*>(k_path_line),
+                                          dim3(c.line_grid), dim3(kLineBlock), args, 0, c.stream));
+  LineStats hs;
+  PM_HIP_CHECK(hipMemcpyAsync(&hs, c.d_lstats, sizeof(hs), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.nsources = hs.nsrc;
+  if (hs.overflow) {
+    if (!tds) {
+      // partial inserts are not all recorded in the frontier list: clear all, grow
+      const uint64_t grow = c.hcap * 4;
+      PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+      PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+      ensure_hash(c, grow);
+    }
+    return false;
+  }
+  out.tr.sources = hs.nsrc;
+  out.tr.acked = hs.acked;
+  out.tr.edges = hs.trav;
+  out.tr.tokens = hs.tokens;
+  out.tr.walks = hs.walks;
+  out.deleted = hs.deleted ? 1u : 0u;
+  c.last_acked = hs.acked;
+  const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
+  out.rm_v.assign(c.nranks, 0);
+  out.rm_e.assign(c.nranks, 0);
+  for (uint32_t r = 0; r < c.nranks; ++r) {
+    out.rm_v[r] = hs.removed[r];
+    out.rm_e[r] = hs.removed[P + r];
+  }
+  out.stride = static_cast<uint32_t>(stride);
+  out.walks.clear();
+  const uint64_t final_walks = tds ? hs.wn[la.C + 1] : 0;
+  if (tds && want_walks && final_walks) {
+    std::vector<uint32_t> all(final_walks * stride);
+    std::vector<uint8_t> kp(final_walks);
+    PM_HIP_CHECK(hipMemcpyAsync(all.data(), a.wbuf + hs.wbase[la.C + 1], all.size() * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipMemcpyAsync(kp.data(), a.keep, final_walks, hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    for (uint64_t i = 0; i < final_walks; ++i)
+      if (kp[i]) out.walks.insert(out.walks.end(), all.begin() + i * stride, all.begin() + (i + 1) * stride);
+  }
+  return true;
+}
+
+}  // namespace pm

@@ -53,6 +53,18 @@ def test_rmat_matches_oracle(pat, scale, p_gen, alphabet, nranks, tmp_path):
     assert sg["walks"] == so["paths"]
 
 
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks", [RMAT_CASES[2], RMAT_CASES[5], RMAT_CASES[7]])
+def test_exact_count_token_passing_matches_oracle(pat, scale, p_gen, alphabet, nranks, tmp_path, monkeypatch):
+    # PM_FUSED_LINES=0: every NLC line through the per-position launch path
+    # (the fallback of the fused line kernels on capacity overflow)
+    monkeypatch.setenv("PM_FUSED_LINES", "0")
+    g = pm.rmat_graph(scale, p_gen)
+    labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, labels, nranks)
+    assert diffs == []
+    assert sg["nlcc_edges"] == so["nlcc_edges"] and sg["tds_edges"] == so["tds_edges"]
+
+
 def _tree_pairs():
     return [(0, 1), (1, 2), (1, 3), (3, 5), (4, 5), (5, 6)], np.array([3, 4, 7, 2, 3, 5, 7], np.uint64)
 
