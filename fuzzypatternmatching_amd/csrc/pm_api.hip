@@ -76,7 +76,7 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   c->hub_threshold = g->hub_threshold;
   if (!c->symmetric)
     throw std::runtime_error("directed (non-symmetric) input graphs are not supported by the GPU path yet");
-  if (c->n >= 0xFFFFFFFFull) throw std::runtime_error("more than 2^32-1 vertices");
+  if (c->n >= (1ull << 30)) throw std::runtime_error("more than 2^30 vertices (30-bit positions in M entries)");
   c->pattern = load_pattern_dir(pattern_dir);
   const PatternGraph& pg = c->pattern.graph;
   if (pg.diameter == 0) throw std::runtime_error("pattern_stat: diameter is 0 or missing");
@@ -107,10 +107,11 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
   c->d_mcol = dalloc<uint32_t>(c->nq);
-  c->d_mst = dalloc<uint8_t>(c->nq);
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
   c->d_slist = dalloc<uint32_t>(c->n);
+  c->d_smask[0] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
+  c->d_smask[1] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
   c->d_sources = dalloc<uint32_t>(c->n);
   c->d_nS = dalloc<uint32_t>(1);
   c->d_flags = dalloc<uint32_t>(4);
@@ -141,7 +142,7 @@ static void destroy_ctx(pm_ctx* c) {
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
-                  c->d_mst, c->d_mlen, c->d_malive, c->d_slist, c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
+                  c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -164,6 +165,7 @@ static void reset_state(Ctx& c) {
   PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[0], 0, c.n * sizeof(uint16_t), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[1], 0, c.n * sizeof(uint16_t), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(c.d_tsm, 0, c.n, c.stream));
+  c.smask_valid = false;
   PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(c.d_flags, 0, 4 * sizeof(uint32_t), c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -207,7 +209,6 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
-      PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
       PM_HIP_CHECK(hipEventRecord(ev[D + 1], c.stream));
       launch_lcc_first(c, slot);
       PM_HIP_CHECK(hipEventRecord(ev[D + 2], c.stream));
@@ -333,25 +334,22 @@ static void export_state(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32
   tpub.assign(n, 0);
   mdeg.assign(n, 0);
   nbrs.clear();
-  std::vector<uint32_t> rowc;
-  std::vector<uint8_t> rows;
+  std::vector<uint32_t> m(c.nq);  // one bulk copy of the active-edge map
+  if (c.nq) PM_HIP_CHECK(hipMemcpy(m.data(), c.d_mcol, c.nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
   for (uint64_t v = 0; v < n; ++v) {
     const uint32_t p = pos[v];
     if (!tp[p]) continue;
     tpub[v] = tp[p];
     mdeg[v] = malive[p];
     const uint32_t L = mlen[p];
-    if (!L) continue;
-    rowc.resize(L);
-    rows.resize(L);
-    PM_HIP_CHECK(hipMemcpy(rowc.data(), c.d_mcol + off[p], L * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    PM_HIP_CHECK(hipMemcpy(rows.data(), c.d_mst + off[p], L, hipMemcpyDeviceToHost));
     uint32_t k = 0;
-    for (uint32_t i = 0; i < L; ++i)
-      if (rows[i] & 1u) {
-        nbrs.push_back(c.perm_host[rowc[i]]);
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint32_t x = m[off[p] + i];
+      if (x & kAlive) {
+        nbrs.push_back(c.perm_host[x & kPosMask]);
         ++k;
       }
+    }
     if (k != malive[p]) throw std::runtime_error("internal: alive count mismatch in export");
   }
 }

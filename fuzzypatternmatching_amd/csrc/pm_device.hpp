@@ -146,6 +146,26 @@ __device__ __forceinline__ void flush_block(BlockAcc a, const OwnerArgs& oa, uns
     for (uint32_t i = threadIdx.x; i < 2 * P; i += blockDim.x) out[i] = s_hist[i];
 }
 
+// Wave-aggregated reservation of n slots on a global counter; returns the
+// lane's first slot.  All lanes of the wave must call it.
+__device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, uint32_t n) {
+  const uint64_t incl = wave_incl_scan(n);
+  const uint64_t total = __shfl(incl, kWave - 1, kWave);
+  unsigned long long base = 0;
+  if (lane_id() == 0 && total) base = atomicAdd(ctr, static_cast<unsigned long long>(total));
+  base = __shfl(base, 0, kWave);
+  return base + incl - n;
+}
+
+__device__ __forceinline__ uint32_t wave_reserve32(uint32_t* ctr, uint32_t n) {
+  const uint64_t incl = wave_incl_scan(n);
+  const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+  uint32_t base = 0;
+  if (lane_id() == 0 && total) base = atomicAdd(ctr, total);
+  base = __shfl(base, 0, kWave);
+  return base + static_cast<uint32_t>(incl) - n;
+}
+
 // Block-aggregated global add: one atomic per block (all threads must call).
 __device__ __forceinline__ void block_atomic_add(unsigned long long* dst, uint64_t v) {
   __shared__ unsigned long long s_b[kWpb];

@@ -98,6 +98,12 @@ static constexpr uint32_t kTileEntries = 64 * kSub; // 512
 static constexpr uint32_t kHeavyDeg = 1024;
 static constexpr int kHeavyKind = 11;
 static constexpr int kMaxRanges = 16 * 12 + 1;
+// Active-edge map entries: neighbour position | kAlive | kFlag (cycle mark,
+// nem_1.hpp:764-770).  Positions use 30 bits (V < 2^30).
+static constexpr uint32_t kAlive = 1u << 31;
+static constexpr uint32_t kFlag = 1u << 30;
+static constexpr uint32_t kPosMask = kFlag - 1;
+
 // Padded row length: nextpow2(degree) up to kHeavyDeg, the degree above.
 __host__ __device__ inline uint64_t padded_degree(uint64_t d) {
   if (d <= 1) return d;
@@ -161,11 +167,16 @@ struct Ctx {
   int cur = 0;
   uint16_t* d_tst = nullptr;      // vertex_state.template_vertices (T_state)
   uint32_t* d_mcol = nullptr;     // active-edge rows (neighbour positions) at the vertex's row start, nq
-  uint8_t* d_mst = nullptr;       // per entry: bit0 alive, bit1 flag (cycle mark)
   uint32_t* d_mlen = nullptr;     // entries written in the row (alive or dead)
   uint32_t* d_malive = nullptr;   // |M[v]|
-  uint32_t* d_slist = nullptr;    // S members after superstep 0 (superset of S later)
+  uint32_t* d_slist = nullptr;    // S members after superstep 0 (superset of S later), positions
   uint32_t* d_nS = nullptr;       // device count of d_slist
+  // live mask of slist per 64 entries, written by every later superstep
+  // (members of S plus vertices removed in that superstep): later passes
+  // skip dead chunks without touching them
+  uint64_t* d_smask[2] = {nullptr, nullptr};
+  int smask_cur = 0;
+  bool smask_valid = false;       // false right after superstep 0 (all entries live)
   uint32_t* d_flags = nullptr;    // [0] not_finished, [1] asymmetric edge state, [2] deleted
   uint64_t* d_counts = nullptr;   // per-slot per-rank counts (vertices, edges) + traversed
   uint64_t* d_part = nullptr;     // per-block counter partials (kPartGridMax x slot_words)

@@ -11,9 +11,9 @@
 //   tpub[2][V] u16                template_vertices (T_pub), ping-pong per superstep;
 //                                 0 <=> vertex not in the state map S
 //   tst[V] u16                    vertex_state.template_vertices (T_state)
-//   mcol[E] u32, mst[E] u8        active-edge map M[v], stored in v's own CSR slot
+//   mcol[E] u32                   active-edge map M[v], stored in v's own CSR slot
 //                                 [offp[v], offp[v]+mlen[v]) so no prefix scan is needed;
-//                                 mst bit0 = alive, bit1 = edge flag
+//                                 entry = neighbour position | kAlive | kFlag (edge flag)
 //   mlen[V], malive[V] u32        written length / alive count of M[v]
 //   slist[nS] u32                 positions that entered S in superstep 0 (S only shrinks)
 //
@@ -210,7 +210,6 @@ struct K1Out {
   uint16_t* tst;
   uint16_t* tpub;
   uint32_t* mcol;
-  uint8_t* mst;
   uint32_t* mlen;
   uint32_t* malive;
 };
@@ -291,12 +290,10 @@ __device__ __forceinline__ void k1_slice(uint32_t v, uint16_t tv, uint32_t j, ui
   } else if (COMPACT) {
     if (contrib) {
       const uint64_t dst = rowbase + cnt + __builtin_popcountll(bal & ((1ull << lane) - 1));
-      o.mcol[dst] = v;
-      o.mst[dst] = 1;
+      o.mcol[dst] = v | kAlive;
     }
   } else if (ok) {
-    o.mcol[rowbase + j] = v;
-    o.mst[rowbase + j] = contrib ? 1 : 0;
+    o.mcol[rowbase + j] = contrib ? (v | kAlive) : v;
   }
   cnt += static_cast<uint32_t>(__builtin_popcountll(bal));
   if (cm) tnacc |= tv;
@@ -383,8 +380,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint64_t g = (__ballot(contrib) >> shift) & gmask;
         if (contrib && !(MODE & 1)) {
           const uint64_t dst = qbase + (uint64_t(rr) << lg) + __builtin_popcountll(g & ((1ull << k) - 1));
-          o.mcol[dst] = vq;
-          o.mst[dst] = 1;
+          o.mcol[dst] = vq | kAlive;
         }
         const uint16_t TN = wave_or_bits(cm ? tvq : 0u, nm, shift, gmask);
         bool surv = false;
@@ -549,8 +545,9 @@ __device__ __forceinline__ int find_row(const uint64_t* rs, uint64_t j) {
 // symmetry, which is reported through flags[1] (the host then refuses to go on).
 __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
+    const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
     const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
-    OwnerArgs oa, const uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
+    OwnerArgs oa, uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, unsigned long long* __restrict__ part) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
@@ -569,12 +566,17 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   const uint32_t nS = *nSp;
   const uint64_t nchunks = (uint64_t(nS) + kWave - 1) / kWave;
   for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb) {
+    const uint64_t live = mask_in ? mask_in[chunk] : ~0ull;
+    if (!live) {  // wave-uniform: nothing left in this chunk
+      if (lane == 0) mask_out[chunk] = 0;
+      continue;
+    }
     const uint64_t i = chunk * kWave + lane;
     uint32_t u = kNone;
     uint16_t Tu = 0;
     uint64_t beg = 0, len = 0;
     uint32_t alive0 = 0;
-    if (i < nS) {
+    if (i < nS && ((live >> lane) & 1ull)) {
       u = slist[i];
       Tu = tcur[u];
       if (Tu) {
@@ -597,33 +599,32 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     for (uint64_t j0 = 0; j0 < total; j0 += uint64_t(kWave) * kU) {
       int r[kU];
       uint64_t e[kU];
-      uint8_t st[kU];
-      uint32_t v[kU];
+      uint32_t m[kU];
 #pragma unroll
       for (int q = 0; q < kU; ++q) {
         const uint64_t j = j0 + uint64_t(q) * kWave + lane;
         r[q] = kWave;
         e[q] = 0;
-        st[q] = 0;
-        v[q] = 0;
+        m[q] = 0;
         if (j < total) {
           r[q] = find_row(s_rs[w], j);
           e[q] = s_beg[w][r[q]] + (j - s_rs[w][r[q]]);
-          st[q] = mst[e[q]];
-          v[q] = mcol[e[q]];
+          m[q] = mcol[e[q]];
         }
       }
       uint16_t tv[kU];
 #pragma unroll
-      for (int q = 0; q < kU; ++q) tv[q] = (st[q] & 1u) ? tcur[v[q]] : uint16_t(0);
+      for (int q = 0; q < kU; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
 #pragma unroll
       for (int q = 0; q < kU; ++q) {
         uint32_t x = 0;
-        if (st[q] & 1u) {
+        if (m[q] & kAlive) {
           const bool ok = (tv[q] & s_nm[w][r[q]]) != 0;
-          const bool flag = ok || (st[q] & 2u);
-          mst[e[q]] = flag ? 1u : 0u;
-          if ((st[q] & 2u) && !ok && tv[q]) asym = true;
+          const bool fl = (m[q] & kFlag) != 0;
+          const bool flag = ok || fl;
+          const uint32_t nm2 = (m[q] & kPosMask) | (flag ? kAlive : 0u);  // flags cleared by verify
+          if (nm2 != m[q]) mcol[e[q]] = nm2;
+          if (fl && !ok && tv[q]) asym = true;
           x = (ok ? tv[q] : 0u) | (flag ? (1u << 16) : 0u);
         }
         const uint32_t inc = seg_scan_orsum(x, r[q]);
@@ -652,6 +653,11 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         malive[u] = 0;
       }
     }
+    // live mask of the next superstep (S only shrinks); a vertex removed now
+    // stays live one more superstep so that its 0 also reaches the other
+    // T_pub buffer (it is dropped once it arrives with T_pub = 0)
+    const uint64_t lm = __ballot(survivor || removed);
+    if (lane == 0) mask_out[chunk] = lm;
     acc.trav += alive0;
     acc.removed |= removed;
     acc.asym |= asym;
@@ -918,7 +924,7 @@ void build_tiling(Ctx& c) {
 }
 
 static K1Out k1_out(Ctx& c) {
-  return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mst, c.d_mlen, c.d_malive};
+  return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mlen, c.d_malive};
 }
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid) {
@@ -960,6 +966,7 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot) {
   if (c.ntiles == 0) {
     PM_HIP_CHECK(hipMemsetAsync(d_slot, 0, slot_words(c) * sizeof(uint64_t), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
+    c.smask_valid = false;
     return;
   }
   const unsigned grid = c.k1_grid;
@@ -971,6 +978,7 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot) {
   size_t tmp = c.scan_tmp_bytes;
   PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_tbase, static_cast<int>(c.tmask_words),
                                                 c.stream));
+  c.smask_valid = false;
   hipLaunchKernelGGL(k_slist_write, dim3(grid_for(c.tmask_words, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_ktab,
                      static_cast<uint32_t>(c.ktab.size() - 1), c.d_hseg,
                      reinterpret_cast<const unsigned long long*>(c.d_tmask), c.d_tbase, c.tmask_words, c.d_slist,
@@ -989,12 +997,17 @@ size_t slist_scan_tmp_bytes(uint64_t words) {
 void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   const unsigned grid = grid_for(chunks, kWpb, kMaxGrid);
-  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS,
-                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mst, c.d_mlen,
+  const unsigned long long* min = c.smask_valid ? reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur])
+                                                : nullptr;
+  auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
+  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS, min, mout,
+                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
                      c.d_malive, reinterpret_cast<unsigned long long*>(c.d_part));
   PM_HIP_CHECK(hipGetLastError());
   reduce_into(c, grid, d_slot);
   c.cur ^= 1;
+  c.smask_cur ^= 1;
+  c.smask_valid = true;
 }
 
 void launch_count_state(Ctx& c, uint64_t* d_slot) {
@@ -1064,15 +1077,15 @@ __global__ void k_row_alive(const uint32_t* __restrict__ items, uint64_t nitems,
 // Level-1 tokens of path/cycle lines: (v, s, parent = s) for v in M[s].
 __global__ void k_tp_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
                           const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
-                          const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
+                          const uint32_t* __restrict__ mlen,
                           uint32_t* __restrict__ tu, uint32_t* __restrict__ ts, uint32_t* __restrict__ tp) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
     uint64_t o = obase[i];
     const uint64_t b = offp[s], L = mlen[s];
     for (uint64_t e = b; e < b + L; ++e) {
-      if (!(mst[e] & 1u)) continue;
-      tu[o] = mcol[e];
+      if (!(mcol[e] & kAlive)) continue;
+      tu[o] = mcol[e] & kPosMask;
       ts[o] = s;
       tp[o] = s;
       ++o;
@@ -1134,7 +1147,7 @@ __global__ void k_tp_unique(const unsigned long long* __restrict__ keys, const u
 // Expansion count: alive entries of M[u] other than the excluded parent.
 __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, const uint32_t* __restrict__ fx,
                                   uint64_t nf, const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
-                                  const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen,
+                                  const uint32_t* __restrict__ mlen,
                                   const uint32_t* __restrict__ malive, uint32_t* __restrict__ cnt,
                                   unsigned long long* __restrict__ trav) {
   uint64_t t = 0;
@@ -1144,7 +1157,7 @@ __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, con
     const uint64_t b = offp[u], L = mlen[u];
     uint32_t c = 0;
     for (uint64_t e = b; e < b + L; ++e)
-      if ((mst[e] & 1u) && mcol[e] != x) ++c;
+      if ((mcol[e] & kAlive) && (mcol[e] & kPosMask) != x) ++c;
     cnt[i] = c;
     t += malive[u];
   }
@@ -1153,8 +1166,8 @@ __global__ void k_tp_expand_count(const unsigned long long* __restrict__ fk, con
 
 __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, const uint32_t* __restrict__ fx,
                                   uint64_t nf, const uint64_t* __restrict__ obase, const uint64_t* __restrict__ offp,
-                                  const uint32_t* __restrict__ mcol, const uint8_t* __restrict__ mst,
-                                  const uint32_t* __restrict__ mlen, uint32_t* __restrict__ tu,
+                                  const uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
+                                  uint32_t* __restrict__ tu,
                                   uint32_t* __restrict__ ts, uint32_t* __restrict__ tp) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nf; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = static_cast<uint32_t>(fk[i] & 0xFFFFFFFFull);
@@ -1163,8 +1176,8 @@ __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, con
     uint64_t o = obase[i];
     const uint64_t b = offp[u], L = mlen[u];
     for (uint64_t e = b; e < b + L; ++e) {
-      if (!(mst[e] & 1u)) continue;
-      const uint32_t w = mcol[e];
+      if (!(mcol[e] & kAlive)) continue;
+      const uint32_t w = mcol[e] & kPosMask;
       if (w == x) continue;
       tu[o] = w;
       ts[o] = s;
@@ -1179,9 +1192,8 @@ __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, con
 __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts,
                               const uint32_t* __restrict__ tp, uint64_t ntok, LineArgs la,
                               const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
-                              const uint32_t* __restrict__ mcol, uint8_t* __restrict__ mst,
-                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ perm,
-                              uint8_t* __restrict__ tsm) {
+                              uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
+                              const uint32_t* __restrict__ perm, uint8_t* __restrict__ tsm) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntok; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = tu[i], s = ts[i];
     if (!pos_ok(tpub[u], la.C + 1, la)) continue;
@@ -1196,9 +1208,9 @@ __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* _
       uint64_t lo = offp[s], hi = offp[s] + mlen[s];
       while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (perm[mcol[mid]] < pid) lo = mid + 1; else hi = mid;
+        if (perm[mcol[mid] & kPosMask] < pid) lo = mid + 1; else hi = mid;
       }
-      if (lo < offp[s] + mlen[s] && mcol[lo] == p && (mst[lo] & 1u)) mst[lo] = 3;
+      if (lo < offp[s] + mlen[s] && (mcol[lo] & kPosMask) == p && (mcol[lo] & kAlive)) mcol[lo] |= kFlag;
     }
   }
 }
@@ -1206,16 +1218,16 @@ __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* _
 // ---- TDS ----------------------------------------------------------------
 __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
                            const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
-                           const uint8_t* __restrict__ mst, const uint32_t* __restrict__ mlen, int stride,
+                           const uint32_t* __restrict__ mlen, int stride,
                            uint32_t* __restrict__ walks) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
     uint64_t o = obase[i];
     const uint64_t b = offp[s], L = mlen[s];
     for (uint64_t e = b; e < b + L; ++e) {
-      if (!(mst[e] & 1u)) continue;
+      if (!(mcol[e] & kAlive)) continue;
       walks[o * stride + 0] = s;
-      walks[o * stride + 1] = mcol[e];
+      walks[o * stride + 1] = mcol[e] & kPosMask;
       ++o;
     }
   }
@@ -1226,7 +1238,7 @@ __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, 
 template <int PASS>
 __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int k, int stride, LineArgs la,
                              const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
-                             const uint32_t* __restrict__ mcol, const uint8_t* __restrict__ mst,
+                             const uint32_t* __restrict__ mcol,
                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive,
                              uint32_t* __restrict__ cnt, const uint64_t* __restrict__ obase,
                              uint32_t* __restrict__ wout, unsigned long long* __restrict__ trav) {
@@ -1240,8 +1252,8 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
       const uint64_t b = offp[u], L = mlen[u];
       uint64_t o = PASS ? obase[i] : 0;
       for (uint64_t e = b; e < b + L; ++e) {
-        if (!(mst[e] & 1u)) continue;
-        const uint32_t nb = mcol[e];
+        if (!(mcol[e] & kAlive)) continue;
+        const uint32_t nb = mcol[e] & kPosMask;
         if (k == la.C) {
           if (la.VC) {
             if (nb != s) continue;
@@ -1388,7 +1400,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   auto* ts = arena_alloc<uint32_t>(c, ntok);
   auto* tp = arena_alloc<uint32_t>(c, ntok);
   hipLaunchKernelGGL(k_tp_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
+                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mlen, tu, ts, tp);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += ntok;
   SeenSet seen{};
@@ -1434,21 +1446,21 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     }
     auto* ecnt = arena_alloc<uint32_t>(c, nf);
     hipLaunchKernelGGL(k_tp_expand_count, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf,
-                       c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, ecnt, d_trav);
+                       c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, ecnt, d_trav);
     auto* eb = arena_alloc<uint64_t>(c, nf + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, ecnt, eb, nf);
     tu = arena_alloc<uint32_t>(c, nnext);
     ts = arena_alloc<uint32_t>(c, nnext);
     tp = arena_alloc<uint32_t>(c, nnext);
     hipLaunchKernelGGL(k_tp_expand_write, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf, eb,
-                       c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, tu, ts, tp);
+                       c.d_offp, c.d_mcol, c.d_mlen, tu, ts, tp);
     PM_HIP_CHECK(hipGetLastError());
     ntok = nnext;
     res.tokens += ntok;
   }
   if (ntok > 0) {
     hipLaunchKernelGGL(k_tp_terminal, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
-                       la, tpub, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_perm, c.d_tsm);
+                       la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_perm, c.d_tsm);
     PM_HIP_CHECK(hipGetLastError());
   }
   unsigned long long trav = 0;
@@ -1483,20 +1495,20 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   const uint64_t trav_init = nw;
   auto* walks = arena_alloc<uint32_t>(c, nw * stride);
   hipLaunchKernelGGL(k_tds_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, stride, walks);
+                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mlen, stride, walks);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += nw;
   for (int k = 1; k <= C && nw > 0; ++k) {
     auto* wc = arena_alloc<uint32_t>(c, nw);
     hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                       stride, la, tpub, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc,
+                       stride, la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, wc,
                        static_cast<const uint64_t*>(nullptr), static_cast<uint32_t*>(nullptr), d_trav);
     auto* wb = arena_alloc<uint64_t>(c, nw + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
     auto* wn = arena_alloc<uint32_t>(c, nnext * stride);
     if (nnext) {
       hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                         stride, la, tpub, c.d_offp, c.d_mcol, c.d_mst, c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
+                         stride, la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
       PM_HIP_CHECK(hipGetLastError());
     }
     walks = wn;

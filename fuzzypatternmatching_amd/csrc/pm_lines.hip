@@ -62,8 +62,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 struct LineKernelArgs {
   // graph / state (positions)
   const uint64_t* offp;
-  const uint32_t* mcol;
-  uint8_t* mst;
+  uint32_t* mcol;
   const uint32_t* mlen;
   const uint32_t* malive;
   uint16_t* tpub;
@@ -71,6 +70,7 @@ struct LineKernelArgs {
   uint8_t* tsm;
   const uint32_t* slist;
   const uint32_t* nS;
+  const unsigned long long* smask;  // live mask of slist per 64 entries (null: all live)
   uint32_t* sources;
   OwnerArgs oa;
   LineArgs la;
@@ -89,17 +89,6 @@ struct LineKernelArgs {
   uint64_t kcap;
   LineStats* st;
 };
-
-// Wave-aggregated reservation of n slots on a global counter; returns the
-// lane's first slot.  All lanes of the wave must call it.
-__device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, uint32_t n) {
-  const uint64_t incl = wave_incl_scan(n);
-  const uint64_t total = __shfl(incl, kWave - 1, kWave);
-  unsigned long long base = 0;
-  if (lane_id() == 0 && total) base = atomicAdd(ctr, static_cast<unsigned long long>(total));
-  base = __shfl(base, 0, kWave);
-  return base + incl - n;
-}
 
 __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
   x = wave_sum(x);
@@ -163,9 +152,9 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
     uint64_t lo = b, hi = e;
     while (lo < hi) {
       const uint64_t mid = (lo + hi) >> 1;
-      if (a.perm[a.mcol[mid]] < pid) lo = mid + 1; else hi = mid;
+      if (a.perm[a.mcol[mid] & kPosMask] < pid) lo = mid + 1; else hi = mid;
     }
-    if (lo < e && a.mcol[lo] == p && (a.mst[lo] & 1u)) a.mst[lo] = 3;
+    if (lo < e && (a.mcol[lo] & kPosMask) == p && (a.mcol[lo] & kAlive)) a.mcol[lo] |= kFlag;
   }
 }
 
@@ -186,8 +175,9 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, uint32_t
   for (int d = kWave / 2; d > 0; d >>= 1) Lmax = max(Lmax, static_cast<uint64_t>(__shfl_xor(Lmax, d, kWave)));
   for (uint64_t j = 0; j < Lmax; ++j) {
     uint64_t slot = kEmpty;
-    if (j < L && (a.mst[b + j] & 1u)) {
-      const uint32_t w = a.mcol[b + j];
+    const uint32_t m = j < L ? a.mcol[b + j] : 0u;
+    if (m & kAlive) {
+      const uint32_t w = m & kPosMask;
       if (w != excl) {
         ++emitted;
         if (k + 1 == la.C + 1) {
@@ -256,10 +246,10 @@ __device__ __forceinline__ GridIdx grid_idx() {
 // P1 for one 64-entry chunk of slist: returns the lane's source (ok) after
 // appending it to the source list and marking the token source map.
 __device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t i, uint32_t nS, bool tds,
-                                              uint32_t& s) {
+                                              uint64_t live, uint32_t& s) {
   bool ok = false;
   s = 0;
-  if (i < nS) {
+  if (i < nS && ((live >> lane_id()) & 1ull)) {
     s = a.slist[i];
     const uint16_t T = a.tpub[s];
     ok = T && pos_ok(T, 0, a.la);
@@ -323,8 +313,10 @@ __global__ __launch_bounds__(kLineBlock) void k_path_line(LineKernelArgs a) {
   // P1 + position 1: (v, s, parent = s) for v in M[s]
   const uint32_t nS = *a.nS;
   for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
+    const uint64_t live = a.smask ? a.smask[i0 / kWave] : ~0ull;
+    if (!live) continue;  // wave-uniform
     uint32_t s;
-    const bool ok = select_source(a, i0 + lane_id(), nS, false, s);
+    const bool ok = select_source(a, i0 + lane_id(), nS, false, live, s);
     if (ok) trav += a.malive[s];
     tokens += tp_forward(a, s, s, kNone, 0, ok);
   }
@@ -374,8 +366,8 @@ __device__ __forceinline__ uint32_t tds_children(const LineKernelArgs& a, const 
   const uint32_t s = w[0];
   uint32_t c = 0;
   for (uint64_t e = b; e < b + L; ++e) {
-    if (!(a.mst[e] & 1u)) continue;
-    const uint32_t nb = a.mcol[e];
+    if (!(a.mcol[e] & kAlive)) continue;
+    const uint32_t nb = a.mcol[e] & kPosMask;
     if (k == la.C) {
       if (la.VC) {
         if (nb != s) continue;
@@ -406,8 +398,10 @@ __global__ __launch_bounds__(kLineBlock) void k_tds_line(LineKernelArgs a) {
   // P1 + position 1 walks [s, w]; region 1 starts at slot 0
   const uint32_t nS = *a.nS;
   for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
+    const uint64_t live = a.smask ? a.smask[i0 / kWave] : ~0ull;
+    if (!live) continue;  // wave-uniform
     uint32_t s;
-    const bool ok = select_source(a, i0 + lane_id(), nS, true, s);
+    const bool ok = select_source(a, i0 + lane_id(), nS, true, live, s);
     uint32_t cnt = 0;
     uint64_t b = 0, L = 0;
     if (ok) {
@@ -421,9 +415,9 @@ __global__ __launch_bounds__(kLineBlock) void k_tds_line(LineKernelArgs a) {
       if ((pos + cnt) * stride <= a.wcap) {
         uint64_t o = pos;
         for (uint64_t e = b; e < b + L; ++e) {
-          if (!(a.mst[e] & 1u)) continue;
+          if (!(a.mcol[e] & kAlive)) continue;
           a.wbuf[o * stride + 0] = s;
-          a.wbuf[o * stride + 1] = a.mcol[e];
+          a.wbuf[o * stride + 1] = a.mcol[e] & kPosMask;
           ++o;
         }
       } else {
@@ -572,7 +566,6 @@ bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
   LineKernelArgs a{};
   a.offp = c.d_offp;
   a.mcol = c.d_mcol;
-  a.mst = c.d_mst;
   a.mlen = c.d_mlen;
   a.malive = c.d_malive;
   a.tpub = c.d_tpub[c.cur];
@@ -580,6 +573,7 @@ bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
   a.tsm = c.d_tsm;
   a.slist = c.d_slist;
   a.nS = c.d_nS;
+  a.smask = c.smask_valid ? reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur]) : nullptr;
   a.sources = c.d_sources;
   a.oa.hubs = c.d_hubs;
   a.oa.perm = c.d_perm;
