@@ -429,6 +429,10 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     if (itr == 0) nf = true;  // forced token passing (beta.cpp:686-688)
     if (nf) {
       nf = false;
+      // fused lines run in batches (one launch for consecutive lines, see
+      // run_lines_fused); a line whose batch overflowed runs on the exact path
+      std::vector<FusedLineOut> batch;
+      size_t batch_pl0 = 0, exact_at = SIZE_MAX;
       for (size_t pl = 0; pl < P.lines.size(); ++pl) {
         const NlcLine& line = P.lines[pl];
         for (auto& r : subgraphs[pl]) r.clear();  // reopened with truncation (beta.cpp:713-717)
@@ -439,8 +443,21 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         std::vector<uint32_t> walks;
         uint32_t stride = 0;
         FusedLineOut fo;
+        bool fused = false;
         auto t1 = tick();
-        if (c.fused_lines && run_line_fused(c, pl, files, fo)) {
+        if (c.fused_lines && pl != exact_at) {
+          if (pl < batch_pl0 || pl >= batch_pl0 + batch.size()) {
+            bool overflow = false;
+            const size_t n = run_lines_fused(c, pl, files, batch, overflow);
+            batch_pl0 = pl;
+            if (overflow) exact_at = pl + n;
+          }
+          if (pl >= batch_pl0 && pl < batch_pl0 + batch.size()) {
+            fo = std::move(batch[pl - batch_pl0]);
+            fused = true;
+          }
+        }
+        if (fused) {
           tr = fo.tr;
           deleted = fo.deleted;
           vc = cur_vc;

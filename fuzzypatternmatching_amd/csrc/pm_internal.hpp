@@ -86,6 +86,12 @@ struct KRange {
   uint32_t rlo[4], rlen[4];
   uint16_t rtu[4];
   uint32_t nrel;
+  // verify (keep_bits) of the label's template bits: bit kbit[i] survives iff
+  // kneed[i] is a subset of TN (kneed = adj[t], or 1 << 16 when adj[t] = 0);
+  // nkeep > 4 falls back to the LDS loop
+  uint16_t kbit[4];
+  uint32_t kneed[4];
+  uint32_t nkeep;
 };
 struct HSeg {
   uint32_t row;   // row position
@@ -120,6 +126,15 @@ struct LineStats {
   unsigned long long wbase[20]; // TDS: slot offset of each position's walks
   unsigned int overflow, pad;
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
+};
+
+// One NLC line as seen by the fused line kernel (pm_lines.hip).
+struct LineDesc {
+  LineArgs la;
+  int32_t tds;  // pl >= 4: tds_batch_1 (beta.cpp:762-767)
+  int32_t i0;   // pattern_indices[0] (post-processing bit)
+  int32_t il;   // interleave_lp
+  int32_t pad;
 };
 
 struct Ctx {
@@ -196,7 +211,9 @@ struct Ctx {
   bool lcc_started = false; // superstep 0 of the first call done
 
   // fused NLC lines (pm_lines.hip)
-  LineStats* d_lstats = nullptr;
+  LineStats* d_lstats = nullptr;  // per line
+  LineDesc* d_ldesc = nullptr;
+  size_t d_lstats_n = 0;
   unsigned long long* d_hkey = nullptr;  // (source, vertex) hash table, persistent
   unsigned long long* d_hval = nullptr;
   uint64_t hcap = 0;
@@ -242,13 +259,13 @@ struct TpResult {
   uint64_t sources = 0, acked = 0, edges = 0, tokens = 0, walks = 0;
 };
 TpResult run_path_line(Ctx& c, const NlcLine& line);
-// One fused kernel per line (token passing + post-processing).  Returns false
-// when a capacity overflowed (no terminal or post effect has happened;
-// c.nsources names the marked sources): the caller reruns the line through
-// run_path_line / run_tds_line, launch_post_tp and count_state.  Otherwise
+// Output of one line of the fused kernel (token passing + post-processing).
 // rm_v / rm_e are the vertices / edges per rank that left S in
 // post-processing (the active counts after the line are the counts before it
-// minus these: token passing itself changes neither T_pub nor |M|).
+// minus these: token passing itself changes neither T_pub nor |M|).  A line
+// that overflowed a capacity had no terminal or post effect (c.nsources names
+// its marked sources) and is rerun through run_path_line / run_tds_line,
+// launch_post_tp and count_state.
 struct FusedLineOut {
   TpResult tr;
   uint32_t deleted = 0;
@@ -256,7 +273,11 @@ struct FusedLineOut {
   std::vector<uint32_t> walks;  // kept TDS walks (positions), when requested
   uint32_t stride = 0;
 };
-bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out);
+// Lines pl0.. in one launch; returns how many completed (their outputs in
+// outs).  It stops after a line that deleted with interleave_lp set, or before
+// a line that overflowed (overflow = true: rerun that line on the exact-count
+// path).
+size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);

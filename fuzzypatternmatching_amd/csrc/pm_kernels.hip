@@ -247,12 +247,38 @@ __device__ __forceinline__ uint16_t tbits_rel(uint32_t p, const RelRuns& x, cons
   return static_cast<uint16_t>(t);
 }
 
+// keep_bits(tu, TN) of a range from its precomputed needs (wave-uniform).
+struct KeepArgs {
+  uint32_t bit[4], need[4];
+  uint32_t n;
+};
+
+__device__ __forceinline__ KeepArgs load_keep(const KRange& R) {
+  KeepArgs k;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    k.bit[i] = __builtin_amdgcn_readfirstlane(R.kbit[i]);
+    k.need[i] = __builtin_amdgcn_readfirstlane(R.kneed[i]);
+  }
+  k.n = __builtin_amdgcn_readfirstlane(R.nkeep);
+  return k;
+}
+
+__device__ __forceinline__ uint16_t keep_fast(uint16_t tu, uint16_t TN, const KeepArgs& k, const uint16_t* adj) {
+  if (k.n > 4) return keep_bits(tu, TN, adj);
+  uint32_t out = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < static_cast<int>(k.n) && (TN & k.need[i]) == k.need[i]) out |= k.bit[i];
+  return static_cast<uint16_t>(out);
+}
+
 // Verify of the row at position u by the calling lane; returns survivor.
 __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t TN, uint32_t len, uint32_t cnt,
-                                              const uint16_t* adj, const OwnerArgs& oa, const K1Out& o, BlockAcc& acc,
-                                              unsigned long long* s_hist) {
+                                              const uint16_t* adj, const KeepArgs& ka, const OwnerArgs& oa,
+                                              const K1Out& o, BlockAcc& acc, unsigned long long* s_hist) {
   if (!TN) return false;
-  const uint16_t T = keep_bits(tu, TN, adj);
+  const uint16_t T = keep_fast(tu, TN, ka, adj);
   if (!T) {
     acc.removed = 1;
     return false;
@@ -270,6 +296,16 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
   return true;
 }
 
+// DPP lane moves (gfx9 encodings): wave_shr:1 gives lane i the value of lane
+// i-1; row_shl:s gives lane i the value of lane i+s inside its 16-lane row.
+__device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x138, 0xF, 0xF, false));
+}
+template <int S>
+__device__ __forceinline__ uint32_t dpp_row_shl(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x100 + S, 0xF, 0xF, true));
+}
+
 // One 64-slot slice of a row scanned by the whole wave (G >= 64 and heavy
 // segments).  j = slot index of this lane inside the row; carry = the row's
 // previous slot (kNone at the row start).  COMPACT: M position = running
@@ -278,9 +314,9 @@ template <bool COMPACT, int MODE>
 __device__ __forceinline__ void k1_slice(uint32_t v, uint16_t tv, uint32_t j, uint64_t rowbase, uint16_t nm,
                                          const K1Out& o, uint32_t& cnt, uint32_t& tnacc, uint32_t& carry) {
   const int lane = lane_id();
-  uint32_t pv = __shfl_up(v, 1, kWave);
+  uint32_t pv = dpp_wave_shr1(v);
   if (lane == 0) pv = carry;
-  carry = __shfl(v, kWave - 1, kWave);
+  carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), kWave - 1));
   const bool ok = v != kNone;
   const bool first = ok && (j == 0 || pv != v);
   const bool cm = ok && (tv & nm) != 0;
@@ -299,12 +335,72 @@ __device__ __forceinline__ void k1_slice(uint32_t v, uint16_t tv, uint32_t j, ui
   if (cm) tnacc |= tv;
 }
 
+// Uniform parameters of the tile being processed.
+struct K1Tile {
+  uint64_t qbase, t0;
+  uint32_t start, nrows;
+  uint16_t tu, nm;
+};
+
+// G <= 64 slots per row, G = 1 << LG lanes per row, 64/G rows per sub-tile.
+// Compile-time G: the per-row OR reaches the row's first lane through DPP
+// row shifts (+ two cross-row shuffles for G = 32, 64), M positions and
+// counts come from one ballot per sub-tile.
+template <int LG, int MODE, bool WIDE>
+__device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, const RelRuns& rel_runs,
+                                         const uint32_t* s_runs, int nruns, const KeepArgs& keep,
+                                         const uint16_t* s_adj, const OwnerArgs& oa, const K1Out& o, BlockAcc& acc,
+                                         unsigned long long* s_hist, unsigned long long* tm) {
+  constexpr int G = 1 << LG;
+  constexpr uint64_t gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
+  const int lane = lane_id();
+  const int k = lane & (G - 1);
+  const int lead = lane & ~(G - 1);
+  uint64_t words = 0;  // lane q keeps the survivor mask of sub-tile q
+#pragma unroll 1
+  for (int q = 0; q < kSub; ++q) {
+    // rolled loop: the slice in use rotates into v[0] (no dynamic register indexing)
+    const uint32_t vq = v[0];
+#pragma unroll
+    for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
+    const uint16_t tv = vq != kNone ? tbits_rel<WIDE>(vq, rel_runs, s_runs, nruns) : uint16_t(0);
+    const uint32_t rr = static_cast<uint32_t>((T.t0 + q * kWave + lane) >> LG);  // row inside the run
+    const uint32_t pv = dpp_wave_shr1(vq);
+    const bool ok = vq != kNone;
+    const bool first = ok && (k == 0 || pv != vq);
+    const bool cm = ok && (tv & T.nm) != 0;
+    const bool contrib = cm && first;
+    const uint64_t bal = __ballot(contrib);
+    const uint64_t gb = (bal >> lead) & gmask;  // this row's contribution bits
+    if (contrib && !(MODE & 1)) {
+      const uint64_t dst = T.qbase + (uint64_t(rr) << LG) + __builtin_popcountll(gb & ((1ull << k) - 1));
+      o.mcol[dst] = vq | kAlive;
+    }
+    uint32_t x = cm ? tv : 0u;
+    if (G >= 2) x |= dpp_row_shl<1>(x);
+    if (G >= 4) x |= dpp_row_shl<2>(x);
+    if (G >= 8) x |= dpp_row_shl<4>(x);
+    if (G >= 16) x |= dpp_row_shl<8>(x);
+    if (G >= 32) x |= __shfl_down(x, 16, kWave);
+    if (G >= 64) x |= __shfl_down(x, 32, kWave);
+    bool surv = false;
+    if (k == 0 && rr < T.nrows) {
+      const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(gb));
+      surv = k1_finish_row(T.start + rr, T.tu, static_cast<uint16_t>(x & T.nm), c, c, s_adj, keep, oa, o, acc,
+                           s_hist);
+    }
+    const uint64_t sm = __ballot(surv);
+    if (lane == q) words = sm;
+  }
+  if (lane < kSub && !(MODE & 8)) tm[lane] = words;
+}
+
 // MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores,
 // bit1 skips G <= 64 tiles, bit2 skips G >= 128 tiles, bit3 drops every
 // store except a checksum of the loaded slots.  WIDE: some range has more
 // than four relevant label runs (tbits_rel scans them all).
 template <int MODE, bool WIDE = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lcc_first(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, unsigned long long* __restrict__ tmask,
@@ -342,14 +438,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                            __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase));
     unsigned long long* tm = tmask + uint64_t(t) * kSub;
     const RelRuns rel_runs = load_rel(s_tab[r]);
+    const KeepArgs keep = load_keep(s_tab[r]);
 #define PM_TB(x) ((x) != kNone ? tbits_rel<WIDE>((x), rel_runs, s_runs, nruns) : uint16_t(0))
     if (kind <= 6) {
       if (MODE & 2) continue;
       // ---- G <= 64: G lanes per row, 64/G rows per sub-tile
       const int lg = static_cast<int>(kind);
-      const int k = lane & ((1 << lg) - 1);
-      const int shift = (lane >> lg) << lg;
-      const uint64_t gmask = lg == 6 ? ~0ull : ((1ull << (1u << lg)) - 1);
       const uint64_t t0 = uint64_t(rel) * kTileEntries;          // slot offset of the tile in the run
       const uint64_t tend = uint64_t(nrows) << lg;              // slots of the run
       uint32_t v[kSub];
@@ -363,34 +457,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         for (int q = 0; q < kSub; ++q) acc.vs += v[q] ^ PM_TB(v[q]);
         continue;
       }
-#pragma unroll 1
-      for (int q = 0; q < kSub; ++q) {
-        // rolled loop: the slice in use rotates into v[0] (no dynamic register indexing)
-        const uint32_t vq = v[0];
-#pragma unroll
-        for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
-        const uint16_t tvq = PM_TB(vq);
-        const uint64_t s = t0 + q * kWave + lane;
-        const uint32_t rr = static_cast<uint32_t>(s >> lg);    // row inside the run
-        const uint32_t pv = __shfl_up(vq, 1, kWave);
-        const bool ok = vq != kNone;
-        const bool first = ok && (k == 0 || pv != vq);
-        const bool cm = ok && (tvq & nm) != 0;
-        const bool contrib = cm && first;
-        const uint64_t g = (__ballot(contrib) >> shift) & gmask;
-        if (contrib && !(MODE & 1)) {
-          const uint64_t dst = qbase + (uint64_t(rr) << lg) + __builtin_popcountll(g & ((1ull << k) - 1));
-          o.mcol[dst] = vq | kAlive;
-        }
-        const uint16_t TN = wave_or_bits(cm ? tvq : 0u, nm, shift, gmask);
-        bool surv = false;
-        if (k == 0 && rr < nrows) {
-          const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(g));
-          surv = k1_finish_row(start + rr, tu, TN, c, c, s_adj, oa, o, acc, s_hist);
-        }
-        const uint64_t sm = __ballot(surv);
-        if (lane == 0) tm[q] = sm;
+      const K1Tile T{qbase, t0, start, nrows, tu, nm};
+#define PM_K1L(LG) k1_light<LG, MODE, WIDE>(v, T, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm)
+      switch (lg) {
+        case 0: PM_K1L(0); break;
+        case 1: PM_K1L(1); break;
+        case 2: PM_K1L(2); break;
+        case 3: PM_K1L(3); break;
+        case 4: PM_K1L(4); break;
+        case 5: PM_K1L(5); break;
+        default: PM_K1L(6); break;
       }
+#undef PM_K1L
     } else if (kind <= 10) {
       if (MODE & 4) continue;
       // ---- G = 128..1024: consecutive 64-slot slices of one row at a time
@@ -431,7 +509,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
           if (sl == spr - 1) {
             const uint16_t TN = wave_or_bits(tnacc, nm, 0, ~0ull);
             bool surv = false;
-            if (lane == 0 && rr < nrows) surv = k1_finish_row(start + rr, tu, TN, cnt, cnt, s_adj, oa, o, acc, s_hist);
+            if (lane == 0 && rr < nrows) surv = k1_finish_row(start + rr, tu, TN, cnt, cnt, s_adj, keep, oa, o, acc, s_hist);
             if (__ballot(surv)) smask |= 1ull << (rr - static_cast<uint32_t>(t0 >> lg));
           }
         }
@@ -475,7 +553,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
           __threadfence();
           const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
           const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
-          surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, oa, o, acc, s_hist);
+          surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
         }
       }
       if (lane < kSub && !(MODE & 8)) tm[lane] = (lane == 0 && surv) ? 1ull : 0ull;
@@ -859,6 +937,15 @@ void build_tiling(Ctx& c) {
       R.kind = static_cast<uint32_t>(kind);
       R.qbase = dev_at(c.d_offp, a);
       R.nrel = 0;
+      R.nkeep = 0;
+      for (int t = 0; t < 16; ++t) {
+        if (!((tu >> t) & 1u)) continue;
+        if (R.nkeep < 4) {
+          R.kbit[R.nkeep] = static_cast<uint16_t>(1u << t);
+          R.kneed[R.nkeep] = c.pa.adj[t] ? c.pa.adj[t] : (1u << 16);
+        }
+        ++R.nkeep;
+      }
       for (int m = 0; m < nl; ++m) {
         if (!(tus[m] & nm) || c.lr.len[m] == 0) continue;
         if (R.nrel < 4) {

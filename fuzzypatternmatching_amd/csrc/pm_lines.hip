@@ -73,7 +73,7 @@ struct LineKernelArgs {
   const unsigned long long* smask;  // live mask of slist per 64 entries (null: all live)
   uint32_t* sources;
   OwnerArgs oa;
-  LineArgs la;
+  const LineArgs* la;  // current line (global memory: indexed at run time)
   int i0;  // pattern_indices[0] (post-processing bit)
   unsigned* gbar;  // grid barrier state
   // hash table (path lines), persistent, clean between lines
@@ -85,9 +85,13 @@ struct LineKernelArgs {
   // walk storage (TDS lines): positions laid out one after the other
   uint32_t* wbuf;
   uint64_t wcap;  // u32 slots
-  uint8_t* keep;  // terminal keep flags
-  uint64_t kcap;
-  LineStats* st;
+  uint32_t* kept;  // kept walks of the launch (stride C+2 of their line)
+  uint64_t kept_cap;
+  unsigned long long* kept_ctr;  // u32 slots used in kept
+  LineStats* st;   // per line (indexed by pl)
+  const LineDesc* lines;
+  int pl_begin, pl_end;
+  unsigned* done;  // lines processed by the launch
 };
 
 __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
@@ -138,7 +142,7 @@ __device__ __forceinline__ uint64_t ht_insert(const LineKernelArgs& a, uint32_t 
 
 // Terminal position C+1 of a path / cycle line (nem_1.hpp:661-791).
 __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t p) {
-  const LineArgs& la = a.la;
+  const LineArgs& la = *a.la;
   if (!pos_ok(a.tpub[u], la.C + 1, la)) return;
   if (!la.VC) {
     if (u == s) return;
@@ -165,7 +169,7 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
 __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t excl,
                                                int k, bool active) {
   uint32_t emitted = 0;
-  const LineArgs& la = a.la;
+  const LineArgs& la = *a.la;
   uint64_t b = 0, L = 0;
   if (active) {
     b = a.offp[u];
@@ -252,8 +256,8 @@ __device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t 
   if (i < nS && ((live >> lane_id()) & 1ull)) {
     s = a.slist[i];
     const uint16_t T = a.tpub[s];
-    ok = T && pos_ok(T, 0, a.la);
-    if (ok && !tds && !a.la.VC && !((T >> a.la.ilast) & 1u)) ok = false;
+    ok = T && pos_ok(T, 0, *a.la);
+    if (ok && !tds && !a.la->VC && !((T >> a.la->ilast) & 1u)) ok = false;
   }
   const uint64_t pos = wave_reserve(&a.st->nsrc, ok ? 1u : 0u);
   if (ok) {
@@ -304,65 +308,13 @@ __device__ __forceinline__ void line_post(const LineKernelArgs& a, const GridIdx
   }
 }
 
-// ---- path / cycle lines (nem_1) ----------------------------------------
-__global__ __launch_bounds__(kLineBlock) void k_path_line(LineKernelArgs a) {
-  __shared__ unsigned long long s_hist[2 * kMaxRanks];
-  const GridIdx g = grid_idx();
-  LineStats* st = a.st;
-  uint64_t trav = 0, tokens = 0;
-  // P1 + position 1: (v, s, parent = s) for v in M[s]
-  const uint32_t nS = *a.nS;
-  for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
-    const uint64_t live = a.smask ? a.smask[i0 / kWave] : ~0ull;
-    if (!live) continue;  // wave-uniform
-    uint32_t s;
-    const bool ok = select_source(a, i0 + lane_id(), nS, false, live, s);
-    if (ok) trav += a.malive[s];
-    tokens += tp_forward(a, s, s, kNone, 0, ok);
-  }
-  tree_barrier(a.gbar);
-  uint64_t lo = 0;
-  for (int k = 1; k <= a.la.C; ++k) {
-    if (ld_acq(&st->overflow)) break;  // same value in every wave after the barrier
-    const uint64_t hi = ld_acq(&st->ftotal);
-    for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
-      const uint64_t i = i0 + lane_id();
-      const bool act = i < hi;
-      uint32_t s = 0, u = 0, excl = kNone;
-      if (act) {
-        const uint32_t h = ld_acq(&a.front[i]);
-        const unsigned long long key = ld_acq(&a.hkey[h]);
-        const uint32_t par = static_cast<uint32_t>(ld_acq(&a.hval[h]));
-        s = static_cast<uint32_t>(key >> 32);
-        u = static_cast<uint32_t>(key);
-        excl = par == kMulti ? kNone : par;
-        trav += a.malive[u];
-      }
-      tokens += tp_forward(a, u, s, excl, k, act);
-    }
-    lo = hi;
-    tree_barrier(a.gbar);
-  }
-  wave_add(&st->trav, trav);
-  wave_add(&st->tokens, tokens);
-  if (ld_acq(&st->overflow)) return;  // every block returns; the host clears the table
-  line_post(a, g, s_hist);
-  // hash cleanup: no insert happens after the last barrier
-  const uint64_t nf = ld_acq(&st->ftotal);
-  for (uint64_t i = g.tid; i < nf; i += g.nth) {
-    const uint32_t h = ld_acq(&a.front[i]);
-    a.hkey[h] = kEmpty;
-    a.hval[h] = kEmpty;
-  }
-}
-
 // ---- TDS lines (tds_batch_1) -------------------------------------------
 // Walks of position L (L+1 vertices) are stored from st->wbase[L] on, stride
 // C+2 u32, each position in fresh memory (no cache line is reused across
 // phases).  Sender-side checks follow k_tds_expand.
 __device__ __forceinline__ uint32_t tds_children(const LineKernelArgs& a, const uint32_t* w, int k, uint64_t b,
                                                  uint64_t L, uint32_t* out, int stride) {
-  const LineArgs& la = a.la;
+  const LineArgs& la = *a.la;
   const uint32_t s = w[0];
   uint32_t c = 0;
   for (uint64_t e = b; e < b + L; ++e) {
@@ -388,13 +340,181 @@ __device__ __forceinline__ uint32_t tds_children(const LineKernelArgs& a, const 
   return c;
 }
 
-__global__ __launch_bounds__(kLineBlock) void k_tds_line(LineKernelArgs a) {
-  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+// Block-local index (single-block mode: block 0 finishes a small line alone).
+__device__ __forceinline__ GridIdx block_idx() {
+  GridIdx g;
+  g.tid = threadIdx.x;
+  g.nth = blockDim.x;
+  g.gw = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  g.nw = blockDim.x / kWave;
+  return g;
+}
+
+__device__ __forceinline__ void phase_sync(const LineKernelArgs& a, bool single) {
+  if (single) __syncthreads();
+  else tree_barrier(a.gbar);
+}
+
+// A line whose sources and position-1 frontier are at most this large is
+// finished by block 0 alone (block barriers instead of grid barriers).
+static constexpr uint64_t kSmallLine = 16384;
+
+// ---- path / cycle lines (nem_1) ----------------------------------------
+// Positions 2..C+1 and post-processing; every participating wave calls it.
+__device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
+                                          unsigned long long* s_hist) {
+  LineStats* st = a.st;
+  uint64_t trav = 0, tokens = 0, lo = 0;
+  for (int k = 1; k <= a.la->C; ++k) {
+    if (ld_acq(&st->overflow)) break;  // same value in every wave after the barrier
+    const uint64_t hi = ld_acq(&st->ftotal);
+    for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
+      const uint64_t i = i0 + lane_id();
+      const bool act = i < hi;
+      uint32_t s = 0, u = 0, excl = kNone;
+      if (act) {
+        const uint32_t h = ld_acq(&a.front[i]);
+        const unsigned long long key = ld_acq(&a.hkey[h]);
+        const uint32_t par = static_cast<uint32_t>(ld_acq(&a.hval[h]));
+        s = static_cast<uint32_t>(key >> 32);
+        u = static_cast<uint32_t>(key);
+        excl = par == kMulti ? kNone : par;
+        trav += a.malive[u];
+      }
+      tokens += tp_forward(a, u, s, excl, k, act);
+    }
+    lo = hi;
+    phase_sync(a, single);
+  }
+  wave_add(&st->trav, trav);
+  wave_add(&st->tokens, tokens);
+  if (ld_acq(&st->overflow)) return;  // the host clears the table and reruns the line
+  line_post(a, g, s_hist);
+  // hash cleanup: no insert happens after the last position
+  const uint64_t nf = ld_acq(&st->ftotal);
+  for (uint64_t i = g.tid; i < nf; i += g.nth) {
+    const uint32_t h = ld_acq(&a.front[i]);
+    a.hkey[h] = kEmpty;
+    a.hval[h] = kEmpty;
+  }
+}
+
+__device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long long* s_hist) {
   const GridIdx g = grid_idx();
   LineStats* st = a.st;
-  const LineArgs& la = a.la;
-  const int stride = la.C + 2;
   uint64_t trav = 0, tokens = 0;
+  // P1 + position 1: (v, s, parent = s) for v in M[s]
+  const uint32_t nS = *a.nS;
+  for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
+    const uint64_t live = a.smask ? a.smask[i0 / kWave] : ~0ull;
+    if (!live) continue;  // wave-uniform
+    uint32_t s;
+    const bool ok = select_source(a, i0 + lane_id(), nS, false, live, s);
+    if (ok) trav += a.malive[s];
+    tokens += tp_forward(a, s, s, kNone, 0, ok);
+  }
+  wave_add(&st->trav, trav);
+  wave_add(&st->tokens, tokens);
+  tree_barrier(a.gbar);
+  const bool single = ld_acq(&st->nsrc) <= kSmallLine && ld_acq(&st->ftotal) <= kSmallLine;
+  if (!single) path_rest(a, g, false, s_hist);
+  else if (blockIdx.x == 0) path_rest(a, block_idx(), true, s_hist);
+}
+
+// ---- TDS lines (tds_batch_1) -------------------------------------------
+// Positions 2..C+1, terminal and post-processing.  Walks of position L are
+// stored from wbase[L] on (fresh, 128-B aligned memory per position); kept
+// walks are appended to the launch's kept buffer.
+__device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
+                                         unsigned long long* s_hist) {
+  LineStats* st = a.st;
+  const LineArgs& la = *a.la;
+  const int stride = la.C + 2;
+  uint64_t trav = 0, tokens = 0, in_base = 0;
+  for (int k = 1; k <= la.C; ++k) {
+    if (ld_acq(&st->overflow)) break;
+    const uint64_t nin = ld_acq(&st->wn[k]);
+    const uint64_t out_base = (in_base + nin * stride + 31) & ~uint64_t(31);
+    tokens += g.tid == 0 ? nin : 0;
+    const uint32_t* win = a.wbuf + in_base;
+    for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
+      const uint64_t i = i0 + lane_id();
+      const bool act = i < nin;
+      const uint32_t* w = win + (act ? i : 0) * stride;
+      uint32_t cnt = 0;
+      uint64_t b = 0, L = 0;
+      if (act) {
+        const uint32_t u = w[k];
+        if (pos_ok(a.tpub[u], k, la) && enum_ok(w, k, u, la)) {
+          b = a.offp[u];
+          L = a.mlen[u];
+          trav += a.malive[u];
+          cnt = tds_children(a, w, k, b, L, nullptr, stride);
+        }
+      }
+      const uint64_t pos = wave_reserve(&st->wn[k + 1], cnt);
+      if (cnt) {
+        if (out_base + (pos + cnt) * stride <= a.wcap)
+          tds_children(a, w, k, b, L, a.wbuf + out_base + pos * stride, stride);
+        else
+          atomicOr(&st->overflow, 1u);
+      }
+    }
+    in_base = out_base;
+    phase_sync(a, single);
+  }
+  // every final walk may be kept: its room must exist before any terminal effect
+  const uint64_t nw = ld_acq(&st->wn[la.C + 1]);
+  const uint64_t kept0 = ld_acq(a.kept_ctr);
+  if (ld_acq(&st->overflow) || kept0 + nw * stride > a.kept_cap) {
+    if (g.tid == 0) atomicOr(&st->overflow, 1u);
+    wave_add(&st->trav, trav);
+    return;
+  }
+  // terminal position C+1 (tds_batch_1.hpp:641-758)
+  {
+    const int k = la.C + 1;
+    tokens += g.tid == 0 ? nw : 0;
+    if (g.tid == 0) st->wbase[0] = kept0;  // this line's kept walks start here (u32 slots)
+    uint64_t kept = 0;
+    for (uint64_t i0 = g.gw * kWave; i0 < nw; i0 += g.nw * kWave) {
+      const uint64_t i = i0 + lane_id();
+      bool kp = false;
+      const uint32_t* w = a.wbuf + in_base + (i < nw ? i : 0) * stride;
+      if (i < nw) {
+        const uint32_t u = w[k], s = w[0];
+        if (pos_ok(a.tpub[u], k, la)) {
+          if (!la.VC) {
+            if (u != s) {
+              kp = true;
+              if (a.tpub[s]) a.tsm[s] = 2;
+            }
+          } else if (u == s) {
+            kp = true;
+            a.tsm[s] = 2;
+          }
+        }
+      }
+      const uint64_t pos = wave_reserve(a.kept_ctr, kp ? static_cast<uint32_t>(stride) : 0u);
+      if (kp) {
+        uint32_t* d = a.kept + pos;
+        for (int p = 0; p < stride; ++p) d[p] = w[p];
+      }
+      kept += kp;
+    }
+    wave_add(&st->walks, kept);
+  }
+  wave_add(&st->trav, trav);
+  wave_add(&st->tokens, tokens);
+  phase_sync(a, single);
+  line_post(a, g, s_hist);
+}
+
+__device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long long* s_hist) {
+  const GridIdx g = grid_idx();
+  LineStats* st = a.st;
+  const int stride = a.la->C + 2;
+  uint64_t trav = 0;
   // P1 + position 1 walks [s, w]; region 1 starts at slot 0
   const uint32_t nS = *a.nS;
   for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
@@ -425,81 +545,32 @@ __global__ __launch_bounds__(kLineBlock) void k_tds_line(LineKernelArgs a) {
       }
     }
   }
-  tree_barrier(a.gbar);
-  uint64_t in_base = 0;
-  for (int k = 1; k <= la.C; ++k) {
-    if (ld_acq(&st->overflow)) break;
-    const uint64_t nin = ld_acq(&st->wn[k]);
-    // next region: 32-slot (128 B) aligned after this one (fresh cache lines)
-    const uint64_t out_base = (in_base + nin * stride + 31) & ~uint64_t(31);
-    if (g.tid == 0) {
-      st->wbase[k] = in_base;
-      st->wbase[k + 1] = out_base;
-    }
-    tokens += g.tid == 0 ? nin : 0;
-    const uint32_t* win = a.wbuf + in_base;
-    for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
-      const uint64_t i = i0 + lane_id();
-      const bool act = i < nin;
-      const uint32_t* w = win + (act ? i : 0) * stride;
-      uint32_t cnt = 0;
-      uint64_t b = 0, L = 0;
-      if (act) {
-        const uint32_t u = w[k];
-        if (pos_ok(a.tpub[u], k, la) && enum_ok(w, k, u, la)) {
-          b = a.offp[u];
-          L = a.mlen[u];
-          trav += a.malive[u];
-          cnt = tds_children(a, w, k, b, L, nullptr, stride);
-        }
-      }
-      const uint64_t pos = wave_reserve(&st->wn[k + 1], cnt);
-      if (cnt) {
-        if (out_base + (pos + cnt) * stride <= a.wcap)
-          tds_children(a, w, k, b, L, a.wbuf + out_base + pos * stride, stride);
-        else
-          atomicOr(&st->overflow, 1u);
-      }
-    }
-    in_base = out_base;
-    tree_barrier(a.gbar);
-  }
-  // terminal keep flags must fit before any terminal effect happens
-  if (ld_acq(&st->overflow) || ld_acq(&st->wn[la.C + 1]) > a.kcap) {
-    if (g.tid == 0) atomicOr(&st->overflow, 1u);
-    wave_add(&st->trav, trav);
-    return;
-  }
-  // terminal position C+1 (tds_batch_1.hpp:641-758)
-  {
-    const int k = la.C + 1;
-    const uint64_t nw = ld_acq(&st->wn[k]);
-    tokens += g.tid == 0 ? nw : 0;
-    uint64_t kept = 0;
-    for (uint64_t i = g.tid; i < nw; i += g.nth) {
-      const uint32_t* w = a.wbuf + in_base + i * stride;
-      const uint32_t u = w[k], s = w[0];
-      uint8_t kp = 0;
-      if (pos_ok(a.tpub[u], k, la)) {
-        if (!la.VC) {
-          if (u != s) {
-            kp = 1;
-            if (a.tpub[s]) a.tsm[s] = 2;
-          }
-        } else if (u == s) {
-          kp = 1;
-          a.tsm[s] = 2;
-        }
-      }
-      a.keep[i] = kp;
-      kept += kp;
-    }
-    wave_add(&st->walks, kept);
-  }
   wave_add(&st->trav, trav);
-  wave_add(&st->tokens, tokens);
   tree_barrier(a.gbar);
-  line_post(a, g, s_hist);
+  const bool single = ld_acq(&st->nsrc) <= kSmallLine && ld_acq(&st->wn[1]) <= kSmallLine;
+  if (!single) tds_rest(a, g, false, s_hist);
+  else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist);
+}
+
+// NLC lines [pl_begin, pl_end) in order, one grid barrier at each line end
+// (the next line's sources see its post-processing).  Stops after a line
+// that overflowed or that deleted with interleave_lp set (the host runs the
+// interleaved LCC, beta.cpp:1163-1197, then relaunches).
+__global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
+    const LineDesc& d = a.lines[pl];
+    LineKernelArgs b = a;
+    b.la = &d.la;
+    b.i0 = d.i0;
+    b.st = a.st + pl;
+    if (d.tds) tds_line(b, s_hist);
+    else path_line(b, s_hist);
+    tree_barrier(a.gbar);
+    const bool stop = ld_acq(&b.st->overflow) || (d.il && ld_acq(&b.st->deleted));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.done = static_cast<unsigned>(pl + 1);
+    if (stop) break;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -527,42 +598,67 @@ static void ensure_hash(Ctx& c, uint64_t want) {
 }
 
 void free_line_buffers(Ctx& c) {
-  void* ptrs[] = {c.d_lstats, c.d_hkey, c.d_hval, c.d_front, c.d_gbar};
+  void* ptrs[] = {c.d_lstats, c.d_hkey, c.d_hval, c.d_front, c.d_gbar, c.d_ldesc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c.d_lstats = nullptr;
   c.d_hkey = c.d_hval = nullptr;
   c.d_front = nullptr;
   c.d_gbar = nullptr;
+  c.d_ldesc = nullptr;
   c.hcap = 0;
 }
 
-bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
-  const NlcLine& line = c.pattern.lines[pl];
-  const bool tds = pl >= 4;  // beta.cpp:762-767
-  const LineArgs la = make_line_args(c, line);
-  const int stride = la.C + 2;
-  if (tds && line.enumeration.size() < static_cast<size_t>(stride))
-    throw std::runtime_error("pattern_non_local_constraint enumeration shorter than the TDS walk");
-  if (la.C + 2 > 18) return false;
+static void upload_lines(Ctx& c) {
+  if (c.d_ldesc) return;
+  const size_t nl = c.pattern.lines.size();
+  std::vector<LineDesc> h(std::max<size_t>(nl, 1));
+  for (size_t pl = 0; pl < nl; ++pl) {
+    const NlcLine& line = c.pattern.lines[pl];
+    h[pl] = LineDesc{};
+    h[pl].la = make_line_args(c, line);
+    h[pl].tds = pl >= 4 ? 1 : 0;
+    h[pl].i0 = static_cast<int32_t>(line.indices[0]);
+    h[pl].il = line.interleave_lp ? 1 : 0;
+  }
+  c.d_ldesc = dmalloc<LineDesc>(h.size());
+  PM_HIP_CHECK(hipMemcpy(c.d_ldesc, h.data(), h.size() * sizeof(LineDesc), hipMemcpyHostToDevice));
+  c.d_lstats_n = nl;
+}
+
+size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow) {
+  const size_t nl = c.pattern.lines.size();
+  overflow = false;
+  outs.clear();
+  if (pl0 >= nl) return 0;
+  for (size_t pl = pl0; pl < nl; ++pl) {
+    const NlcLine& line = c.pattern.lines[pl];
+    const size_t stride = line.cycle_length + 2;
+    if (pl >= 4 && line.enumeration.size() < stride)
+      throw std::runtime_error("pattern_non_local_constraint enumeration shorter than the TDS walk");
+    if (stride > 18) throw std::runtime_error("NLC line longer than 16 positions");
+  }
+  upload_lines(c);
   if (!c.d_lstats) {
-    c.d_lstats = dmalloc<LineStats>(1);
-    c.d_gbar = dmalloc<unsigned>(kGbarWords);
-    PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, kGbarWords * sizeof(unsigned), c.stream));
+    c.d_lstats = dmalloc<LineStats>(std::max<size_t>(nl, 1));
+    c.d_gbar = dmalloc<unsigned>(kGbarWords + 64);
+    PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, (kGbarWords + 64) * sizeof(unsigned), c.stream));
   }
   if (!c.line_grid) {
-    int per_cu = 0, per_cu2 = 0;
-    PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_path_line, kLineBlock, 0));
-    PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_tds_line, kLineBlock, 0));
+    int per_cu = 0;
+    PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lines, kLineBlock, 0));
     hipDeviceProp_t prop;
     PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
-    if (std::min(per_cu, per_cu2) < 1) throw std::runtime_error("fused line kernels cannot be resident");
+    if (per_cu < 1) throw std::runtime_error("fused line kernel cannot be resident");
     // one block per CU: the barrier cost grows with the number of blocks
     c.line_grid = static_cast<unsigned>(std::min<int>(prop.multiProcessorCount, 1024));
   }
   // the table is sized from the superstep-0 matching rows (upper bound of |S|)
   ensure_hash(c, std::max<uint64_t>(1ull << 16, 4 * c.ss0_rows));
-  PM_HIP_CHECK(hipMemsetAsync(c.d_lstats, 0, sizeof(LineStats), c.stream));
+  unsigned* d_done = c.d_gbar + kGbarWords;                                   // [0] lines done
+  auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
+  PM_HIP_CHECK(hipMemsetAsync(c.d_lstats + pl0, 0, (nl - pl0) * sizeof(LineStats), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(d_done, 0, 64 * sizeof(unsigned), c.stream));
   LineKernelArgs a{};
   a.offp = c.d_offp;
   a.mcol = c.d_mcol;
@@ -579,8 +675,6 @@ bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
   a.oa.perm = c.d_perm;
   a.oa.nhubs = static_cast<uint32_t>(c.hubs_host.size());
   a.oa.nranks = c.nranks;
-  a.la = la;
-  a.i0 = static_cast<int>(line.indices[0]);
   a.gbar = c.d_gbar;
   a.hkey = c.d_hkey;
   a.hval = c.d_hval;
@@ -588,60 +682,73 @@ bool run_line_fused(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
   a.front = c.d_front;
   a.fcap = c.hcap / 2;
   a.st = c.d_lstats;
-  if (tds) {
-    c.arena.reset();
-    const uint64_t room = c.arena.cap - 8192;
-    a.kcap = room / (8 * (4 * uint64_t(stride) + 1));  // final walks whose keep flag fits
-    a.keep = static_cast<uint8_t*>(c.arena.get(a.kcap));
-    a.wcap = (c.arena.cap - c.arena.used - 4096) / sizeof(uint32_t);
-    a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
-  }
+  a.lines = c.d_ldesc;
+  a.pl_begin = static_cast<int>(pl0);
+  a.pl_end = static_cast<int>(nl);
+  a.done = d_done;
+  a.kept_ctr = d_kept_ctr;
+  c.arena.reset();
+  const uint64_t room = (c.arena.cap - 8192) / sizeof(uint32_t);
+  a.kept_cap = room / 4;
+  a.kept = static_cast<uint32_t*>(c.arena.get(a.kept_cap * sizeof(uint32_t)));
+  a.wcap = (c.arena.cap - c.arena.used - 4096) / sizeof(uint32_t);
+  a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
   void* args[] = {&a};
-  PM_HIP_CHECK(hipLaunchCooperativeKernel(tds ? reinterpret_cast<const void*>(k_tds_line)
-                                              : reinterpret_cast<const void*>(k_path_line),
-                                          dim3(c.line_grid), dim3(kLineBlock), args, 0, c.stream));
-  LineStats hs;
-  PM_HIP_CHECK(hipMemcpyAsync(&hs, c.d_lstats, sizeof(hs), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(c.line_grid),
+                                          dim3(kLineBlock), args, 0, c.stream));
+  std::vector<LineStats> hs(nl - pl0);
+  unsigned done = 0;
+  unsigned long long kept_slots = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(hs.data(), c.d_lstats + pl0, hs.size() * sizeof(LineStats), hipMemcpyDeviceToHost,
+                              c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(&done, d_done, sizeof(done), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(&kept_slots, d_kept_ctr, sizeof(kept_slots), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  c.nsources = hs.nsrc;
-  if (hs.overflow) {
-    if (!tds) {
-      // partial inserts are not all recorded in the frontier list: clear all, grow
-      const uint64_t grow = c.hcap * 4;
-      PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
-      PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
-      ensure_hash(c, grow);
-    }
-    return false;
+  std::vector<uint32_t> kept;
+  if (want_walks && kept_slots) {
+    kept.resize(kept_slots);
+    PM_HIP_CHECK(hipMemcpy(kept.data(), a.kept, kept_slots * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
-  out.tr.sources = hs.nsrc;
-  out.tr.acked = hs.acked;
-  out.tr.edges = hs.trav;
-  out.tr.tokens = hs.tokens;
-  out.tr.walks = hs.walks;
-  out.deleted = hs.deleted ? 1u : 0u;
-  c.last_acked = hs.acked;
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
-  out.rm_v.assign(c.nranks, 0);
-  out.rm_e.assign(c.nranks, 0);
-  for (uint32_t r = 0; r < c.nranks; ++r) {
-    out.rm_v[r] = hs.removed[r];
-    out.rm_e[r] = hs.removed[P + r];
+  size_t completed = 0;
+  for (unsigned j = 0; j + pl0 < done; ++j) {
+    const LineStats& st = hs[j];
+    const size_t pl = pl0 + j;
+    c.nsources = st.nsrc;
+    if (st.overflow) {
+      overflow = true;
+      if (pl < 4) {
+        // partial inserts are not all recorded in the frontier list: clear all, grow
+        const uint64_t grow = c.hcap * 4;
+        PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+        PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+        ensure_hash(c, grow);
+      }
+      break;
+    }
+    FusedLineOut out;
+    out.tr.sources = st.nsrc;
+    out.tr.acked = st.acked;
+    out.tr.edges = st.trav;
+    out.tr.tokens = st.tokens;
+    out.tr.walks = st.walks;
+    out.deleted = st.deleted ? 1u : 0u;
+    c.last_acked = st.acked;
+    out.rm_v.assign(c.nranks, 0);
+    out.rm_e.assign(c.nranks, 0);
+    for (uint32_t r = 0; r < c.nranks; ++r) {
+      out.rm_v[r] = st.removed[r];
+      out.rm_e[r] = st.removed[P + r];
+    }
+    out.stride = static_cast<uint32_t>(c.pattern.lines[pl].cycle_length + 2);
+    if (pl >= 4 && want_walks && st.walks) {
+      const uint64_t b = st.wbase[0];
+      out.walks.assign(kept.begin() + b, kept.begin() + b + st.walks * out.stride);
+    }
+    outs.push_back(std::move(out));
+    ++completed;
   }
-  out.stride = static_cast<uint32_t>(stride);
-  out.walks.clear();
-  const uint64_t final_walks = tds ? hs.wn[la.C + 1] : 0;
-  if (tds && want_walks && final_walks) {
-    std::vector<uint32_t> all(final_walks * stride);
-    std::vector<uint8_t> kp(final_walks);
-    PM_HIP_CHECK(hipMemcpyAsync(all.data(), a.wbuf + hs.wbase[la.C + 1], all.size() * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, c.stream));
-    PM_HIP_CHECK(hipMemcpyAsync(kp.data(), a.keep, final_walks, hipMemcpyDeviceToHost, c.stream));
-    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-    for (uint64_t i = 0; i < final_walks; ++i)
-      if (kp[i]) out.walks.insert(out.walks.end(), all.begin() + i * stride, all.begin() + (i + 1) * stride);
-  }
-  return true;
+  return completed;
 }
 
 }  // namespace pm
