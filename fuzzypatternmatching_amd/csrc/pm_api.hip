@@ -164,7 +164,7 @@ static void relayout(Ctx& c) {
 static void reset_state(Ctx& c) {
   PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[0], 0, c.n * sizeof(uint16_t), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[1], 0, c.n * sizeof(uint16_t), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(c.d_tsm, 0, c.n, c.stream));
+  // d_tsm needs no reset: only sources are read, and selecting a source resets its entry
   c.smask_valid = false;
   PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(c.d_flags, 0, 4 * sizeof(uint32_t), c.stream));
@@ -766,9 +766,10 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     const unsigned grid = variant >= 16 ? std::min<unsigned>(static_cast<unsigned>(variant), pm::kPartGridMax)
                                         : ctx->k1_grid;
     const int mode = variant >= 16 ? 0 : variant;
-    pm::launch_lcc_first_kernel(*ctx, mode, grid);  // warm
+    pm::ensure_counts(*ctx, 1);
+    pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
     PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
-    for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, mode, grid);
+    for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);
     PM_HIP_CHECK(hipEventRecord(b, ctx->stream));
     PM_HIP_CHECK(hipEventSynchronize(b));
     float ms = 0.f;

@@ -87,19 +87,6 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
   return x;
 }
 
-// Segmented inclusive scan over lanes whose row ids are non-decreasing:
-// OR of the low 16 bits, sum of the high 16 bits.
-__device__ __forceinline__ uint32_t seg_scan_orsum(uint32_t x, int row) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, kWave);
-    const int ry = __shfl_up(row, d, kWave);
-    if (lane >= d && ry == row) x = ((x | y) & 0xFFFFu) + (((x >> 16) + (y >> 16)) << 16);
-  }
-  return x;
-}
-
 // Per-block counter partials (no same-address global atomics: a wave-level
 // atomic per chunk on one word serialises at one L2 channel).  Layout of one
 // block's W = 2P + 4 words: [vertices per rank | edges per rank | traversed |
@@ -117,9 +104,19 @@ __device__ __forceinline__ void acc_owner(unsigned long long* s_hist, const Owne
   atomicAdd(&s_hist[oa.nranks + r], static_cast<unsigned long long>(edges));
 }
 
+// Destination of a kernel's counters: per-block partials, summed into the
+// counter slot by k_reduce_partials (a separate launch: a last-block
+// reduction needs a device-scope release fence per block, which on the
+// multi-XCD MI355X writes back the XCD's dirty L2 lines -- measured 1.7x
+// slower superstep 0).
+struct Partials {
+  unsigned long long* part;
+  unsigned long long* slot;
+};
+
 // All threads of the block must call this (after their loops).
 __device__ __forceinline__ void flush_block(BlockAcc a, const OwnerArgs& oa, unsigned long long* s_hist,
-                                            unsigned long long* s_red, unsigned long long* __restrict__ part) {
+                                            unsigned long long* s_red, const Partials& pp) {
   const int lane = lane_id(), w = threadIdx.x / kWave;
   const uint64_t v[6] = {wave_sum(a.trav), wave_sum(a.match), wave_sum(a.vs), wave_sum(a.es),
                          wave_sum(a.removed), wave_sum(a.asym)};
@@ -128,7 +125,7 @@ __device__ __forceinline__ void flush_block(BlockAcc a, const OwnerArgs& oa, uns
   __syncthreads();
   const uint32_t P = oa.nranks <= 1 ? 1 : oa.nranks;
   const uint32_t W = 2 * P + 4;
-  unsigned long long* out = part + uint64_t(blockIdx.x) * W;
+  unsigned long long* out = pp.part + uint64_t(blockIdx.x) * W;
   if (threadIdx.x < 6) {
     unsigned long long t = 0;
     for (int i = 0; i < kWpb; ++i) t += s_red[i * 6 + threadIdx.x];
@@ -155,15 +152,6 @@ __device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, uint32
   if (lane_id() == 0 && total) base = atomicAdd(ctr, static_cast<unsigned long long>(total));
   base = __shfl(base, 0, kWave);
   return base + incl - n;
-}
-
-__device__ __forceinline__ uint32_t wave_reserve32(uint32_t* ctr, uint32_t n) {
-  const uint64_t incl = wave_incl_scan(n);
-  const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
-  uint32_t base = 0;
-  if (lane_id() == 0 && total) base = atomicAdd(ctr, total);
-  base = __shfl(base, 0, kWave);
-  return base + static_cast<uint32_t>(incl) - n;
 }
 
 // Block-aggregated global add: one atomic per block (all threads must call).

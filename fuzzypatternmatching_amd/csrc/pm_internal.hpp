@@ -124,7 +124,8 @@ struct LineStats {
   unsigned long long nsrc, trav, tokens, acked, deleted, walks, ftotal;
   unsigned long long wn[20];    // TDS walks per position (1..C+1)
   unsigned long long wbase[20]; // TDS: slot offset of each position's walks
-  unsigned int overflow, pad;
+  unsigned int overflow, single;  // single: finished by block 0 alone
+  unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
 };
 
@@ -248,7 +249,7 @@ void build_tiling(Ctx& c);
 // traversed | matching rows | removed flag | asymmetry flag].
 uint32_t slot_words(const Ctx& c);
 void launch_lcc_first(Ctx& c, uint64_t* d_slot);
-void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid);  // variant != 0: ablation builds
+void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot);  // variant != 0: diagnostics
 unsigned lcc_first_grid(const Ctx& c);
 void launch_lcc_step(Ctx& c, uint64_t* d_slot);
 void launch_count_state(Ctx& c, uint64_t* d_slot);

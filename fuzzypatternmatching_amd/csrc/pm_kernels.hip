@@ -32,6 +32,7 @@
 
 namespace pm {
 
+
 // One block: thread t sums blocks t, t+256, ... of every word (independent
 // loads in flight), then a wave + LDS reduction per word.
 __global__ __launch_bounds__(kBlock) void k_reduce_partials(const unsigned long long* __restrict__ part,
@@ -345,18 +346,21 @@ struct K1Tile {
 // G <= 64 slots per row, G = 1 << LG lanes per row, 64/G rows per sub-tile.
 // Compile-time G: the per-row OR reaches the row's first lane through DPP
 // row shifts (+ two cross-row shuffles for G = 32, 64), M positions and
-// counts come from one ballot per sub-tile.
+// counts come from one ballot per sub-tile.  The row verify runs after the
+// kSub sub-tiles, one row per lane (TN and count staged in LDS), so its
+// branches and state stores use full waves; survivor bit r of the tile
+// mask = row r of the tile.
 template <int LG, int MODE, bool WIDE>
 __device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, const RelRuns& rel_runs,
                                          const uint32_t* s_runs, int nruns, const KeepArgs& keep,
                                          const uint16_t* s_adj, const OwnerArgs& oa, const K1Out& o, BlockAcc& acc,
-                                         unsigned long long* s_hist, unsigned long long* tm) {
+                                         unsigned long long* s_hist, unsigned long long* tm, uint32_t* s_rows) {
   constexpr int G = 1 << LG;
   constexpr uint64_t gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
+  constexpr uint32_t R = kTileEntries >> LG;  // rows per tile
   const int lane = lane_id();
   const int k = lane & (G - 1);
   const int lead = lane & ~(G - 1);
-  uint64_t words = 0;  // lane q keeps the survivor mask of sub-tile q
 #pragma unroll 1
   for (int q = 0; q < kSub; ++q) {
     // rolled loop: the slice in use rotates into v[0] (no dynamic register indexing)
@@ -364,7 +368,6 @@ __device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, c
 #pragma unroll
     for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
     const uint16_t tv = vq != kNone ? tbits_rel<WIDE>(vq, rel_runs, s_runs, nruns) : uint16_t(0);
-    const uint32_t rr = static_cast<uint32_t>((T.t0 + q * kWave + lane) >> LG);  // row inside the run
     const uint32_t pv = dpp_wave_shr1(vq);
     const bool ok = vq != kNone;
     const bool first = ok && (k == 0 || pv != vq);
@@ -372,8 +375,9 @@ __device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, c
     const bool contrib = cm && first;
     const uint64_t bal = __ballot(contrib);
     const uint64_t gb = (bal >> lead) & gmask;  // this row's contribution bits
+    const uint32_t rt = static_cast<uint32_t>((q * kWave + lane) >> LG);  // row inside the tile
     if (contrib && !(MODE & 1)) {
-      const uint64_t dst = T.qbase + (uint64_t(rr) << LG) + __builtin_popcountll(gb & ((1ull << k) - 1));
+      const uint64_t dst = T.qbase + ((T.t0 >> LG) + rt) * G + __builtin_popcountll(gb & ((1ull << k) - 1));
       o.mcol[dst] = vq | kAlive;
     }
     uint32_t x = cm ? tv : 0u;
@@ -383,16 +387,27 @@ __device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, c
     if (G >= 16) x |= dpp_row_shl<8>(x);
     if (G >= 32) x |= __shfl_down(x, 16, kWave);
     if (G >= 64) x |= __shfl_down(x, 32, kWave);
+    if (k == 0) s_rows[rt] = (x & T.nm) | (static_cast<uint32_t>(__builtin_popcountll(gb)) << 16);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // verify, one row per lane
+  const uint32_t row0 = static_cast<uint32_t>(T.t0 >> LG);  // first row of the tile in the run
+#pragma unroll 1
+  for (uint32_t w0 = 0; w0 < static_cast<uint32_t>(kSub) * kWave; w0 += kWave) {
     bool surv = false;
-    if (k == 0 && rr < T.nrows) {
-      const uint32_t c = static_cast<uint32_t>(__builtin_popcountll(gb));
-      surv = k1_finish_row(T.start + rr, T.tu, static_cast<uint16_t>(x & T.nm), c, c, s_adj, keep, oa, o, acc,
-                           s_hist);
+    if (w0 < R) {
+      const uint32_t r = w0 + lane;
+      if (r < R && row0 + r < T.nrows) {
+        const uint32_t pk = s_rows[r];
+        const uint32_t c = pk >> 16;
+        surv = k1_finish_row(T.start + row0 + r, T.tu, static_cast<uint16_t>(pk & 0xFFFFu), c, c, s_adj, keep, oa,
+                             o, acc, s_hist);
+      }
     }
     const uint64_t sm = __ballot(surv);
-    if (lane == q) words = sm;
+    if (lane == 0 && !(MODE & 8)) tm[w0 / kWave] = sm;
   }
-  if (lane < kSub && !(MODE & 8)) tm[lane] = words;
+  __builtin_amdgcn_wave_barrier();
 }
 
 // MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores,
@@ -400,16 +415,17 @@ __device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, c
 // store except a checksum of the loaded slots.  WIDE: some range has more
 // than four relevant label runs (tbits_rel scans them all).
 template <int MODE, bool WIDE = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_lcc_first(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, unsigned long long* __restrict__ tmask,
-    unsigned long long* __restrict__ part) {
-  __shared__ KRange s_tab[kMaxRanges];
+    Partials pp) {
+  extern __shared__ KRange s_tab[];  // nr + 1 entries (dynamic LDS)
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
   __shared__ uint32_t s_runs[3 * 16];
+  __shared__ uint32_t s_rows[kWpb][kTileEntries];  // light tiles: TN | count << 16 per row
   for (uint32_t i = threadIdx.x; i <= nr; i += blockDim.x) s_tab[i] = ktab[i];
   load_adj(s_adj, pa);
   if (threadIdx.x < 16) {
@@ -458,7 +474,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         continue;
       }
       const K1Tile T{qbase, t0, start, nrows, tu, nm};
-#define PM_K1L(LG) k1_light<LG, MODE, WIDE>(v, T, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm)
+#define PM_K1L(LG) \
+  k1_light<LG, MODE, WIDE>(v, T, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, s_rows[wid])
       switch (lg) {
         case 0: PM_K1L(0); break;
         case 1: PM_K1L(1); break;
@@ -560,7 +577,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
   }
 #undef PM_TB
-  flush_block(acc, oa, s_hist, s_red, part);
+  flush_block(acc, oa, s_hist, s_red, pp);
 }
 
 // slist from the superstep-0 survivor masks: an exclusive scan of the mask
@@ -586,8 +603,8 @@ __global__ void k_slist_write(const KRange* __restrict__ ktab, uint32_t nr, cons
       const int b = __ffsll(static_cast<long long>(m)) - 1;
       m &= m - 1;
       uint32_t row;
-      if (R.kind <= 6) {
-        row = R.start + static_cast<uint32_t>((uint64_t(rel) * kTileEntries + q * kWave + b) >> R.kind);
+      if (R.kind <= 6) {  // bit r of the tile = row r of the tile
+        row = R.start + rel * (kTileEntries >> R.kind) + q * kWave + b;
       } else if (R.kind <= 10) {
         const uint32_t te = kTileEntries > (1u << R.kind) ? kTileEntries : (1u << R.kind);
         row = R.start + static_cast<uint32_t>((uint64_t(rel) * te) >> R.kind) + b;
@@ -597,16 +614,6 @@ __global__ void k_slist_write(const KRange* __restrict__ ktab, uint32_t nr, cons
       slist[o++] = row;
     }
   }
-}
-
-// Last row r (0..63) of a wave's strip space whose start <= j.
-__device__ __forceinline__ int find_row(const uint64_t* rs, uint64_t j) {
-  int lo = 0, hi = kWave - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (rs[mid] <= j) lo = mid; else hi = mid - 1;
-  }
-  return lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -620,13 +627,46 @@ __device__ __forceinline__ int find_row(const uint64_t* rs, uint64_t j) {
 // removed; else T_pub = T_state, erase flag-0 entries, clear flags.  An entry
 // whose flag was preset by a cycle terminal (nem_1.hpp:764-770) survives one
 // verify without a message; if its neighbour is still in S that breaks the
-// symmetry, which is reported through flags[1] (the host then refuses to go on).
+// symmetry, which is reported through the asymmetry counter (the host then
+// refuses to go on).
+//
+// After superstep 0 the rows are short (a few entries): one lane per row of
+// slist walks its row four entries at a time (four independent loads, then
+// four T_pub gathers); rows above kLprMax entries are walked by the whole
+// wave, one after the other.  Dead 64-entry chunks of slist are skipped
+// through the live mask of the previous superstep.
+static constexpr uint32_t kLprMax = 32;
+
+__device__ __forceinline__ void k2_entry(uint32_t* __restrict__ mcol, uint64_t e, uint32_t m, uint16_t tv,
+                                         uint16_t nm, uint32_t& tn, uint32_t& cnt, bool& asym) {
+  const bool ok = (tv & nm) != 0;
+  const bool fl = (m & kFlag) != 0;
+  const bool flag = ok || fl;
+  const uint32_t m2 = (m & kPosMask) | (flag ? kAlive : 0u);  // flags cleared by verify
+  if (m2 != m) mcol[e] = m2;
+  if (fl && !ok && tv) asym = true;
+  if (ok) tn |= tv;
+  cnt += flag ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint32_t wave_or32(uint32_t x) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) x |= __shfl_xor(x, d, kWave);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) x = max(x, static_cast<uint32_t>(__shfl_xor(x, d, kWave)));
+  return x;
+}
+
 __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
     const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
-    uint32_t* __restrict__ malive, unsigned long long* __restrict__ part) {
+    uint32_t* __restrict__ malive, Partials pp) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -634,11 +674,6 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   load_adj(s_adj, pa);
   __syncthreads();
   BlockAcc acc;
-  __shared__ uint64_t s_rs[kWpb][kWave];
-  __shared__ uint64_t s_beg[kWpb][kWave];
-  __shared__ uint32_t s_acc[kWpb][kWave];
-  __shared__ uint32_t s_cnt[kWpb][kWave];
-  __shared__ uint16_t s_nm[kWpb][kWave];
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t nS = *nSp;
@@ -651,9 +686,9 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     }
     const uint64_t i = chunk * kWave + lane;
     uint32_t u = kNone;
-    uint16_t Tu = 0;
-    uint64_t beg = 0, len = 0;
-    uint32_t alive0 = 0;
+    uint16_t Tu = 0, nm = 0;
+    uint64_t beg = 0;
+    uint32_t len = 0, alive0 = 0;
     if (i < nS && ((live >> lane) & 1ull)) {
       u = slist[i];
       Tu = tcur[u];
@@ -661,67 +696,64 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         beg = offp[u];
         len = mlen[u];
         alive0 = malive[u];
+        nm = nbr_mask(Tu, s_adj);
       } else {
         tnxt[u] = 0;
       }
     }
-    const uint64_t incl = wave_incl_scan(len);
-    const uint64_t total = __shfl(incl, kWave - 1, kWave);
-    s_rs[w][lane] = incl - len;
-    s_beg[w][lane] = beg;
-    s_nm[w][lane] = nbr_mask(Tu, s_adj);
-    s_acc[w][lane] = 0;
-    s_cnt[w][lane] = 0;
-    __builtin_amdgcn_wave_barrier();
+    uint32_t tn = 0, cnt = 0;
     bool asym = false;
-    for (uint64_t j0 = 0; j0 < total; j0 += uint64_t(kWave) * kU) {
-      int r[kU];
-      uint64_t e[kU];
-      uint32_t m[kU];
+    // short rows: one lane per row
+    const bool lng = len > kLprMax;
+    const uint32_t ls = lng ? 0u : len;
+    const uint32_t lmax = wave_max32(ls);
+    for (uint32_t j = 0; j < lmax; j += 4) {
+      uint32_t m[4];
+      uint16_t tv[4];
 #pragma unroll
-      for (int q = 0; q < kU; ++q) {
-        const uint64_t j = j0 + uint64_t(q) * kWave + lane;
-        r[q] = kWave;
-        e[q] = 0;
-        m[q] = 0;
-        if (j < total) {
-          r[q] = find_row(s_rs[w], j);
-          e[q] = s_beg[w][r[q]] + (j - s_rs[w][r[q]]);
-          m[q] = mcol[e[q]];
+      for (int q = 0; q < 4; ++q) m[q] = j + q < ls ? mcol[beg + j + q] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (m[q] & kAlive) k2_entry(mcol, beg + j + q, m[q], tv[q], nm, tn, cnt, asym);
+    }
+    // long rows: the whole wave walks each
+    uint64_t lb = __ballot(lng);
+    while (lb) {
+      const int r = __ffsll(static_cast<long long>(lb)) - 1;
+      lb &= lb - 1;
+      const uint64_t br = (uint64_t(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(beg >> 32), r))) << 32) |
+                          static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(beg), r));
+      const uint32_t lr = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(len), r));
+      const uint16_t nmr = static_cast<uint16_t>(__builtin_amdgcn_readlane(static_cast<int>(nm), r));
+      uint32_t tnr = 0, cntr = 0;
+      for (uint32_t j0 = 0; j0 < lr; j0 += 4 * kWave) {
+        uint32_t m[4];
+        uint16_t tv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t j = j0 + q * kWave + lane;
+          m[q] = j < lr ? mcol[br + j] : 0u;
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (m[q] & kAlive) k2_entry(mcol, br + j0 + q * kWave + lane, m[q], tv[q], nmr, tnr, cntr, asym);
       }
-      uint16_t tv[kU];
-#pragma unroll
-      for (int q = 0; q < kU; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
-#pragma unroll
-      for (int q = 0; q < kU; ++q) {
-        uint32_t x = 0;
-        if (m[q] & kAlive) {
-          const bool ok = (tv[q] & s_nm[w][r[q]]) != 0;
-          const bool fl = (m[q] & kFlag) != 0;
-          const bool flag = ok || fl;
-          const uint32_t nm2 = (m[q] & kPosMask) | (flag ? kAlive : 0u);  // flags cleared by verify
-          if (nm2 != m[q]) mcol[e[q]] = nm2;
-          if (fl && !ok && tv[q]) asym = true;
-          x = (ok ? tv[q] : 0u) | (flag ? (1u << 16) : 0u);
-        }
-        const uint32_t inc = seg_scan_orsum(x, r[q]);
-        const int rnext = __shfl_down(r[q], 1, kWave);
-        if (r[q] < kWave && (lane == kWave - 1 || rnext != r[q])) {
-          s_acc[w][r[q]] |= inc & 0xFFFFu;
-          s_cnt[w][r[q]] += inc >> 16;
-        }
-        __builtin_amdgcn_wave_barrier();
+      tnr = wave_or32(tnr);
+      cntr = static_cast<uint32_t>(wave_sum(cntr));
+      if (lane == r) {
+        tn = tnr;
+        cnt = cntr;
       }
     }
     bool survivor = false, removed = false;
-    uint32_t cnt = 0;
     if (Tu) {
-      const uint16_t TN = static_cast<uint16_t>(s_acc[w][lane] & 0xFFFFu);
-      const uint16_t T = keep_bits(tst[u], TN, s_adj);
+      const uint16_t T = keep_bits(tst[u], static_cast<uint16_t>(tn), s_adj);
       if (T) {
         survivor = true;
-        cnt = s_cnt[w][lane];
         tst[u] = T;
         tnxt[u] = T;
         malive[u] = cnt;
@@ -729,6 +761,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         removed = true;
         tnxt[u] = 0;
         malive[u] = 0;
+        cnt = 0;
       }
     }
     // live mask of the next superstep (S only shrinks); a vertex removed now
@@ -748,7 +781,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
       }
     }
   }
-  flush_block(acc, oa, s_hist, s_red, part);
+  flush_block(acc, oa, s_hist, s_red, pp);
 }
 
 // Counts of the current state (after token-passing post-processing).
@@ -756,7 +789,7 @@ __global__ __launch_bounds__(kBlock) void k_count_state(const uint32_t* __restri
                                                         const uint32_t* __restrict__ nSp,
                                                         const uint16_t* __restrict__ tpub,
                                                         const uint32_t* __restrict__ malive, OwnerArgs oa,
-                                                        unsigned long long* __restrict__ part) {
+                                                        Partials pp) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
@@ -774,7 +807,7 @@ __global__ __launch_bounds__(kBlock) void k_count_state(const uint32_t* __restri
       acc_owner(s_hist, oa, u, malive[u]);
     }
   }
-  flush_block(acc, oa, s_hist, s_red, part);
+  flush_block(acc, oa, s_hist, s_red, pp);
 }
 
 // ---------------------------------------------------------------------------
@@ -802,6 +835,10 @@ void launch_degree_labels(Ctx& c) {
 }
 
 uint32_t slot_words(const Ctx& c) { return 2 * (c.nranks <= 1 ? 1 : c.nranks) + 4; }
+
+static Partials partials(Ctx& c, uint64_t* d_slot) {
+  return Partials{reinterpret_cast<unsigned long long*>(c.d_part), reinterpret_cast<unsigned long long*>(d_slot)};
+}
 
 static void reduce_into(Ctx& c, unsigned grid, uint64_t* d_slot) {
   hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, c.stream,
@@ -1014,13 +1051,14 @@ static K1Out k1_out(Ctx& c) {
   return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mlen, c.d_malive};
 }
 
-void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid) {
+void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
   if (c.ntiles == 0) return;
   if (c.nheavy) PM_HIP_CHECK(hipMemsetAsync(c.d_hscr, 0, 3 * size_t(c.nheavy) * sizeof(uint32_t), c.stream));
 #define PM_K1_ARGS                                                                                                    \
-  dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab, static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,     \
+  dim3(grid), dim3(kBlock), c.ktab.size() * sizeof(KRange), c.stream, c.d_ktab,                                    \
+      static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,                                                  \
       c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c), c.d_hscr, c.nheavy,                                  \
-      reinterpret_cast<unsigned long long*>(c.d_tmask), reinterpret_cast<unsigned long long*>(c.d_part)
+      reinterpret_cast<unsigned long long*>(c.d_tmask), partials(c, d_slot)
   switch (variant) {
     case 0:
       if (c.k1_wide) hipLaunchKernelGGL((k_lcc_first<0, true>), PM_K1_ARGS);
@@ -1042,7 +1080,8 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid) {
 // never more waves than tiles.
 unsigned lcc_first_grid(const Ctx& c) {
   int per_cu = 0;
-  PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lcc_first<0>, kBlock, 0));
+  PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lcc_first<0>, kBlock,
+                                                           c.ktab.size() * sizeof(KRange)));
   hipDeviceProp_t prop;
   PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
   const uint64_t cap = std::min<uint64_t>(kPartGridMax, uint64_t(std::max(per_cu, 1)) * prop.multiProcessorCount);
@@ -1057,7 +1096,7 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot) {
     return;
   }
   const unsigned grid = c.k1_grid;
-  launch_lcc_first_kernel(c, 0, grid);
+  launch_lcc_first_kernel(c, 0, grid, d_slot);
   reduce_into(c, grid, d_slot);
   // slist = survivors in label-major row order
   hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(
@@ -1089,7 +1128,7 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
-                     c.d_malive, reinterpret_cast<unsigned long long*>(c.d_part));
+                     c.d_malive, partials(c, d_slot));
   PM_HIP_CHECK(hipGetLastError());
   reduce_into(c, grid, d_slot);
   c.cur ^= 1;
@@ -1100,7 +1139,7 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
 void launch_count_state(Ctx& c, uint64_t* d_slot) {
   const unsigned grid = grid_for(c.nS_host, kBlock, kMaxGrid);
   hipLaunchKernelGGL(k_count_state, dim3(grid), dim3(kBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tpub[c.cur],
-                     c.d_malive, owner_args(c), reinterpret_cast<unsigned long long*>(c.d_part));
+                     c.d_malive, owner_args(c), partials(c, d_slot));
   PM_HIP_CHECK(hipGetLastError());
   reduce_into(c, grid, d_slot);
 }

@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "pm_device.hpp"
@@ -416,7 +418,11 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
   tree_barrier(a.gbar);
-  const bool single = ld_acq(&st->nsrc) <= kSmallLine && ld_acq(&st->ftotal) <= kSmallLine;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->tstamp[1] = __builtin_amdgcn_s_memrealtime();
+  const uint64_t nsrc = ld_acq(&st->nsrc);
+  if (nsrc == 0) return;  // no tokens, nothing to post-process (every block agrees)
+  const bool single = nsrc <= kSmallLine && ld_acq(&st->ftotal) <= kSmallLine;
+  if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
   if (!single) path_rest(a, g, false, s_hist);
   else if (blockIdx.x == 0) path_rest(a, block_idx(), true, s_hist);
 }
@@ -547,7 +553,11 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   }
   wave_add(&st->trav, trav);
   tree_barrier(a.gbar);
-  const bool single = ld_acq(&st->nsrc) <= kSmallLine && ld_acq(&st->wn[1]) <= kSmallLine;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->tstamp[1] = __builtin_amdgcn_s_memrealtime();
+  const uint64_t nsrc = ld_acq(&st->nsrc);
+  if (nsrc == 0) return;  // no walks, nothing to post-process (every block agrees)
+  const bool single = nsrc <= kSmallLine && ld_acq(&st->wn[1]) <= kSmallLine;
+  if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
   if (!single) tds_rest(a, g, false, s_hist);
   else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist);
 }
@@ -564,9 +574,12 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     b.la = &d.la;
     b.i0 = d.i0;
     b.st = a.st + pl;
+    if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[0] = __builtin_amdgcn_s_memrealtime();
     if (d.tds) tds_line(b, s_hist);
     else path_line(b, s_hist);
+    if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[2] = __builtin_amdgcn_s_memrealtime();
     tree_barrier(a.gbar);
+    if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[3] = __builtin_amdgcn_s_memrealtime();
     const bool stop = ld_acq(&b.st->overflow) || (d.il && ld_acq(&b.st->deleted));
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.done = static_cast<unsigned>(pl + 1);
     if (stop) break;
@@ -710,6 +723,13 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     PM_HIP_CHECK(hipMemcpy(kept.data(), a.kept, kept_slots * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
+  if (std::getenv("PM_PHASE_TIMES"))
+    for (unsigned j = 0; j + pl0 < done; ++j) {
+      const LineStats& st = hs[j];
+      std::fprintf(stderr, "[pm] line %zu: P1 %.1f us, rest %.1f us, end barrier %.1f us (%s, %llu sources)\n",
+                   pl0 + j, (st.tstamp[1] - st.tstamp[0]) * 0.01, (st.tstamp[2] - st.tstamp[1]) * 0.01,
+                   (st.tstamp[3] - st.tstamp[2]) * 0.01, st.single ? "block 0" : "grid", st.nsrc);
+    }
   size_t completed = 0;
   for (unsigned j = 0; j + pl0 < done; ++j) {
     const LineStats& st = hs[j];
