@@ -100,6 +100,7 @@ def main():
         f"final |S|={s0['final_vertices']} |M|={s0['final_edges']}, host {s0['seconds'] * 1e3:.3f} ms, "
         f"device {s0['device_seconds'] * 1e3:.3f} ms, lcc_first kernel {kern_ms:.4f} ms")
 
+    m.close()  # release device memory before the runtime (and any profiler) tears down
     if rank != 0:
         if dist is not None:
             dist.barrier()

@@ -15,7 +15,8 @@ import numpy as np
 
 from . import _abi
 
-__all__ = ["Graph", "rmat_graph", "pattern_summary", "write_graph", "read_graph", "PatternMatcher", "PMError"]
+__all__ = ["Graph", "rmat_graph", "rmat_edges", "pattern_summary", "write_graph", "read_graph", "PatternMatcher",
+           "ShardedPatternMatcher", "partition_edges", "comm_unique_id", "run_beta_local_shards", "PMError"]
 
 DEFAULT_HUB_THRESHOLD = 1048576  # generate_rmat.cpp:106
 
@@ -90,6 +91,82 @@ def rmat_graph(scale, p_gen=1, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
         raise _err()
     off, col = _take_host_csr(off_p, col_p, n.value)
     return Graph(off, col, True, nranks, hub_threshold)
+
+
+def rmat_edges(scale, p_gen, first=0, stride=1):
+    """Directed pairs (u,v),(v,u) of generator ranks first, first+stride, ... < p_gen
+    (generate_rmat.cpp:202-213): the share of one process of a sharded run."""
+    lib = _lib()
+    src_p, dst_p, m = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    if lib.pm_rmat_edges(scale, p_gen, first, stride, ctypes.byref(src_p), ctypes.byref(dst_p), ctypes.byref(m)) != 0:
+        raise _err()
+    k = max(m.value, 1)
+    src = np.ctypeslib.as_array(ctypes.cast(src_p, ctypes.POINTER(ctypes.c_uint32)), shape=(k,))[: m.value].copy()
+    dst = np.ctypeslib.as_array(ctypes.cast(dst_p, ctypes.POINTER(ctypes.c_uint32)), shape=(k,))[: m.value].copy()
+    lib.pm_free_host(src_p)
+    lib.pm_free_host(dst_p)
+    return src, dst
+
+
+def partition_edges(src, dst, n, group=None, device="cpu"):
+    """Owner partitioning of a distributed edge list (delegate_partitioned_graph.ipp:818-969
+    without delegates): every process holds some directed edges; they are exchanged with one
+    all-to-all so that process q receives the edges whose source v has v % world == q.
+
+    Returns (off[n+1] u64 by id -- other owners' rows empty, col u32 sorted within each row,
+    degree[n] u32 global degrees).  Collective over `group` (gloo on CPU, nccl = RCCL on GPU)."""
+    import torch
+    import torch.distributed as dist
+    G = dist.get_world_size(group)
+    s = torch.from_numpy(np.ascontiguousarray(src, dtype=np.int64)).to(device)
+    d = torch.from_numpy(np.ascontiguousarray(dst, dtype=np.int64)).to(device)
+    owner = s % G
+    order = torch.argsort(owner, stable=True)
+    s, d, owner = s[order], d[order], owner[order]
+    send = torch.bincount(owner, minlength=G).to(torch.int64)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    sc, rc = send.tolist(), recv.tolist()
+    rs = torch.empty(sum(rc), dtype=torch.int64, device=device)
+    rd = torch.empty(sum(rc), dtype=torch.int64, device=device)
+    dist.all_to_all_single(rs, s, rc, sc, group=group)
+    dist.all_to_all_single(rd, d, rc, sc, group=group)
+    del s, d, owner, order
+    key = torch.sort(rs * n + rd).values
+    rs, rd = key // n, key % n
+    del key
+    deg = torch.bincount(rs, minlength=n).to(torch.int32)
+    gdeg = deg.clone()
+    dist.all_reduce(gdeg, group=group)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(deg.cpu().numpy().astype(np.uint64))
+    return off, rd.to(torch.int32).cpu().numpy().view(np.uint32).copy(), gdeg.cpu().numpy().view(np.uint32).copy()
+
+
+def comm_unique_id():
+    """RCCL communicator id (bytes) for pm_create_shard; created on one rank, sent to all."""
+    buf = ctypes.create_string_buffer(256)
+    k = _lib().pm_comm_unique_id(buf, len(buf))
+    if k < 0:
+        raise _err()
+    return buf.raw[:k]
+
+
+def run_beta_local_shards(graph, pattern_dir, nshards, result_dir="", max_iterations=0, device=0, labels=None):
+    """The sharded search with `nshards` shards driven by threads of this process on one
+    device (in-process exchange instead of RCCL): parity of the sharded path on one GPU."""
+    desc = _abi.GraphDesc(graph.n, graph.off.ctypes.data, graph.col.ctypes.data, int(graph.symmetric), graph.nranks,
+                          graph.hub_threshold)
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.uint64)
+    if result_dir:
+        os.makedirs(result_dir, exist_ok=True)
+    st = _abi.RunStats()
+    rc = _lib().pm_run_beta_local_shards(ctypes.byref(desc), pattern_dir.encode(), device, nshards,
+                                         None if lab is None else lab.ctypes.data, result_dir.encode(),
+                                         max_iterations, ctypes.byref(st))
+    if rc != 0:
+        raise _err()
+    return st.as_dict()
 
 
 def pattern_summary(pattern_dir):
@@ -189,3 +266,24 @@ class PatternMatcher:
         nbrs = np.zeros(max(ne.value, 1), np.uint32)
         self._check(_lib().pm_export_state(self._ctx, None, None, nbrs.ctypes.data, ctypes.byref(ne)))
         return tpub, mdeg, nbrs[: ne.value]
+
+
+class ShardedPatternMatcher(PatternMatcher):
+    """One rank of a sharded search (one process per GPU; RCCL between the shards).
+
+    off/col/degree come from partition_edges(); unique_id from comm_unique_id() on one rank,
+    distributed to all.  Construction, run_beta, set_labels and export_state are collective."""
+
+    def __init__(self, n, off, col, degree, pattern_dir, nshards, shard, unique_id, device=0, nranks=1,
+                 hub_threshold=DEFAULT_HUB_THRESHOLD, symmetric=True):
+        self._off = np.ascontiguousarray(off, dtype=np.uint64)
+        self._col = np.ascontiguousarray(col if len(col) else np.zeros(1, np.uint32), dtype=np.uint32)
+        self._deg = np.ascontiguousarray(degree, dtype=np.uint32)
+        self.graph = Graph(self._off, self._col[: int(self._off[-1])], symmetric, nranks, hub_threshold)
+        self.graph.n = int(n)
+        self._sdesc = _abi.ShardDesc(n, self._off.ctypes.data, self._col.ctypes.data, self._deg.ctypes.data,
+                                     int(symmetric), nranks, hub_threshold, nshards, shard)
+        uid = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
+        self._ctx = _lib().pm_create_shard(ctypes.byref(self._sdesc), pattern_dir.encode(), device, uid)
+        if not self._ctx:
+            raise _err()

@@ -28,6 +28,20 @@ class GraphDesc(ctypes.Structure):
     ]
 
 
+class ShardDesc(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("off", ctypes.c_void_p),
+        ("col", ctypes.c_void_p),
+        ("degree", ctypes.c_void_p),
+        ("symmetric", ctypes.c_int32),
+        ("nranks", ctypes.c_uint32),
+        ("hub_threshold", ctypes.c_uint64),
+        ("nshards", ctypes.c_uint32),
+        ("shard", ctypes.c_uint32),
+    ]
+
+
 class LccStats(ctypes.Structure):
     _fields_ = [
         ("supersteps", c_u64),
@@ -91,6 +105,12 @@ SIGNATURES = [
     ("pm_pattern_summary", ctypes.c_int, [c_char_p, c_char_p, c_u64]),
     ("pm_debug_time_lcc_first", ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     ("pm_build_arch", c_char_p, []),
+    ("pm_comm_unique_id", ctypes.c_int, [c_vp, c_u64]),
+    ("pm_create_shard", c_vp, [ctypes.POINTER(ShardDesc), c_char_p, ctypes.c_int, c_vp]),
+    ("pm_run_beta_local_shards", ctypes.c_int, [ctypes.POINTER(GraphDesc), c_char_p, ctypes.c_int, c_u32, c_vp,
+                                                c_char_p, c_u64, ctypes.POINTER(RunStats)]),
+    ("pm_rmat_edges", ctypes.c_int, [c_u64, c_u64, c_u64, c_u64, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                                     ctypes.POINTER(c_u64)]),
 ]
 
 _lib = None

@@ -93,19 +93,24 @@ inline Csr build_csr(uint64_t n, const std::vector<std::pair<uint32_t, uint32_t>
   return g;
 }
 
-// All P_gen generator ranks' streams, symmetrized: 2 * 2^S * 16 directed pairs.
-inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs(uint64_t scale, uint64_t p_gen,
-                                                             unsigned threads = hw_threads()) {
+// The streams of generator ranks `vranks` (of P_gen), symmetrized, in rank
+// order: 2 * 2^S * 16 / P_gen directed pairs per rank (generate_rmat.cpp:202-213).
+inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs_of(uint64_t scale, uint64_t p_gen,
+                                                                const std::vector<uint64_t>& vranks,
+                                                                unsigned threads = hw_threads()) {
   if (scale > 32) throw std::runtime_error("scale > 32 not supported (u32 vertex ids)");
+  if (p_gen == 0) throw std::runtime_error("P_gen must be positive");
+  for (uint64_t r : vranks)
+    if (r >= p_gen) throw std::runtime_error("generator rank out of range");
   const uint64_t per_rank = rmat_edges_per_rank(scale, p_gen);
-  std::vector<std::pair<uint32_t, uint32_t>> pairs(2 * per_rank * p_gen);
-  std::atomic<uint64_t> next_rank(0);
+  std::vector<std::pair<uint32_t, uint32_t>> pairs(2 * per_rank * vranks.size());
+  std::atomic<uint64_t> next(0);
   auto worker = [&] {
     for (;;) {
-      const uint64_t r = next_rank.fetch_add(1);
-      if (r >= p_gen) break;
-      RmatStream s(rmat_seed(r), scale);
-      uint64_t base = 2 * per_rank * r;
+      const uint64_t i = next.fetch_add(1);
+      if (i >= vranks.size()) break;
+      RmatStream s(rmat_seed(vranks[i]), scale);
+      uint64_t base = 2 * per_rank * i;
       for (uint64_t e = 0; e < per_rank; ++e) {
         auto uv = s.next_edge();
         pairs[base + 2 * e] = {static_cast<uint32_t>(uv.first), static_cast<uint32_t>(uv.second)};
@@ -114,10 +119,18 @@ inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs(uint64_t scale, uin
     }
   };
   std::vector<std::thread> pool;
-  const unsigned nt = std::max<unsigned>(1, std::min<unsigned>(threads, static_cast<unsigned>(p_gen)));
+  const unsigned nt = std::max<unsigned>(1, std::min<unsigned>(threads, static_cast<unsigned>(vranks.size())));
   for (unsigned t = 0; t < nt; ++t) pool.emplace_back(worker);
   for (auto& th : pool) th.join();
   return pairs;
+}
+
+// All P_gen generator ranks' streams, symmetrized: 2 * 2^S * 16 directed pairs.
+inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs(uint64_t scale, uint64_t p_gen,
+                                                             unsigned threads = hw_threads()) {
+  std::vector<uint64_t> all(p_gen);
+  for (uint64_t r = 0; r < p_gen; ++r) all[r] = r;
+  return rmat_pairs_of(scale, p_gen, all, threads);
 }
 
 inline Csr build_rmat_csr(uint64_t scale, uint64_t p_gen, unsigned threads = hw_threads()) {

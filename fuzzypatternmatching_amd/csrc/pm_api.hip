@@ -23,6 +23,8 @@
 #include "../../include/pm_abi.h"
 #include "host/graph_store.hpp"
 #include "pm_internal.hpp"
+#include "pm_shard.hpp"
+#include <thread>
 
 struct pm_ctx : public pm::Ctx {};
 
@@ -62,18 +64,38 @@ static void require_gfx950(int device) {
     throw std::runtime_error(std::string("device arch ") + prop.gcnArchName + " is not gfx950 (MI355X)");
 }
 
-static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int device) {
-  if (!g || !g->off || !g->col) throw std::runtime_error("pm_create: null graph");
+// Graph of one context: the whole graph (nshards == 1) or one shard's rows.
+struct CtxInput {
+  uint64_t n = 0;
+  const uint64_t* off = nullptr;   // n + 1 offsets of the rows this context scans
+  const uint32_t* col = nullptr;
+  const uint32_t* gdeg = nullptr;  // global degrees (null: from off)
+  bool symmetric = true;
+  uint32_t nranks = 1;
+  uint64_t hub_threshold = 1048576;
+  uint32_t nshards = 1, shard = 0;
+  Comm* comm = nullptr;            // ownership passes to the context
+};
+
+static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int device) {
+  std::unique_ptr<Comm> comm(in.comm);
+  if (!in.off || !in.col) throw std::runtime_error("pm_create: null graph");
+  if (in.nshards == 0 || in.shard >= in.nshards) throw std::runtime_error("pm_create: bad shard index");
+  if (in.nshards > 1 && !comm) throw std::runtime_error("pm_create: sharded context without a communicator");
   require_gfx950(device);
   auto c = std::make_unique<pm_ctx>();
   c->device = device;
   PM_HIP_CHECK(hipSetDevice(device));
   PM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  c->n = g->n;
-  c->nnz = g->off[g->n];
-  c->symmetric = g->symmetric != 0;
-  c->nranks = g->nranks ? g->nranks : 1;
-  c->hub_threshold = g->hub_threshold;
+  c->n = in.n;
+  c->nnz = in.off[in.n];
+  c->symmetric = in.symmetric;
+  c->nranks = in.nranks ? in.nranks : 1;
+  c->hub_threshold = in.hub_threshold;
+  c->nshards = in.nshards;
+  c->shard = in.shard;
+  c->comm = comm.get();
+  c->comm_owned = comm.release();
   if (!c->symmetric)
     throw std::runtime_error("directed (non-symmetric) input graphs are not supported by the GPU path yet");
   if (c->n >= (1ull << 30)) throw std::runtime_error("more than 2^30 vertices (30-bit positions in M entries)");
@@ -85,19 +107,36 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   for (int t = 0; t < c->pa.K; ++t) c->pa.plabel[t] = pg.vertex_data[t];
   for (const auto& l : c->pattern.lines)
     if (l.selected_vertices) throw std::runtime_error("pattern_nlc selected_vertices=1 is not supported yet");
-  for (uint64_t v = 0; v < c->n; ++v)
-    if (g->off[v + 1] - g->off[v] >= c->hub_threshold) c->hubs_host.push_back(v);
-  // device graph + state; padded slot count (label independent)
+  // global degrees (labels, hubs, layout order) and offsets of the rows scanned here
+  c->deg_host.resize(c->n);
+  for (uint64_t v = 0; v < c->n; ++v) {
+    const uint64_t d = in.gdeg ? in.gdeg[v] : in.off[v + 1] - in.off[v];
+    if (d > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
+    if (in.gdeg && in.off[v + 1] - in.off[v] && (in.off[v + 1] - in.off[v] != d || v % c->nshards != c->shard))
+      throw std::runtime_error("shard rows must be the owned rows (v % nshards == shard) with their full degree");
+    c->deg_host[v] = static_cast<uint32_t>(d);
+    if (d >= c->hub_threshold) c->hubs_host.push_back(v);
+  }
+  std::vector<uint64_t> goff;
+  if (in.gdeg) {
+    goff.assign(c->n + 1, 0);
+    for (uint64_t v = 0; v < c->n; ++v) goff[v + 1] = goff[v] + in.gdeg[v];
+  }
+  const uint64_t* off_all = in.gdeg ? goff.data() : in.off;
+  // device graph + state; padded slot count of the rows scanned here (label independent)
   c->nq = 0;
-  for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(g->off[v + 1] - g->off[v]);
+  for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(in.off[v + 1] - in.off[v]);
+  c->mcap = c->nq;
   c->d_off = dalloc<uint64_t>(c->n + 1);
+  c->d_offl = in.gdeg ? dalloc<uint64_t>(c->n + 1) : c->d_off;
   c->d_offp = dalloc<uint64_t>(c->n + 1);
   c->d_offr = dalloc<uint64_t>(c->n + 1);
   c->d_colp = dalloc<uint32_t>(c->nq);
   c->d_perm = dalloc<uint32_t>(c->n);
   c->d_pos = dalloc<uint32_t>(c->n);
   c->d_labs = dalloc<uint64_t>(c->n);
-  PM_HIP_CHECK(hipMemcpy(c->d_off, g->off, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMemcpy(c->d_off, off_all, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  if (in.gdeg) PM_HIP_CHECK(hipMemcpy(c->d_offl, in.off, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   if (!c->hubs_host.empty()) {
     c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
     PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
@@ -121,20 +160,33 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
   size_t free_b = 0, total_b = 0;
   PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
   size_t arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
+  if (c->nshards > 1) arena = std::min<size_t>(arena, size_t(8) << 30);  // in-process groups share one device
   arena = std::max<size_t>(arena, size_t(64) << 20);
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
   // default labels = degree labels; the id-major adjacency is staged in the
   // M column buffer and permuted into the label-major d_colp
-  PM_HIP_CHECK(hipMemcpy(c->d_mcol, g->col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (c->nnz) PM_HIP_CHECK(hipMemcpy(c->d_mcol, in.col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
   launch_degree_labels(*c);
   c->labels_host.assign(c->n, 0);
-  for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(g->off[v + 1] - g->off[v]);
+  for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(c->deg_host[v]);
   build_label_layout(*c, c->d_mcol, false, c->d_colp);
   build_tiling(*c);
   PM_HIP_CHECK(hipStreamSynchronize(c->stream));
   return c.release();
+}
+
+static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int device) {
+  if (!g || !g->off || !g->col) throw std::runtime_error("pm_create: null graph");
+  CtxInput in;
+  in.n = g->n;
+  in.off = g->off;
+  in.col = g->col;
+  in.symmetric = g->symmetric != 0;
+  in.nranks = g->nranks;
+  in.hub_threshold = g->hub_threshold;
+  return create_ctx(in, pattern_dir, device);
 }
 
 static void destroy_ctx(pm_ctx* c) {
@@ -143,9 +195,11 @@ static void destroy_ctx(pm_ctx* c) {
   void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
-                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base};
+                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  delete c->comm_owned;
   free_line_buffers(*c);
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -157,6 +211,7 @@ static void destroy_ctx(pm_ctx* c) {
 static void relayout(Ctx& c) {
   build_label_layout(c, c.d_colp, true, c.d_mcol);
   std::swap(c.d_colp, c.d_mcol);
+  c.mcap = c.nq;  // d_mcol is the former d_colp (nq entries, no remote region)
   build_tiling(c);
   c.lcc_started = false;
 }
@@ -173,6 +228,7 @@ static void reset_state(Ctx& c) {
   c.nS_host = 0;
   c.lcc_started = false;
   c.nsources = 0;
+  c.m_dirty = true;
 }
 
 // Per-superstep outputs of one LCC call.
@@ -182,6 +238,9 @@ struct LccOut {
   std::vector<double> seconds;
   bool not_finished = false;
   uint64_t matching_rows = 0;  // vertices with a label match (superstep 0 of the first call)
+  // this shard's counts: per rank after the last superstep; superstep-0 survivors and M entries
+  std::vector<uint64_t> loc_vc, loc_ec;
+  uint64_t loc_surv = 0, loc_edges = 0;
 };
 
 static void ensure_counts(Ctx& c, size_t slots) {
@@ -209,28 +268,41 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
-      PM_HIP_CHECK(hipEventRecord(ev[D + 1], c.stream));
-      launch_lcc_first(c, slot);
-      PM_HIP_CHECK(hipEventRecord(ev[D + 2], c.stream));
+      launch_lcc_first(c, slot, ev[D + 1], ev[D + 2]);
       k_timed = true;
       // |slist| is read back with the counters at the end of the call; until
       // then later supersteps size their grids by its upper bound
       c.nS_host = static_cast<uint32_t>(std::min<uint64_t>(c.ss0_rows, 0xFFFFFFFFull));
       c.lcc_started = true;
+      shard_after_first(c);  // sharded: every shard's slist, then T_pub
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
       launch_lcc_step(c, slot);
+      shard_exchange_tpub(c);
     }
     PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
   uint32_t nS = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&nS, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-  std::vector<uint64_t> host(D * W);
+  std::vector<uint64_t> host(D * W), local;
+  if (c.comm) {  // this shard's counts, then the sums over the shards
+    local.resize(D * W);
+    PM_HIP_CHECK(hipMemcpyAsync(local.data(), c.d_counts, local.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                c.stream));
+    c.comm->allreduce_sum_u64(c.d_counts, D * W, c.stream);
+  }
   PM_HIP_CHECK(hipMemcpyAsync(host.data(), c.d_counts, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (!c.comm) local = host;
   c.nS_host = nS;
+  c.m_dirty = true;
   LccOut out;
   bool asym = false;
+  {
+    const uint64_t* h = local.data() + (D - 1) * W;
+    out.loc_vc.assign(h, h + c.nranks);
+    out.loc_ec.assign(h + P, h + P + c.nranks);
+  }
   for (uint64_t ss = 0; ss < D; ++ss) {
     const uint64_t* h = host.data() + ss * W;
     std::vector<uint64_t> vc(c.nranks), ec(c.nranks);
@@ -244,8 +316,12 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     if (ss == 0 && init_step) {
       // superstep 0 visits only label-matching rows; their adjacency size is
       // a property of the layout (build_tiling), identical to the reference's count
-      out.trav.back() = c.ss0_trav;
+      out.trav.back() = c.ss0_trav_all;
       out.matching_rows = c.ss0_rows;
+      for (uint32_t r = 0; r < c.nranks; ++r) {  // this shard's survivors (roofline bytes)
+        out.loc_surv += local[r];
+        out.loc_edges += local[P + r];
+      }
     }
     if (h[2 * P + 2]) out.not_finished = true;
     if (h[2 * P + 3]) asym = true;
@@ -338,7 +414,7 @@ static void export_state(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32
   if (c.nq) PM_HIP_CHECK(hipMemcpy(m.data(), c.d_mcol, c.nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
   for (uint64_t v = 0; v < n; ++v) {
     const uint32_t p = pos[v];
-    if (!tp[p]) continue;
+    if (!tp[p] || v % c.nshards != c.shard) continue;  // sharded: owned rows only (export_state_all)
     tpub[v] = tp[p];
     mdeg[v] = malive[p];
     const uint32_t L = mlen[p];
@@ -352,6 +428,43 @@ static void export_state(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32
     }
     if (k != malive[p]) throw std::runtime_error("internal: alive count mismatch in export");
   }
+}
+
+// Sharded: every shard exports the S members it owns; the records
+// [id, T_pub, |M|, neighbours...] are gathered so that each shard returns the
+// whole state, by vertex id (collective).
+static void export_state_all(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32_t>& mdeg,
+                             std::vector<uint32_t>& nbrs) {
+  export_state(c, tpub, mdeg, nbrs);
+  if (!c.comm) return;
+  std::vector<uint32_t> rec;
+  uint64_t pos = 0;
+  for (uint64_t v = 0; v < c.n; ++v) {
+    if (!tpub[v]) continue;
+    const uint32_t k = mdeg[v];
+    if (v % c.nshards == c.shard) {
+      rec.push_back(static_cast<uint32_t>(v));
+      rec.push_back(tpub[v]);
+      rec.push_back(k);
+      rec.insert(rec.end(), nbrs.begin() + pos, nbrs.begin() + pos + k);
+    }
+    pos += k;
+  }
+  const auto parts = shard_allgatherv(c, rec);
+  tpub.assign(c.n, 0);
+  mdeg.assign(c.n, 0);
+  std::vector<std::pair<const std::vector<uint32_t>*, uint64_t>> at(c.n, {nullptr, 0});
+  for (const auto& part : parts)
+    for (uint64_t i = 0; i < part.size(); i += 3 + part[i + 2]) {
+      const uint32_t v = part[i];
+      tpub[v] = static_cast<uint16_t>(part[i + 1]);
+      mdeg[v] = part[i + 2];
+      at[v] = {&part, i + 3};
+    }
+  nbrs.clear();
+  for (uint64_t v = 0; v < c.n; ++v)
+    if (tpub[v]) nbrs.insert(nbrs.end(), at[v].first->begin() + at[v].second,
+                             at[v].first->begin() + at[v].second + mdeg[v]);
 }
 
 static void write_lines(const std::string& path, const std::vector<std::string>& lines) {
@@ -394,7 +507,10 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   };
   // active vertex / edge counts per rank after the latest step
   std::vector<uint64_t> cur_vc(c.nranks, 0), cur_ec(c.nranks, 0);
+  std::vector<uint64_t> loc_vc(c.nranks, 0), loc_ec(c.nranks, 0);  // this shard's share (sharded)
   auto record_lcc = [&](const LccOut& lo, uint64_t itr_) {
+    loc_vc = lo.loc_vc;
+    loc_ec = lo.loc_ec;
     for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
       f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
       add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
@@ -416,11 +532,11 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     auto t0 = tick();
     LccOut lo = lcc_call(c, init_step);
     ph_lcc += since(t0);
-    if (was_init) {
-      first_scanned = lo.trav[0];
+    if (was_init) {  // this shard's superstep-0 kernel (roofline bytes)
+      first_scanned = c.ss0_trav;
       first_matching = lo.matching_rows;
-      for (auto x : lo.vcount[0]) first_surv += x;
-      for (auto x : lo.ecount[0]) first_edges += x;
+      first_surv = lo.loc_surv;
+      first_edges = lo.loc_edges;
     }
     record_lcc(lo, itr);
     nf = nf || lo.not_finished;
@@ -445,7 +561,48 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         FusedLineOut fo;
         bool fused = false;
         auto t1 = tick();
-        if (c.fused_lines && pl != exact_at) {
+        if (c.comm) {
+          // sharded: one line per launch over this shard's sources, then the
+          // line's sums and the post-processed T_pub of every shard
+          shard_replicate_m(c);
+          std::vector<FusedLineOut> one;
+          bool overflow = false;
+          if (c.fused_lines && run_lines_fused(c, pl, files, one, overflow, 1) == 1) {
+            fo = std::move(one[0]);
+            tr = fo.tr;
+            deleted = fo.deleted;
+            for (uint32_t r = 0; r < c.nranks; ++r) {
+              loc_vc[r] -= fo.rm_v[r];
+              loc_ec[r] -= fo.rm_e[r];
+            }
+            walks.swap(fo.walks);
+            stride = fo.stride;
+          } else {
+            tr = pl >= 4 ? run_tds_line(c, line, walks, stride) : run_path_line(c, line);
+            deleted = launch_post_tp(c, line);
+            count_state(c, loc_vc, loc_ec);
+            stride = static_cast<uint32_t>(line.cycle_length + 2);
+          }
+          std::vector<uint64_t> sums = {deleted, tr.sources, tr.acked, tr.edges, tr.tokens, tr.walks};
+          sums.insert(sums.end(), loc_vc.begin(), loc_vc.end());
+          sums.insert(sums.end(), loc_ec.begin(), loc_ec.end());
+          sums = shard_allreduce(c, sums);
+          deleted = sums[0] ? 1u : 0u;
+          tr.sources = sums[1];
+          tr.acked = sums[2];
+          tr.edges = sums[3];
+          tr.tokens = sums[4];
+          tr.walks = sums[5];
+          vc.assign(sums.begin() + 6, sums.begin() + 6 + c.nranks);
+          ec.assign(sums.begin() + 6 + c.nranks, sums.begin() + 6 + 2 * c.nranks);
+          shard_exchange_tpub(c);
+          if (files && pl >= 4) {
+            std::vector<uint32_t> all;
+            for (auto& part : shard_allgatherv(c, walks)) all.insert(all.end(), part.begin(), part.end());
+            walks.swap(all);
+          }
+          ph_tp += since(t1);
+        } else if (c.fused_lines && pl != exact_at) {
           if (pl < batch_pl0 || pl >= batch_pl0 + batch.size()) {
             bool overflow = false;
             const size_t n = run_lines_fused(c, pl, files, batch, overflow);
@@ -457,7 +614,9 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
             fused = true;
           }
         }
-        if (fused) {
+        if (c.comm) {
+          // done above
+        } else if (fused) {
           tr = fo.tr;
           deleted = fo.deleted;
           vc = cur_vc;
@@ -537,7 +696,11 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     // result dump (beta.cpp:1370-1425) -- after pattern_time_end, as in the reference
     std::vector<uint16_t> tpub;
     std::vector<uint32_t> mdeg, nbrs;
-    export_state(c, tpub, mdeg, nbrs);
+    export_state_all(c, tpub, mdeg, nbrs);
+    if (c.shard != 0) {  // shard 0 writes every rank's files
+      if (st) *st = s;
+      return;
+    }
     const std::string d = out_dir + "/0";
     const char* subdirs[] = {"all_ranks_active_vertices_count", "all_ranks_active_edges_count", "all_ranks_messages",
                              "all_ranks_active_vertices", "all_ranks_active_edges", "all_ranks_subgraphs",
@@ -653,6 +816,7 @@ int pm_lcc_bsp(pm_ctx* ctx, int init_step, uint64_t itr, pm_lcc_stats* out) {
 
 int pm_token_passing(pm_ctx* ctx, uint32_t pl, pm_tp_stats* out) {
   PM_API_BODY(ctx, {
+    if (ctx->comm) throw std::runtime_error("pm_token_passing: sharded contexts run lines through pm_run_beta");
     if (pl >= ctx->pattern.lines.size()) throw std::runtime_error("NLC line index out of range");
     const auto& line = ctx->pattern.lines[pl];
     pm::TpResult r;
@@ -689,12 +853,135 @@ int pm_export_state(pm_ctx* ctx, uint16_t* tpub, uint32_t* mdeg, uint32_t* nbrs,
   PM_API_BODY(ctx, {
     std::vector<uint16_t> t;
     std::vector<uint32_t> d, nb;
-    pm::export_state(*ctx, t, d, nb);
+    pm::export_state_all(*ctx, t, d, nb);
     if (tpub) std::copy(t.begin(), t.end(), tpub);
     if (mdeg) std::copy(d.begin(), d.end(), mdeg);
     if (nbrs) std::copy(nb.begin(), nb.end(), nbrs);
     if (n_edges) *n_edges = nb.size();
   });
+}
+
+int pm_comm_unique_id(uint8_t* out, uint64_t len) {
+  try {
+    return static_cast<int>(pm::rccl_unique_id(out, len));
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+pm_ctx* pm_create_shard(const pm_shard_desc* d, const char* pattern_dir, int device, const uint8_t* unique_id) {
+  try {
+    if (!d || !unique_id) throw std::runtime_error("pm_create_shard: null argument");
+    PM_HIP_CHECK(hipSetDevice(device));
+    pm::CtxInput in;
+    in.n = d->n;
+    in.off = d->off;
+    in.col = d->col;
+    in.gdeg = d->degree;
+    if (!in.gdeg) throw std::runtime_error("pm_create_shard: null degree array");
+    in.symmetric = d->symmetric != 0;
+    in.nranks = d->nranks;
+    in.hub_threshold = d->hub_threshold;
+    in.nshards = d->nshards;
+    in.shard = d->shard;
+    // the exchanges run whenever a communicator is present (also for one shard)
+    in.comm = pm::make_rccl_comm(unique_id, static_cast<int>(d->nshards), static_cast<int>(d->shard));
+    return pm::create_ctx(in, pattern_dir, device);
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, int device, uint32_t nshards,
+                             const uint64_t* labels, const char* result_dir, uint64_t max_iterations,
+                             pm_run_stats* out) {
+  try {
+    if (!g || !g->off || !g->col) throw std::runtime_error("pm_run_beta_local_shards: null graph");
+    if (nshards == 0 || nshards > 64) throw std::runtime_error("pm_run_beta_local_shards: 1..64 shards");
+    const uint64_t n = g->n;
+    std::vector<uint32_t> gdeg(n);
+    for (uint64_t v = 0; v < n; ++v) gdeg[v] = static_cast<uint32_t>(g->off[v + 1] - g->off[v]);
+    // owner rule: shard q holds the rows of ids v % nshards == q
+    std::vector<std::vector<uint64_t>> offs(nshards, std::vector<uint64_t>(n + 1, 0));
+    std::vector<std::vector<uint32_t>> cols(nshards);
+    for (uint32_t q = 0; q < nshards; ++q) {
+      for (uint64_t v = 0; v < n; ++v) {
+        const bool own = v % nshards == q;
+        offs[q][v + 1] = offs[q][v] + (own ? gdeg[v] : 0);
+        if (own) cols[q].insert(cols[q].end(), g->col + g->off[v], g->col + g->off[v + 1]);
+      }
+      if (cols[q].empty()) cols[q].push_back(0);
+    }
+    pm::ThreadGroup grp(static_cast<int>(nshards));
+    std::vector<pm_run_stats> st(nshards);
+    std::vector<std::string> errs(nshards);
+    const std::string dir = result_dir ? result_dir : "";
+    auto work = [&](uint32_t q) {
+      std::unique_lock<std::mutex> dev(grp.device);
+      pm_ctx* ctx = nullptr;
+      try {
+        PM_HIP_CHECK(hipSetDevice(device));
+        pm::CtxInput in;
+        in.n = n;
+        in.off = offs[q].data();
+        in.col = cols[q].data();
+        in.gdeg = gdeg.data();
+        in.symmetric = g->symmetric != 0;
+        in.nranks = g->nranks;
+        in.hub_threshold = g->hub_threshold;
+        in.nshards = nshards;
+        in.shard = q;
+        in.comm = pm::make_thread_comm(&grp, static_cast<int>(q));
+        ctx = pm::create_ctx(in, pattern_dir, device);
+        if (labels) {
+          ctx->labels_host.assign(labels, labels + n);
+          PM_HIP_CHECK(hipMemcpy(ctx->d_labels, labels, n * sizeof(uint64_t), hipMemcpyHostToDevice));
+          pm::relayout(*ctx);
+        }
+        pm::run_beta(*ctx, dir, max_iterations, &st[q]);
+      } catch (const std::exception& e) {
+        errs[q] = e.what();
+        grp.abort();
+      }
+      if (ctx) pm::destroy_ctx(ctx);
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t q = 0; q < nshards; ++q) pool.emplace_back(work, q);
+    for (auto& t : pool) t.join();
+    for (uint32_t q = 0; q < nshards; ++q)
+      if (!errs[q].empty() && errs[q] != "another shard failed")
+        throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
+    for (uint32_t q = 0; q < nshards; ++q)
+      if (!errs[q].empty()) throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
+    if (out) *out = st[0];
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t stride, uint32_t** src, uint32_t** dst,
+                  uint64_t* m) {
+  try {
+    if (stride == 0) throw std::runtime_error("pm_rmat_edges: stride 0");
+    std::vector<uint64_t> vr;
+    for (uint64_t r = first; r < p_gen; r += stride) vr.push_back(r);
+    auto pairs = pm::rmat_pairs_of(scale, p_gen, vr);
+    *m = pairs.size();
+    *src = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, pairs.size()) * sizeof(uint32_t)));
+    *dst = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, pairs.size()) * sizeof(uint32_t)));
+    for (size_t i = 0; i < pairs.size(); ++i) {
+      (*src)[i] = pairs[i].first;
+      (*dst)[i] = pairs[i].second;
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
 }
 
 int pm_rmat_csr(uint64_t scale, uint64_t p_gen, uint64_t** off, uint32_t** col, uint64_t* n) {
@@ -767,6 +1054,7 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
                                         : ctx->k1_grid;
     const int mode = variant >= 16 ? 0 : variant;
     pm::ensure_counts(*ctx, 1);
+    pm::lcc_first_prepare(*ctx);
     pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
     PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
     for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);

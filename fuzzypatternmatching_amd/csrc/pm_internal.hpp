@@ -54,6 +54,18 @@ struct LineArgs {
   uint16_t pad;
 };
 
+// Collectives between the shards of one sharded search.  All
+// buffers are device memory; the calls are stream ordered on `s` and every
+// shard makes the same calls in the same order.  RcclComm (one process per
+// GPU, RCCL over xGMI) and ThreadComm (several shards driven by threads of
+// one process on one device, parity tests) implement it (pm_shard.hip).
+struct Comm {
+  virtual ~Comm() {}
+  // recv receives nshards consecutive `bytes` blocks, block g = shard g's send
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  virtual void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) = 0;
+};
+
 // Device scratch arena (bump allocator, reset per NLC line).
 struct Arena {
   char* base = nullptr;
@@ -153,7 +165,9 @@ struct Ctx {
   // vertex positions ordered by (label, degree, id); every device array below
   // is indexed by position and the adjacency holds neighbour positions (each
   // row keeps the id order of the input, so duplicates stay adjacent).
-  uint64_t* d_off = nullptr;      // id-major offsets (degrees), V+1
+  uint64_t* d_off = nullptr;      // id-major offsets of the whole graph (degrees: labels, layout), V+1
+  uint64_t* d_offl = nullptr;     // id-major offsets of this shard's rows (== d_off unsharded), V+1
+  std::vector<uint32_t> deg_host; // global degree by vertex id (tiling bounds)
   uint64_t nq = 0;                // padded slots (label independent)
   uint64_t* d_offp = nullptr;     // label-major padded row starts, V+1
   uint64_t* d_offr = nullptr;     // label-major unpadded offsets (degree sums), V+1
@@ -177,6 +191,27 @@ struct Ctx {
   uint32_t* d_hscr = nullptr;     // 3 x nheavy: TN, distinct count, segments done
   uint64_t ss0_trav = 0;          // adjacency entries of label-matching rows
   uint64_t ss0_rows = 0;          // label-matching rows with degree > 0
+  uint64_t ss0_trav_all = 0;      // ss0_trav summed over the shards
+
+  // sharding: shard `shard` of `nshards` owns the rows of ids v % nshards ==
+  // shard (superstep-0 scans, M rows, LCC updates, NLCC sources); T_pub is
+  // replicated and refreshed after every state change by an all-gather of
+  // the owned slist entries, and before token passing the alive M rows of S
+  // are all-gathered into the remote region of d_mcol (rows of other shards'
+  // vertices then start there: d_offp of a remote position is overwritten).
+  uint32_t nshards = 1, shard = 0;
+  Comm* comm = nullptr;
+  Comm* comm_owned = nullptr;     // deleted with the context
+  uint64_t mcap = 0;              // capacity (entries) of d_colp and d_mcol: nq + remote region
+  uint32_t xmaxS = 0;             // max |slist| over shards (exchange block size)
+  std::vector<uint32_t> xnS;      // |slist| per shard
+  uint32_t* d_xslist = nullptr;   // nshards x xmaxS slist positions of every shard
+  uint32_t* d_xnS = nullptr;      // |slist| per shard (device)
+  uint16_t* d_xsend = nullptr;    // xmaxS T_pub values (packed)
+  uint16_t* d_xrecv = nullptr;    // nshards x xmaxS
+  uint64_t* d_xred = nullptr;     // host-vector all-reduce staging
+  size_t xred_cap = 0;
+  bool m_dirty = true;            // M changed since the last replication
 
   // vertex state (device, by position)
   uint16_t* d_tpub[2] = {nullptr, nullptr};  // template_vertices (T_pub), 0 = not in S
@@ -248,7 +283,9 @@ void build_tiling(Ctx& c);
 // Counter slots: W = slot_words(c) u64 = [vertices per rank | edges per rank |
 // traversed | matching rows | removed flag | asymmetry flag].
 uint32_t slot_words(const Ctx& c);
-void launch_lcc_first(Ctx& c, uint64_t* d_slot);
+// ev0/ev1 (may be null) bracket the kernel launch alone (roofline timing)
+void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+void lcc_first_prepare(Ctx& c);  // zeroes the heavy-row scratch before a launch
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot);  // variant != 0: diagnostics
 unsigned lcc_first_grid(const Ctx& c);
 void launch_lcc_step(Ctx& c, uint64_t* d_slot);
@@ -278,11 +315,22 @@ struct FusedLineOut {
 // outs).  It stops after a line that deleted with interleave_lp set, or before
 // a line that overflowed (overflow = true: rerun that line on the exact-count
 // path).
-size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow);
+// max_lines bounds the lines of one launch (sharded searches run one line per
+// launch: the shards exchange T_pub between lines).
+size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
+                       size_t max_lines = SIZE_MAX);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);
 
 LineArgs make_line_args(const Ctx& c, const NlcLine& line);
+
+// Shard exchanges (pm_shard.hip); no-ops when nshards == 1.
+void shard_after_first(Ctx& c);      // after superstep 0: slists of all shards + T_pub
+void shard_exchange_tpub(Ctx& c);    // T_pub of every shard's slist entries
+void shard_replicate_m(Ctx& c);      // alive M rows of S into the remote region (if m_dirty)
+std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  // host vector, sum
+// Variable-size gather of a host u32 vector: every shard receives all blocks.
+std::vector<std::vector<uint32_t>> shard_allgatherv(Ctx& c, const std::vector<uint32_t>& v);
 
 }  // namespace pm

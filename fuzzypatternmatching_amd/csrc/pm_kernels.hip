@@ -137,41 +137,6 @@ __global__ __launch_bounds__(kBlock) void k_copy_rows(const uint32_t* __restrict
   }
 }
 
-// Run boundaries for the pattern's distinct labels: out[l*kLB + 0] = first
-// position with the label, [1 + k] = first position with padded degree >=
-// 1 << k (k = 0..10), [12] = first with degree > kHeavyDeg, [13] = one past
-// the last position with the label.
-static constexpr int kLB = 14;
-__global__ void k_label_bounds(const uint64_t* __restrict__ labs, const uint64_t* __restrict__ offp, uint64_t n,
-                               const uint64_t* __restrict__ want, int nl, uint64_t* __restrict__ out) {
-  const int l = threadIdx.x;
-  if (l >= nl) return;
-  const uint64_t L = want[l];
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t m = (lo + hi) >> 1;
-    if (labs[m] < L) lo = m + 1; else hi = m;
-  }
-  const uint64_t a = lo;
-  hi = n;
-  while (lo < hi) {
-    const uint64_t m = (lo + hi) >> 1;
-    if (labs[m] <= L) lo = m + 1; else hi = m;
-  }
-  const uint64_t b = lo;
-  out[l * kLB + 0] = a;
-  out[l * kLB + 13] = b;
-  for (int k = 0; k <= 11; ++k) {
-    const uint64_t th = k <= 10 ? (1ull << k) : uint64_t(kHeavyDeg) + 1;
-    uint64_t x = a, y = b;
-    while (x < y) {
-      const uint64_t m = (x + y) >> 1;
-      if (offp[m + 1] - offp[m] < th) x = m + 1; else y = m;
-    }
-    out[l * kLB + 1 + k] = x;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // K1: superstep 0 of the first LCC call fused with its global verify.
 //
@@ -848,7 +813,35 @@ static void reduce_into(Ctx& c, unsigned grid, uint64_t* d_slot) {
 }
 
 // Sorts the vertices by (label, degree, id) (two stable LSD radix passes:
-// degree, then label) and writes the renumbered adjacency into dst.
+// degree, then label) and writes the renumbered adjacency into dst.  Sharded
+// (nshards > 1): by (label, degree class, owner, degree, id) -- two more
+// passes (owner, class) between them -- so every (label, class) run of the
+// tiling splits into one contiguous sub-run per shard while the label runs
+// stay whole.  Keys use the global degrees (d_off); slots and copied rows the
+// shard's own rows (d_offl: other shards' rows are empty here).
+__global__ void k_owner_keys(const uint32_t* __restrict__ ids, uint64_t n, uint32_t nshards,
+                             uint32_t* __restrict__ key) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    key[i] = ids[i] % nshards;
+}
+
+// degree class: 0 for degree 0, 1 + k for padded degree 1 << k (k <= 10), 12 above kHeavyDeg
+__host__ __device__ inline uint32_t degree_class(uint64_t d) {
+  if (d == 0) return 0;
+  if (d > kHeavyDeg) return 12;
+  uint32_t k = 0;
+  while ((1ull << k) < d) ++k;
+  return 1 + k;
+}
+
+__global__ void k_class_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ ids, uint64_t n,
+                             uint32_t* __restrict__ key) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t u = ids[i];
+    key[i] = degree_class(off[u + 1] - off[u]);
+  }
+}
+
 void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst) {
   const uint64_t n = c.n;
   c.arena.reset();
@@ -860,7 +853,7 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
       hipLaunchKernelGGL(k_to_ids, dim3(grid_for(c.nq, kBlock, 65535)), dim3(kBlock), 0, c.stream, src_col, c.nq,
                          c.d_perm);
     } else {
-      PM_HIP_CHECK(hipMemcpyAsync(src_start, c.d_off, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+      PM_HIP_CHECK(hipMemcpyAsync(src_start, c.d_offl, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
     }
     auto* dkey = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
     auto* dkey2 = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
@@ -877,14 +870,24 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
     void* d_tmp = c.arena.get(tmp);
     PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 32,
                                                     c.stream));
+    if (c.nshards > 1) {
+      int obits = 1;
+      while ((1u << obits) < c.nshards) ++obits;
+      hipLaunchKernelGGL(k_owner_keys, dim3(g), dim3(kBlock), 0, c.stream, ids2, n, c.nshards, dkey);
+      PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids2, ids, static_cast<int>(n), 0,
+                                                      obits, c.stream));
+      hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, ids, n, dkey);
+      PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 4,
+                                                      c.stream));
+    }
     hipLaunchKernelGGL(k_gather_labels, dim3(g), dim3(kBlock), 0, c.stream, c.d_labels, ids2, n, lkey);
     PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, lkey, c.d_labs, ids2, c.d_perm, static_cast<int>(n), 0,
                                                     64, c.stream));
     hipLaunchKernelGGL(k_inverse_perm, dim3(g), dim3(kBlock), 0, c.stream, c.d_perm, n, c.d_pos);
-    // label-major offsets: padded (slots) and real (degree sums)
+    // label-major offsets of this shard's rows: padded (slots) and real (degree sums)
     auto* pdeg = lkey;  // reuse
     auto* rdeg = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
-    hipLaunchKernelGGL(k_perm_degrees, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, c.d_perm, n, pdeg, rdeg);
+    hipLaunchKernelGGL(k_perm_degrees, dim3(g), dim3(kBlock), 0, c.stream, c.d_offl, c.d_perm, n, pdeg, rdeg);
     size_t tmp3 = 0;
     PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp3, pdeg, c.d_offp + 1, static_cast<int>(n), c.stream));
     void* d_tmp3 = c.arena.get(tmp3);
@@ -893,7 +896,7 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
     PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_offr, 0, sizeof(uint64_t), c.stream));
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, kWpb, 65535)), dim3(kBlock), 0, c.stream, src_col, src_start,
-                       c.d_off, c.d_offp, c.d_perm, c.d_pos, n, dst);
+                       c.d_offl, c.d_offp, c.d_perm, c.d_pos, n, dst);
     PM_HIP_CHECK(hipGetLastError());
   } else {
     PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
@@ -920,18 +923,38 @@ void build_tiling(Ctx& c) {
     }
   }
   const int nl = static_cast<int>(labs.size());
+  // Run boundaries in the label-major order (host binary searches over
+  // perm_host): B[0] = first position with the label, B[1 + k] = first with
+  // padded degree >= 1 << k (k = 0..10), B[12] = first with degree >
+  // kHeavyDeg, B[13] = one past the label's last position.
+  static constexpr int kLB = 14;
+  const uint64_t n = c.n;
+  auto lab_at = [&](uint64_t i) { return c.labels_host[c.perm_host[i]]; };
+  auto cls_at = [&](uint64_t i) { return degree_class(c.deg_host[c.perm_host[i]]); };
+  auto first_where = [](uint64_t lo, uint64_t hi, auto&& pred) {  // first i in [lo, hi) with pred(i)
+    while (lo < hi) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (pred(m)) hi = m; else lo = m + 1;
+    }
+    return lo;
+  };
   std::vector<uint64_t> bounds(std::max(nl, 1) * kLB, 0);
-  if (nl && c.n) {
-    c.arena.reset();
-    auto* d_want = static_cast<uint64_t*>(c.arena.get(nl * sizeof(uint64_t)));
-    auto* d_out = static_cast<uint64_t*>(c.arena.get(nl * kLB * sizeof(uint64_t)));
-    PM_HIP_CHECK(hipMemcpyAsync(d_want, labs.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_label_bounds, dim3(1), dim3(64), 0, c.stream, c.d_labs, c.d_offp, c.n, d_want, nl, d_out);
-    PM_HIP_CHECK(hipGetLastError());
-    PM_HIP_CHECK(hipMemcpyAsync(bounds.data(), d_out, nl * kLB * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-    c.arena.reset();
+  for (int l = 0; l < nl; ++l) {
+    uint64_t* B = bounds.data() + l * kLB;
+    const uint64_t L = labs[l];
+    B[0] = first_where(0, n, [&](uint64_t i) { return lab_at(i) >= L; });
+    B[13] = first_where(B[0], n, [&](uint64_t i) { return lab_at(i) > L; });
+    for (uint32_t k = 0; k <= 11; ++k)
+      B[1 + k] = first_where(B[0], B[13], [&](uint64_t i) { return cls_at(i) >= 1 + k; });
   }
+  // this shard's sub-run of [a, b) (positions are owner-sorted inside a run)
+  auto owned = [&](uint64_t a, uint64_t b) {
+    if (c.nshards <= 1) return std::make_pair(a, b);
+    const uint32_t G = c.nshards, me = c.shard;
+    const uint64_t x = first_where(a, b, [&](uint64_t i) { return c.perm_host[i] % G >= me; });
+    const uint64_t y = first_where(x, b, [&](uint64_t i) { return c.perm_host[i] % G > me; });
+    return std::make_pair(x, y);
+  };
   auto dev_at = [&](const uint64_t* arr, uint64_t i) {
     uint64_t x = 0;
     PM_HIP_CHECK(hipMemcpy(&x, arr + i, sizeof(x), hipMemcpyDeviceToHost));
@@ -957,14 +980,15 @@ void build_tiling(Ctx& c) {
       if ((tu >> t) & 1u) nm |= c.pa.adj[t];
     const uint64_t first_nz = B[1], hi = B[13];
     if (hi <= first_nz) continue;
-    c.ss0_rows += hi - first_nz;
+    // other shards' rows are empty in offr
     c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
-    if (!nm) continue;  // such rows never enter S (TN = 0): scanned by no kernel, counted above
     // kind k = [B[1+k], B[2+k]) for k = 0..10 (padded degree 1 << k); kind 11 = [B[12], hi)
     for (int kind = 0; kind <= kHeavyKind; ++kind) {
-      const uint64_t a = B[1 + kind];
-      const uint64_t b = kind == kHeavyKind ? hi : B[2 + kind];
+      const auto ab = owned(B[1 + kind], kind == kHeavyKind ? hi : B[2 + kind]);
+      const uint64_t a = ab.first, b = ab.second;
       if (b <= a) continue;
+      c.ss0_rows += b - a;
+      if (!nm) continue;  // such rows never enter S (TN = 0): scanned by no kernel, counted above
       KRange R{};
       R.tile0 = tiles;
       R.start = static_cast<uint32_t>(a);
@@ -1013,6 +1037,12 @@ void build_tiling(Ctx& c) {
       tab.push_back(R);
     }
   }
+  if (c.comm) {
+    std::vector<uint64_t> t = shard_allreduce(c, {c.ss0_trav});
+    c.ss0_trav_all = t[0];
+  } else {
+    c.ss0_trav_all = c.ss0_trav;
+  }
   if (tab.size() + 1 > static_cast<size_t>(kMaxRanges)) throw std::runtime_error("internal: too many tile ranges");
   KRange sent{};
   sent.tile0 = tiles;
@@ -1053,7 +1083,6 @@ static K1Out k1_out(Ctx& c) {
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
   if (c.ntiles == 0) return;
-  if (c.nheavy) PM_HIP_CHECK(hipMemsetAsync(c.d_hscr, 0, 3 * size_t(c.nheavy) * sizeof(uint32_t), c.stream));
 #define PM_K1_ARGS                                                                                                    \
   dim3(grid), dim3(kBlock), c.ktab.size() * sizeof(KRange), c.stream, c.d_ktab,                                    \
       static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,                                                  \
@@ -1088,15 +1117,24 @@ unsigned lcc_first_grid(const Ctx& c) {
   return grid_for(c.ntiles, kWpb, static_cast<unsigned>(cap));
 }
 
-void launch_lcc_first(Ctx& c, uint64_t* d_slot) {
+void lcc_first_prepare(Ctx& c) {
+  if (c.nheavy) PM_HIP_CHECK(hipMemsetAsync(c.d_hscr, 0, 3 * size_t(c.nheavy) * sizeof(uint32_t), c.stream));
+}
+
+void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) {
   if (c.ntiles == 0) {
+    if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
+    if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
     PM_HIP_CHECK(hipMemsetAsync(d_slot, 0, slot_words(c) * sizeof(uint64_t), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
     c.smask_valid = false;
     return;
   }
   const unsigned grid = c.k1_grid;
+  lcc_first_prepare(c);
+  if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
   launch_lcc_first_kernel(c, 0, grid, d_slot);
+  if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
   reduce_into(c, grid, d_slot);
   // slist = survivors in label-major row order
   hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(

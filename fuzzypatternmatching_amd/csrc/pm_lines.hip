@@ -639,8 +639,10 @@ static void upload_lines(Ctx& c) {
   c.d_lstats_n = nl;
 }
 
-size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow) {
-  const size_t nl = c.pattern.lines.size();
+size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
+                       size_t max_lines) {
+  const size_t nl_all = c.pattern.lines.size();
+  const size_t nl = pl0 < nl_all && max_lines < nl_all - pl0 ? pl0 + max_lines : nl_all;
   overflow = false;
   outs.clear();
   if (pl0 >= nl) return 0;
@@ -653,7 +655,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   }
   upload_lines(c);
   if (!c.d_lstats) {
-    c.d_lstats = dmalloc<LineStats>(std::max<size_t>(nl, 1));
+    c.d_lstats = dmalloc<LineStats>(std::max<size_t>(nl_all, 1));
     c.d_gbar = dmalloc<unsigned>(kGbarWords + 64);
     PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, (kGbarWords + 64) * sizeof(unsigned), c.stream));
   }

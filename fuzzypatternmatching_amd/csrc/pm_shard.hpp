@@ -1,0 +1,33 @@
+// Comm factories and the in-process shard group (pm_shard.hip).
+#pragma once
+
+#include <condition_variable>
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "pm_internal.hpp"
+
+namespace pm {
+
+// Shards of one search driven by threads of one process on one device.
+struct ThreadGroup {
+  explicit ThreadGroup(int n_) : n(n_), ptrs(n_, nullptr), hvec(n_, nullptr) {}
+  int n;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<const void*> ptrs;
+  std::vector<std::vector<uint64_t>*> hvec;
+  std::mutex device;  // held by the shard that is computing (released inside collectives)
+  void barrier();     // throws when another shard failed
+  void abort();
+};
+
+Comm* make_rccl_comm(const void* unique_id, int nranks, int rank);
+size_t rccl_unique_id(void* out, size_t len);
+Comm* make_thread_comm(ThreadGroup* g, int rank);
+
+}  // namespace pm

@@ -24,6 +24,15 @@
  *                                 result file: src/run_pattern_matching_beta.cpp:539-1425
  *   pm_export_state               vertex_state_map / template_vertices / vertex_active_edges_map
  *                                 read-out used by the result writers (beta.cpp:1386-1425)
+ *   pm_create_shard               one rank of the delegate-partitioned graph (owner = id % P,
+ *                                 include/havoqgt/delegate_partitioned_graph.ipp:1679-1696) with the
+ *                                 mailbox exchange (include/havoqgt/new_mailbox.hpp:289-713) and the
+ *                                 delegate reductions (impl/vertex_data.hpp:114-126) replaced by RCCL
+ *                                 collectives between supersteps
+ *   pm_comm_unique_id             the RCCL communicator id rank 0 hands to every rank (the role of
+ *                                 MPI_COMM_WORLD set up by havoqgt_init, environment.hpp:136-228)
+ *   pm_rmat_edges                 the edge stream of some generator ranks of generate_rmat
+ *                                 (src/generate_rmat.cpp:202-213, rmat_edge_generator.hpp:218-261)
  *
  * Conventions: plain C types; int status (0 = OK, negative = error with
  * pm_last_error()); device memory is owned by the context; host buffers are
@@ -84,6 +93,19 @@ typedef struct pm_run_stats {
   uint64_t lcc_first_bytes;     /* algorithmic bytes of that kernel                 */
 } pm_run_stats;
 
+/* One shard (rank) of a sharded search: the rows of ids v % nshards == shard. */
+typedef struct pm_shard_desc {
+  uint64_t n;               /* global number of vertex ids                                   */
+  const uint64_t* off;      /* n + 1 offsets by id: the owned rows, every other row empty    */
+  const uint32_t* col;      /* off[n] targets of the owned rows, sorted within each row      */
+  const uint32_t* degree;   /* n global degrees (degree labels, label-major order)           */
+  int32_t symmetric;
+  uint32_t nranks;          /* P used to name per-rank result files (owner rule)              */
+  uint64_t hub_threshold;
+  uint32_t nshards;         /* shards of the search (one per GPU / process)                  */
+  uint32_t shard;
+} pm_shard_desc;
+
 /* Context: uploads the CSR to device `device`, loads <pattern_dir>/0/pattern_*.
  * Returns NULL on failure (message via pm_last_error(NULL)). */
 pm_ctx* pm_create(const pm_graph_desc* graph, const char* pattern_dir, int device);
@@ -115,7 +137,24 @@ int pm_run_beta(pm_ctx* ctx, const char* result_dir, uint64_t max_iterations, pm
  * nbrs must hold that many entries, written row by row in vertex order. */
 int pm_export_state(pm_ctx* ctx, uint16_t* tpub, uint32_t* mdeg, uint32_t* nbrs, uint64_t* n_edges);
 
+/* Sharded search, one process per GPU: rank 0 creates the id (>= 128 bytes, returns its
+ * length), every rank receives it and calls pm_create_shard collectively; pm_run_beta,
+ * pm_lcc_bsp, pm_vertex_data_* and pm_export_state are then collective over the shards.
+ * Result files and pm_run_stats cover the whole graph (shard 0 writes the files). */
+int pm_comm_unique_id(uint8_t* out, uint64_t len);
+pm_ctx* pm_create_shard(const pm_shard_desc* shard, const char* pattern_dir, int device, const uint8_t* unique_id);
+
+/* nshards shards of one search run by threads of this process on one device (the
+ * partitioning of pm_create_shard with an in-process exchange): parity of the sharded
+ * path on a single GPU.  labels may be NULL (degree labels). */
+int pm_run_beta_local_shards(const pm_graph_desc* graph, const char* pattern_dir, int device, uint32_t nshards,
+                             const uint64_t* labels, const char* result_dir, uint64_t max_iterations,
+                             pm_run_stats* out);
+
 /* Host-side input builders (no device needed). */
+/* Directed pairs (u,v),(v,u) of generator ranks first, first + stride, ... < p_gen. */
+int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t stride, uint32_t** src, uint32_t** dst,
+                  uint64_t* m);
 int pm_rmat_csr(uint64_t scale, uint64_t p_gen, uint64_t** off, uint32_t** col, uint64_t* n);
 void pm_free_host(void* p);
 int pm_write_graph(const char* base, uint64_t n, const uint64_t* off, const uint32_t* col, int symmetric,

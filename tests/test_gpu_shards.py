@@ -1,0 +1,105 @@
+"""GPU parity of the sharded search against the CPU oracle.
+
+The shards run as threads of this process on the one device of the test box
+(pm_run_beta_local_shards: the partitioning, tiling and exchanges of the
+multi-GPU path with an in-process Comm in place of RCCL); the RCCL Comm itself
+is exercised with one rank (pm_create_shard).  Results must equal the oracle's
+for every shard count."""
+import os
+
+import numpy as np
+import pytest
+
+import fuzzypatternmatching_amd as pm
+import oracle
+import pmtest
+
+pytestmark = pytest.mark.gpu
+
+PATTERNS = {
+    "tree": os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern"),
+    "cycle": os.path.join(pmtest.ROOT, "patterns", "rmat_log2_cycle4_pattern"),
+}
+
+# (pattern, scale, P_gen, label alphabet or None, result-file ranks, shards)
+SHARD_CASES = [
+    ("tree", 14, 4, None, 1, 2),
+    ("tree", 16, 4, None, 4, 3),
+    ("cycle", 12, 4, 8, 3, 2),
+    ("cycle", 14, 4, None, 1, 4),
+    ("tree", 10, 1, 16, 1, 4),
+    ("cycle", 10, 1, 8, 2, 1),
+]
+
+
+def _check(so, sg):
+    assert sg["iterations"] == so["iterations"] and sg["terminated"] == so["terminated"]
+    assert sg["final_vertices"] == so["final_vertices"] and sg["final_edges"] == so["final_edges"]
+    assert sg["lcc_edges"] == so["lcc_edges"]
+    assert sg["nlcc_edges"] == so["nlcc_edges"]
+    assert sg["tds_edges"] == so["tds_edges"]
+    assert sg["walks"] == so["paths"]
+
+
+def _run_both(off, col, pattern, tmp_path, shards, labels=None, nranks=1, max_iterations=100):
+    a, b = tmp_path / "oracle", tmp_path / "shards"
+    so = oracle.run(off, col, pattern, str(a), labels=labels, nranks=nranks, max_iterations=max_iterations)
+    g = pm.Graph(off, col, True, nranks)
+    sg = pm.run_beta_local_shards(g, pattern, shards, str(b), max_iterations=max_iterations, labels=labels)
+    return so, sg, pmtest.compare_result_dirs(str(a), str(b), nranks)
+
+
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards", SHARD_CASES)
+def test_sharded_rmat_matches_oracle(pat, scale, p_gen, alphabet, nranks, shards, tmp_path):
+    g = pm.rmat_graph(scale, p_gen)
+    labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, shards, labels, nranks)
+    assert diffs == []
+    _check(so, sg)
+
+
+def test_sharded_exact_count_lines(tmp_path, monkeypatch):
+    monkeypatch.setenv("PM_FUSED_LINES", "0")
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS["cycle"], tmp_path, 3, labels, 3)
+    assert diffs == []
+    _check(so, sg)
+
+
+def test_sharded_known_answers(tmp_path):
+    # tiny graphs: most shards own no state-map vertex at all
+    pairs = [(0, 1), (1, 2), (1, 3), (3, 5), (4, 5), (5, 6)]
+    labels = np.array([3, 4, 7, 2, 3, 5, 7], np.uint64)
+    off, col = pmtest.symmetric_csr(pairs, 7)
+    for shards in (2, 5):
+        so, sg, diffs = _run_both(off, col, PATTERNS["tree"], tmp_path / str(shards), shards, labels)
+        assert diffs == []
+        assert sg["final_vertices"] == 7 and sg["walks"] == 1
+    off0 = np.zeros(9, np.uint64)
+    so, sg, diffs = _run_both(off0, np.zeros(0, np.uint32), PATTERNS["tree"], tmp_path / "empty", 3,
+                              np.full(8, 3, np.uint64))
+    assert diffs == [] and sg["final_vertices"] == 0
+
+
+def test_sharded_non_termination_cap(tmp_path):
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS["cycle"], tmp_path, 2, labels, max_iterations=1)
+    assert diffs == []
+    assert sg["terminated"] == so["terminated"] == 0
+
+
+def test_rccl_shard_single_rank(tmp_path):
+    # pm_create_shard with one rank: the RCCL communicator carries every
+    # exchange of the sharded driver (all-gathers and all-reduces of one rank)
+    g = pm.rmat_graph(12, 4)
+    deg = np.diff(g.off).astype(np.uint32)
+    uid = pm.comm_unique_id()
+    assert len(uid) >= 128
+    m = pm.ShardedPatternMatcher(g.n, g.off, g.col, deg, PATTERNS["tree"], 1, 0, uid, nranks=2)
+    sg = m.run_beta(str(tmp_path / "rccl"), max_iterations=100)
+    m.close()
+    so = oracle.run(g.off, g.col, PATTERNS["tree"], str(tmp_path / "oracle"), nranks=2, max_iterations=100)
+    assert pmtest.compare_result_dirs(str(tmp_path / "oracle"), str(tmp_path / "rccl"), 2) == []
+    _check(so, sg)
