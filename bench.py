@@ -12,9 +12,14 @@ Edges traversed: adjacency entries scanned by LCC senders
 (full CSR degree in superstep 0 of the first call, |M[v]| later) plus those
 scanned by NLCC/TDS initiators and relays; counted identically by the oracle.
 
-N > 1 GPUs (torch.distributed.run, one process per GPU): every rank runs an
-independent replica of the workload ("replicas", weak scaling) -- see
-DESIGN.md "Multi-GPU" for why and what the sharded design is.
+N > 1 GPUs (torch.distributed.run, one process per GPU): ONE search over one
+graph sharded across the ranks (owner = id % N rows per GPU, RCCL exchanges
+between supersteps).  Weak scaling: the default graph
+grows with N -- scale 24 + log2(N) from 4N generator ranks, so every GPU holds
+the edge count of the one-GPU config; each process generates the stream of
+its own generator ranks and the edges reach their owners in one all-to-all
+(untimed setup).  `value` = edges traversed by the whole search / max-over-
+ranks time.
 """
 import argparse
 import json
@@ -38,11 +43,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scale", type=int, default=24)
-    ap.add_argument("--p-gen", type=int, default=4)
+    ap.add_argument("--scale", type=int, default=None, help="default 24 + log2(N)")
+    ap.add_argument("--p-gen", type=int, default=None, help="default 4 N")
     ap.add_argument("--pattern", default="rmat_log2_tree_pattern")
     ap.add_argument("--max-iterations", type=int, default=64)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--graph-cache", default=os.environ.get("PM_GRAPH_CACHE"),
+                    help="directory: reuse / store the generated one-GPU graph (repeated profiling runs)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="take the sharded (RCCL) path even at N=1 (rehearsal of the multi-GPU code on one GPU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_lcc_first.json"))
     args = ap.parse_args()
 
@@ -50,7 +59,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
@@ -59,13 +69,45 @@ def main():
     import numpy as np
     import fuzzypatternmatching_amd as pm
 
+    if args.scale is None:
+        args.scale = 24 + max(0, (world - 1).bit_length())
+    if args.p_gen is None:
+        args.p_gen = 4 * world
     pattern_dir = os.path.join(ROOT, "patterns", args.pattern)
     t0 = time.time()
-    g = pm.rmat_graph(args.scale, args.p_gen)
-    log(f"[rank {rank}] generated R-MAT S={args.scale} P_gen={args.p_gen}: V={g.n} E={g.nnz} "
-        f"in {time.time() - t0:.1f}s")
-    t0 = time.time()
-    m = pm.PatternMatcher(g, pattern_dir, device=local_rank if world > 1 else 0)
+    g = None
+    if not sharded:
+        cache = (os.path.join(args.graph_cache, f"rmat_s{args.scale}_p{args.p_gen}") if args.graph_cache else None)
+        if cache and os.path.exists(cache + "_0_of_1"):
+            g = pm.read_graph(cache)
+        else:
+            g = pm.rmat_graph(args.scale, args.p_gen)
+            if cache:
+                os.makedirs(args.graph_cache, exist_ok=True)
+                pm.write_graph(cache, g, 1)
+        n, nnz = g.n, g.nnz
+        log(f"[rank {rank}] generated R-MAT S={args.scale} P_gen={args.p_gen}: V={g.n} E={g.nnz} "
+            f"in {time.time() - t0:.1f}s")
+        t0 = time.time()
+        m = pm.PatternMatcher(g, pattern_dir, device=0)
+    else:
+        import torch
+        n = 1 << args.scale
+        src, dst = pm.rmat_edges(args.scale, args.p_gen, rank, world)
+        log(f"[rank {rank}] generated {src.shape[0]} directed edges of R-MAT S={args.scale} P_gen={args.p_gen} "
+            f"(generator ranks {rank}::{world}) in {time.time() - t0:.1f}s")
+        t0 = time.time()
+        off, col, deg = pm.partition_edges(src, dst, n, device=f"cuda:{local_rank}")
+        del src, dst
+        t = torch.tensor([int(off[-1])], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        nnz = int(t.item())
+        uid = [pm.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        log(f"[rank {rank}] owner partitioning: {int(off[-1])} of {nnz} entries in {time.time() - t0:.1f}s")
+        t0 = time.time()
+        m = pm.ShardedPatternMatcher(n, off, col, deg, pattern_dir, world, rank, uid[0], device=local_rank)
+        del off, col, deg
     log(f"[rank {rank}] uploaded graph in {time.time() - t0:.1f}s")
 
     def barrier_sync():
@@ -83,6 +125,7 @@ def main():
         stats.append(m.run_beta("", args.max_iterations))
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    # the stats of a sharded search already cover the whole graph (every rank reports the same)
     edges = sum(s["lcc_edges"] + s["nlcc_edges"] + s["tds_edges"] for s in stats)
     kern_ms = float(np.mean([s["lcc_first_kernel_ms"] for s in stats]))
     kern_bytes = stats[-1]["lcc_first_bytes"]
@@ -91,9 +134,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        e = torch.tensor([edges], dtype=torch.float64, device="cuda")
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        edges = int(e.item())
     s0 = stats[-1]
     log(f"[rank {rank}] per step: {s0['iterations']} iterations (terminated={s0['terminated']}), "
         f"lcc {s0['lcc_edges']} nlcc {s0['nlcc_edges']} tds {s0['tds_edges']} edges, walks {s0['walks']}, "
@@ -121,7 +161,7 @@ def main():
                 "algorithmic_bytes_per_launch": kern_bytes, "avg_launch_ms": round(kern_ms, 5)}
 
     cpu = None
-    if args.cpu_baseline == "auto" and world == 1:
+    if args.cpu_baseline == "auto" and not sharded:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         t0 = time.time()
@@ -149,11 +189,14 @@ def main():
         "dtype": "u16",
         "data": "synthetic R-MAT (generate_rmat.cpp stream, a,b,c,d=.57/.19/.19/.05, scrambled, symmetrized), "
                 "degree-log2 labels",
-        "config": {"workload": f"C2: R-MAT scale-{args.scale} (P_gen={args.p_gen}) + {args.pattern}, "
-                               f"full LCC+NLCC driver loop per step",
+        "config": {"workload": (f"C2: R-MAT scale-{args.scale} (P_gen={args.p_gen}) + {args.pattern}, "
+                                f"full LCC+NLCC driver loop per step" if not sharded else
+                                f"R-MAT scale-{args.scale} (P_gen={args.p_gen}) + {args.pattern}, one search "
+                                f"sharded over {world} GPUs (owner = id % {world}), full LCC+NLCC driver loop "
+                                f"per step"),
                    "scale": args.scale, "p_gen": args.p_gen, "pattern": args.pattern,
-                   "vertices": g.n, "directed_entries": g.nnz,
-                   "parallelism": "single" if world == 1 else f"replicas{world}"},
+                   "vertices": n, "directed_entries": nnz,
+                   "parallelism": "single" if not sharded else f"shard{world}"},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
@@ -165,3 +208,8 @@ def main():
 
 if __name__ == "__main__":
     main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    # skip interpreter teardown: the HIP runtime's exit handlers crash under
+    # rocprofv3's finalised tool (SIGSEGV after the profile is written)
+    os._exit(0)

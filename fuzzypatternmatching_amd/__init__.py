@@ -101,11 +101,11 @@ def rmat_edges(scale, p_gen, first=0, stride=1):
     if lib.pm_rmat_edges(scale, p_gen, first, stride, ctypes.byref(src_p), ctypes.byref(dst_p), ctypes.byref(m)) != 0:
         raise _err()
     k = max(m.value, 1)
-    src = np.ctypeslib.as_array(ctypes.cast(src_p, ctypes.POINTER(ctypes.c_uint32)), shape=(k,))[: m.value].copy()
-    dst = np.ctypeslib.as_array(ctypes.cast(dst_p, ctypes.POINTER(ctypes.c_uint32)), shape=(k,))[: m.value].copy()
-    lib.pm_free_host(src_p)
-    lib.pm_free_host(dst_p)
-    return src, dst
+    out = []
+    for p in (src_p, dst_p):  # one array at a time: peak host memory = output + one stream copy
+        out.append(np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(k,))[: m.value].copy())
+        lib.pm_free_host(p)
+    return out[0], out[1]
 
 
 def partition_edges(src, dst, n, group=None, device="cpu"):
@@ -118,8 +118,9 @@ def partition_edges(src, dst, n, group=None, device="cpu"):
     import torch
     import torch.distributed as dist
     G = dist.get_world_size(group)
-    s = torch.from_numpy(np.ascontiguousarray(src, dtype=np.int64)).to(device)
-    d = torch.from_numpy(np.ascontiguousarray(dst, dtype=np.int64)).to(device)
+    # u32 ids travel as int32 and widen on the device
+    s = torch.from_numpy(np.ascontiguousarray(src, dtype=np.uint32).view(np.int32)).to(device).long() & 0xFFFFFFFF
+    d = torch.from_numpy(np.ascontiguousarray(dst, dtype=np.uint32).view(np.int32)).to(device).long() & 0xFFFFFFFF
     owner = s % G
     order = torch.argsort(owner, stable=True)
     s, d, owner = s[order], d[order], owner[order]

@@ -94,27 +94,27 @@ inline Csr build_csr(uint64_t n, const std::vector<std::pair<uint32_t, uint32_t>
 }
 
 // The streams of generator ranks `vranks` (of P_gen), symmetrized, in rank
-// order: 2 * 2^S * 16 / P_gen directed pairs per rank (generate_rmat.cpp:202-213).
-inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs_of(uint64_t scale, uint64_t p_gen,
-                                                                const std::vector<uint64_t>& vranks,
-                                                                unsigned threads = hw_threads()) {
+// order: 2 * 2^S * 16 / P_gen directed pairs per rank (generate_rmat.cpp:202-213),
+// written through emit(index, u, v).
+template <typename Emit>
+inline uint64_t rmat_stream_of(uint64_t scale, uint64_t p_gen, const std::vector<uint64_t>& vranks, Emit&& emit,
+                               unsigned threads = hw_threads()) {
   if (scale > 32) throw std::runtime_error("scale > 32 not supported (u32 vertex ids)");
   if (p_gen == 0) throw std::runtime_error("P_gen must be positive");
   for (uint64_t r : vranks)
     if (r >= p_gen) throw std::runtime_error("generator rank out of range");
   const uint64_t per_rank = rmat_edges_per_rank(scale, p_gen);
-  std::vector<std::pair<uint32_t, uint32_t>> pairs(2 * per_rank * vranks.size());
   std::atomic<uint64_t> next(0);
   auto worker = [&] {
     for (;;) {
       const uint64_t i = next.fetch_add(1);
       if (i >= vranks.size()) break;
       RmatStream s(rmat_seed(vranks[i]), scale);
-      uint64_t base = 2 * per_rank * i;
+      const uint64_t base = 2 * per_rank * i;
       for (uint64_t e = 0; e < per_rank; ++e) {
         auto uv = s.next_edge();
-        pairs[base + 2 * e] = {static_cast<uint32_t>(uv.first), static_cast<uint32_t>(uv.second)};
-        pairs[base + 2 * e + 1] = {static_cast<uint32_t>(uv.second), static_cast<uint32_t>(uv.first)};
+        emit(base + 2 * e, static_cast<uint32_t>(uv.first), static_cast<uint32_t>(uv.second));
+        emit(base + 2 * e + 1, static_cast<uint32_t>(uv.second), static_cast<uint32_t>(uv.first));
       }
     }
   };
@@ -122,6 +122,15 @@ inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs_of(uint64_t scale, 
   const unsigned nt = std::max<unsigned>(1, std::min<unsigned>(threads, static_cast<unsigned>(vranks.size())));
   for (unsigned t = 0; t < nt; ++t) pool.emplace_back(worker);
   for (auto& th : pool) th.join();
+  return 2 * per_rank * vranks.size();
+}
+
+inline std::vector<std::pair<uint32_t, uint32_t>> rmat_pairs_of(uint64_t scale, uint64_t p_gen,
+                                                                const std::vector<uint64_t>& vranks,
+                                                                unsigned threads = hw_threads()) {
+  std::vector<std::pair<uint32_t, uint32_t>> pairs(2 * rmat_edges_per_rank(scale, std::max<uint64_t>(p_gen, 1)) *
+                                                   vranks.size());
+  rmat_stream_of(scale, p_gen, vranks, [&](uint64_t i, uint32_t u, uint32_t v) { pairs[i] = {u, v}; }, threads);
   return pairs;
 }
 

@@ -969,14 +969,27 @@ int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t strid
     if (stride == 0) throw std::runtime_error("pm_rmat_edges: stride 0");
     std::vector<uint64_t> vr;
     for (uint64_t r = first; r < p_gen; r += stride) vr.push_back(r);
-    auto pairs = pm::rmat_pairs_of(scale, p_gen, vr);
-    *m = pairs.size();
-    *src = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, pairs.size()) * sizeof(uint32_t)));
-    *dst = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, pairs.size()) * sizeof(uint32_t)));
-    for (size_t i = 0; i < pairs.size(); ++i) {
-      (*src)[i] = pairs[i].first;
-      (*dst)[i] = pairs[i].second;
+    if (p_gen == 0) throw std::runtime_error("P_gen must be positive");
+    const uint64_t total = 2 * pm::rmat_edges_per_rank(scale, p_gen) * vr.size();
+    uint32_t* s = static_cast<uint32_t*>(std::malloc(std::max<uint64_t>(1, total) * sizeof(uint32_t)));
+    uint32_t* d = static_cast<uint32_t*>(std::malloc(std::max<uint64_t>(1, total) * sizeof(uint32_t)));
+    if (!s || !d) {
+      std::free(s);
+      std::free(d);
+      throw std::runtime_error("pm_rmat_edges: out of host memory");
     }
+    try {
+      *m = pm::rmat_stream_of(scale, p_gen, vr, [&](uint64_t i, uint32_t u, uint32_t v) {
+        s[i] = u;
+        d[i] = v;
+      });
+    } catch (...) {
+      std::free(s);
+      std::free(d);
+      throw;
+    }
+    *src = s;
+    *dst = d;
     return 0;
   } catch (const std::exception& e) {
     pm::g_last_error = e.what();
