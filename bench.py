@@ -210,6 +210,8 @@ if __name__ == "__main__":
     main()
     sys.stdout.flush()
     sys.stderr.flush()
-    # skip interpreter teardown: the HIP runtime's exit handlers crash under
-    # rocprofv3's finalised tool (SIGSEGV after the profile is written)
-    os._exit(0)
+    if "rocprof" not in os.environ.get("LD_PRELOAD", ""):
+        # skip the interpreter teardown outside the profiler (nothing left to release);
+        # under rocprofv3 the normal exit writes the profile (it then segfaults in the
+        # HIP module teardown after "tool finalization": run it as a call's last GPU step)
+        os._exit(0)

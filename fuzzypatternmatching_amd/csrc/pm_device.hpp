@@ -87,10 +87,12 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
   return x;
 }
 
-// Per-block counter partials (no same-address global atomics: a wave-level
-// atomic per chunk on one word serialises at one L2 channel).  Layout of one
-// block's W = 2P + 4 words: [vertices per rank | edges per rank | traversed |
-// matching rows | removed flag | asymmetry flag]; k_reduce_partials sums them.
+// Per-block counters: each block sums its waves in LDS, then adds its
+// nonzero totals to the counter slot with one atomic per word (a few thousand
+// same-address atomics per launch at most; per-wave atomics would serialise
+// at one L2 channel).  Layout of the W = 2P + 4 words: [vertices per rank |
+// edges per rank | traversed | matching rows | removed flag | asymmetry flag];
+// the slot is zeroed before the launch.
 static constexpr int kMaxRanks = 64;
 struct BlockAcc {
   uint64_t trav = 0, match = 0, vs = 0, es = 0;
@@ -104,13 +106,8 @@ __device__ __forceinline__ void acc_owner(unsigned long long* s_hist, const Owne
   atomicAdd(&s_hist[oa.nranks + r], static_cast<unsigned long long>(edges));
 }
 
-// Destination of a kernel's counters: per-block partials, summed into the
-// counter slot by k_reduce_partials (a separate launch: a last-block
-// reduction needs a device-scope release fence per block, which on the
-// multi-XCD MI355X writes back the XCD's dirty L2 lines -- measured 1.7x
-// slower superstep 0).
 struct Partials {
-  unsigned long long* part;
+  unsigned long long* part;  // unused (kept for the launch signatures)
   unsigned long long* slot;
 };
 
@@ -124,23 +121,25 @@ __device__ __forceinline__ void flush_block(BlockAcc a, const OwnerArgs& oa, uns
     for (int i = 0; i < 6; ++i) s_red[w * 6 + i] = v[i];
   __syncthreads();
   const uint32_t P = oa.nranks <= 1 ? 1 : oa.nranks;
-  const uint32_t W = 2 * P + 4;
-  unsigned long long* out = pp.part + uint64_t(blockIdx.x) * W;
+  unsigned long long* out = pp.slot;
   if (threadIdx.x < 6) {
     unsigned long long t = 0;
     for (int i = 0; i < kWpb; ++i) t += s_red[i * 6 + threadIdx.x];
     const int j = threadIdx.x;
-    if (j == 0) out[2 * P] = t;
-    if (j == 1) out[2 * P + 1] = t;
-    if (j == 4) out[2 * P + 2] = t;
-    if (j == 5) out[2 * P + 3] = t;
+    int dst = -1;
+    if (j == 0) dst = 2 * P;
+    if (j == 1) dst = 2 * P + 1;
+    if (j == 4) dst = 2 * P + 2;
+    if (j == 5) dst = 2 * P + 3;
     if (oa.nranks <= 1) {
-      if (j == 2) out[0] = t;
-      if (j == 3) out[1] = t;
+      if (j == 2) dst = 0;
+      if (j == 3) dst = 1;
     }
+    if (dst >= 0 && t) atomicAdd(out + dst, t);
   }
   if (oa.nranks > 1)
-    for (uint32_t i = threadIdx.x; i < 2 * P; i += blockDim.x) out[i] = s_hist[i];
+    for (uint32_t i = threadIdx.x; i < 2 * P; i += blockDim.x)
+      if (s_hist[i]) atomicAdd(out + i, s_hist[i]);
 }
 
 // Wave-aggregated reservation of n slots on a global counter; returns the

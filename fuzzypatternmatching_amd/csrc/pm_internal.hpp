@@ -213,6 +213,12 @@ struct Ctx {
   size_t xred_cap = 0;
   bool m_dirty = true;            // M changed since the last replication
 
+  // host side of the driver loop
+  uint64_t* h_pin = nullptr;      // pinned staging for counter / line-stat read-backs
+  size_t h_pin_words = 0;
+  bool fine_timing = false;       // per-superstep events (result files / PM_PHASE_TIMES)
+  bool tpub_clean = false;        // T_pub is zero outside the last search's slist entries
+
   // vertex state (device, by position)
   uint16_t* d_tpub[2] = {nullptr, nullptr};  // template_vertices (T_pub), 0 = not in S
   int cur = 0;
@@ -290,6 +296,9 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
 unsigned lcc_first_grid(const Ctx& c);
 void launch_lcc_step(Ctx& c, uint64_t* d_slot);
 void launch_count_state(Ctx& c, uint64_t* d_slot);
+// Zero T_pub (both buffers) at the slist entries of the last search (every
+// nonzero T_pub entry is one of them, plus the other shards' when sharded).
+void launch_clear_tpub(Ctx& c);
 size_t slist_scan_tmp_bytes(uint64_t words);
 static constexpr unsigned kPartGridMax = 2048;
 
@@ -324,6 +333,8 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);
 
 LineArgs make_line_args(const Ctx& c, const NlcLine& line);
+
+uint64_t* pinned(Ctx& c, size_t words);  // pinned host staging (pm_api.hip)
 
 // Shard exchanges (pm_shard.hip); no-ops when nshards == 1.
 void shard_after_first(Ctx& c);      // after superstep 0: slists of all shards + T_pub

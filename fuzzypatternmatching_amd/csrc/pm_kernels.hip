@@ -33,27 +33,6 @@
 namespace pm {
 
 
-// One block: thread t sums blocks t, t+256, ... of every word (independent
-// loads in flight), then a wave + LDS reduction per word.
-__global__ __launch_bounds__(kBlock) void k_reduce_partials(const unsigned long long* __restrict__ part,
-                                                            uint32_t nblocks, uint32_t W,
-                                                            unsigned long long* __restrict__ slot) {
-  __shared__ unsigned long long s_w[kWpb];
-  for (uint32_t j = 0; j < W; ++j) {
-    unsigned long long t = 0;
-    for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) t += part[uint64_t(b) * W + j];
-    t = wave_sum(t);
-    if (lane_id() == 0) s_w[threadIdx.x / kWave] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long s = 0;
-      for (int i = 0; i < kWpb; ++i) s += s_w[i];
-      slot[j] = s;
-    }
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------
 // K0: labels.
 // vertex_data_db_degree.hpp:109  label = ceil(log2(degree + 1)) == bit_width(degree)
@@ -420,6 +399,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     unsigned long long* tm = tmask + uint64_t(t) * kSub;
     const RelRuns rel_runs = load_rel(s_tab[r]);
     const KeepArgs keep = load_keep(s_tab[r]);
+    const uint32_t hseg_at = __builtin_amdgcn_readfirstlane(s_tab[r].aux);
 #define PM_TB(x) ((x) != kNone ? tbits_rel<WIDE>((x), rel_runs, s_runs, nruns) : uint16_t(0))
     if (kind <= 6) {
       if (MODE & 2) continue;
@@ -500,7 +480,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     } else {
       if (MODE & 4) continue;
       // ---- heavy rows: one kHeavyDeg segment per tile, uncompacted M
-      const HSeg hs = hseg[s_tab[r].aux + rel];
+      const HSeg hs = hseg[hseg_at + rel];
       const uint64_t b0 = offp[hs.row];
       const uint32_t deg = static_cast<uint32_t>(offp[hs.row + 1] - b0);
       const uint32_t j_beg = hs.seg * kHeavyDeg;
@@ -635,6 +615,9 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
+  __shared__ uint64_t s_beg[kWpb][kWave];  // flattened short rows (per wave)
+  __shared__ uint32_t s_end[kWpb][kWave], s_tn[kWpb][kWave], s_cnt[kWpb][kWave];
+  __shared__ uint16_t s_nm[kWpb][kWave];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   load_adj(s_adj, pa);
   __syncthreads();
@@ -668,20 +651,58 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     }
     uint32_t tn = 0, cnt = 0;
     bool asym = false;
-    // short rows: one lane per row
+    // short rows: flattened over the wave -- the chunk's rows are concatenated
+    // and every lane takes every 64th entry (four in flight), so a chunk costs
+    // ceil(entries / 256) rounds of two dependent loads instead of one round per
+    // four entries of its longest row; per-row OR / count through LDS atomics
     const bool lng = len > kLprMax;
     const uint32_t ls = lng ? 0u : len;
-    const uint32_t lmax = wave_max32(ls);
-    for (uint32_t j = 0; j < lmax; j += 4) {
-      uint32_t m[4];
-      uint16_t tv[4];
+    const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(ls));
+    const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+    if (total) {
+      s_end[w][lane] = incl;
+      s_beg[w][lane] = beg;
+      s_nm[w][lane] = nm;
+      s_tn[w][lane] = 0;
+      s_cnt[w][lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t t0 = 0; t0 < total; t0 += 4 * kWave) {
+        uint32_t m[4];
+        uint16_t tv[4];
+        int rr[4];
+        uint64_t e[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] = j + q < ls ? mcol[beg + j + q] : 0u;
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t t = t0 + q * kWave + lane;
+          m[q] = 0u;
+          rr[q] = 0;
+          e[q] = 0;
+          if (t < total) {
+            int lo = 0, hi = kWave - 1;  // row of entry t
+            while (lo < hi) {
+              const int mid = (lo + hi) >> 1;
+              if (s_end[w][mid] > t) hi = mid; else lo = mid + 1;
+            }
+            rr[q] = lo;
+            e[q] = s_beg[w][lo] + (t - (lo ? s_end[w][lo - 1] : 0u));
+            m[q] = mcol[e[q]];
+          }
+        }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
+        for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (m[q] & kAlive) k2_entry(mcol, beg + j + q, m[q], tv[q], nm, tn, cnt, asym);
+        for (int q = 0; q < 4; ++q)
+          if (m[q] & kAlive) {
+            uint32_t tq = 0, cq = 0;
+            k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym);
+            if (tq) atomicOr(&s_tn[w][rr[q]], tq);
+            if (cq) atomicAdd(&s_cnt[w][rr[q]], cq);
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+      tn = s_tn[w][lane];
+      cnt = s_cnt[w][lane];
+      __builtin_amdgcn_wave_barrier();
     }
     // long rows: the whole wave walks each
     uint64_t lb = __ballot(lng);
@@ -805,12 +826,8 @@ static Partials partials(Ctx& c, uint64_t* d_slot) {
   return Partials{reinterpret_cast<unsigned long long*>(c.d_part), reinterpret_cast<unsigned long long*>(d_slot)};
 }
 
-static void reduce_into(Ctx& c, unsigned grid, uint64_t* d_slot) {
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kBlock), 0, c.stream,
-                     reinterpret_cast<const unsigned long long*>(c.d_part), grid, slot_words(c),
-                     reinterpret_cast<unsigned long long*>(d_slot));
-  PM_HIP_CHECK(hipGetLastError());
-}
+// Counters are added into the (zeroed) slot by the kernels themselves.
+static void reduce_into(Ctx&, unsigned, uint64_t*) {}
 
 // Sorts the vertices by (label, degree, id) (two stable LSD radix passes:
 // degree, then label) and writes the renumbered adjacency into dst.  Sharded
@@ -1160,7 +1177,10 @@ size_t slist_scan_tmp_bytes(uint64_t words) {
 
 void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
-  const unsigned grid = grid_for(chunks, kWpb, kMaxGrid);
+  // first later superstep (every slist entry live): one chunk per wave, the
+  // latency-bound rows need waves in flight; afterwards few chunks are live
+  // and a persistent-style grid skips the dead ones cheaply
+  const unsigned grid = grid_for(chunks, kWpb, c.smask_valid ? kMaxGrid : 16384);
   const unsigned long long* min = c.smask_valid ? reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur])
                                                 : nullptr;
   auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
@@ -1172,6 +1192,29 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   c.cur ^= 1;
   c.smask_cur ^= 1;
   c.smask_valid = true;
+}
+
+__global__ void k_clear_tpub(const uint32_t* __restrict__ list, const uint32_t* __restrict__ np, uint64_t cap,
+                             uint16_t* __restrict__ t0, uint16_t* __restrict__ t1) {
+  const uint64_t n = min(static_cast<uint64_t>(*np), cap);
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t p = list[i];
+    t0[p] = 0;
+    t1[p] = 0;
+  }
+}
+
+void launch_clear_tpub(Ctx& c) {
+  if (c.nS_host)
+    hipLaunchKernelGGL(k_clear_tpub, dim3(grid_for(c.nS_host, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_slist,
+                       c.d_nS, uint64_t(c.nS_host), c.d_tpub[0], c.d_tpub[1]);
+  if (c.comm && c.d_xslist)  // the other shards' entries (replicated T_pub)
+    for (uint32_t g = 0; g < c.nshards; ++g)
+      if (g != c.shard && c.xnS[g])
+        hipLaunchKernelGGL(k_clear_tpub, dim3(grid_for(c.xnS[g], kBlock, 4096)), dim3(kBlock), 0, c.stream,
+                           c.d_xslist + uint64_t(g) * c.xmaxS, c.d_xnS + g, uint64_t(c.xnS[g]), c.d_tpub[0],
+                           c.d_tpub[1]);
+  PM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_count_state(Ctx& c, uint64_t* d_slot) {

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 #include "pm_device.hpp"
@@ -164,32 +165,66 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
   }
 }
 
+// Per-wave staging of the rows a wave expands (flattened expansion: the
+// wave's 64 rows are concatenated and every lane takes every 64th entry, so a
+// long row costs one pass over the wave instead of a serial walk by one lane).
+static constexpr int kLineWaves = 16;  // kLineBlock / kWave
+struct WaveRows {
+  uint64_t beg[kLineWaves][kWave];
+  uint32_t end[kLineWaves][kWave];  // inclusive scan of the row lengths
+  uint32_t s[kLineWaves][kWave], u[kLineWaves][kWave], x[kLineWaves][kWave];
+};
+
+// Lane owning concatenated entry t (end[] inclusive scan of the wave's rows).
+__device__ __forceinline__ int row_of(const uint32_t* end, uint32_t t) {
+  int lo = 0, hi = kWave - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (end[mid] > t) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
 // Forwarding from u (token of source s at position k, excluded parent excl):
 // every alive w in M[u] other than excl goes to position k + 1 (terminal
 // action at C + 1, else arrival filter + hash insert).  All lanes of the wave
-// must call it; returns the lane's emitted token count.
-__device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t excl,
-                                               int k, bool active) {
+// must call it; returns the lane's share of the emitted token count.
+__device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows& wr, uint32_t u, uint32_t s,
+                                               uint32_t excl, int k, bool active) {
   uint32_t emitted = 0;
   const LineArgs& la = *a.la;
-  uint64_t b = 0, L = 0;
+  const int wv = threadIdx.x / kWave, lane = lane_id();
+  uint64_t b = 0;
+  uint32_t L = 0;
   if (active) {
     b = a.offp[u];
     L = a.mlen[u];
   }
-  uint64_t Lmax = L;
-  for (int d = kWave / 2; d > 0; d >>= 1) Lmax = max(Lmax, static_cast<uint64_t>(__shfl_xor(Lmax, d, kWave)));
-  for (uint64_t j = 0; j < Lmax; ++j) {
+  const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
+  const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+  if (!total) return 0;
+  wr.beg[wv][lane] = b;
+  wr.end[wv][lane] = incl;
+  wr.s[wv][lane] = s;
+  wr.u[wv][lane] = u;
+  wr.x[wv][lane] = excl;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
+    const uint32_t t = t0 + lane;
     uint64_t slot = kEmpty;
-    const uint32_t m = j < L ? a.mcol[b + j] : 0u;
-    if (m & kAlive) {
-      const uint32_t w = m & kPosMask;
-      if (w != excl) {
-        ++emitted;
-        if (k + 1 == la.C + 1) {
-          tp_terminal(a, w, s, u);
-        } else if (w != s && pos_ok(a.tpub[w], k + 1, la)) {
-          slot = ht_insert(a, s, w, static_cast<uint32_t>(k + 1), u);
+    if (t < total) {
+      const int r = row_of(wr.end[wv], t);
+      const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
+      const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
+      if (m & kAlive) {
+        const uint32_t w = m & kPosMask, sr = wr.s[wv][r], ur = wr.u[wv][r];
+        if (w != wr.x[wv][r]) {
+          ++emitted;
+          if (k + 1 == la.C + 1) {
+            tp_terminal(a, w, sr, ur);
+          } else if (w != sr && pos_ok(a.tpub[w], k + 1, la)) {
+            slot = ht_insert(a, sr, w, static_cast<uint32_t>(k + 1), ur);
+          }
         }
       }
     }
@@ -202,6 +237,7 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, uint32_t
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();
   return emitted;
 }
 
@@ -236,6 +272,7 @@ __device__ __forceinline__ void tree_barrier(unsigned* bar) {
 static constexpr unsigned kGbarWords = 64 + 32 * 64;  // up to 1024 blocks
 
 static constexpr int kLineBlock = 1024;
+static_assert(kLineBlock / kWave == kLineWaves, "WaveRows is sized for kLineBlock");
 struct GridIdx {
   uint64_t tid, nth, gw, nw;
 };
@@ -313,33 +350,57 @@ __device__ __forceinline__ void line_post(const LineKernelArgs& a, const GridIdx
 // ---- TDS lines (tds_batch_1) -------------------------------------------
 // Walks of position L (L+1 vertices) are stored from st->wbase[L] on, stride
 // C+2 u32, each position in fresh memory (no cache line is reused across
-// phases).  Sender-side checks follow k_tds_expand.
-__device__ __forceinline__ uint32_t tds_children(const LineKernelArgs& a, const uint32_t* w, int k, uint64_t b,
-                                                 uint64_t L, uint32_t* out, int stride) {
-  const LineArgs& la = *a.la;
-  const uint32_t s = w[0];
-  uint32_t c = 0;
-  for (uint64_t e = b; e < b + L; ++e) {
-    if (!(a.mcol[e] & kAlive)) continue;
-    const uint32_t nb = a.mcol[e] & kPosMask;
-    if (k == la.C) {
-      if (la.VC) {
-        if (nb != s) continue;
-      } else {
-        if (nb == s) continue;
-        if (!enum_ok(w, k + 1, nb, la)) continue;
-      }
-    } else {
-      if (!enum_ok(w, k + 1, nb, la)) continue;
-    }
-    if (out) {
-      uint32_t* d = out + uint64_t(c) * stride;
-      for (int p = 0; p <= k; ++p) d[p] = w[p];
-      d[k + 1] = nb;
-    }
-    ++c;
+// phases).  Sender-side checks of a child nb of walk w at position k + 1
+// (tds_batch_1.hpp:793-909), as in k_tds_expand.
+__device__ __forceinline__ bool tds_child_ok(const uint32_t* w, int k, uint32_t nb, const LineArgs& la) {
+  if (k == la.C) {
+    if (la.VC) return nb == w[0];
+    if (nb == w[0]) return false;
   }
-  return c;
+  return enum_ok(w, k + 1, nb, la);
+}
+
+// Flattened expansion of the wave's walks win[i0 .. i0 + 64) at position k
+// (rows b/L per lane, L = 0 for walks that fail the arrival checks): children
+// are appended to region out (counter wn[k + 1]).  All lanes must call it.
+__device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRows& wr, const uint32_t* win,
+                                                uint64_t i0, int k, uint64_t b, uint32_t L, uint32_t* out,
+                                                uint64_t out_room, int stride) {
+  const LineArgs& la = *a.la;
+  const int wv = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
+  const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+  if (!total) return;
+  wr.beg[wv][lane] = b;
+  wr.end[wv][lane] = incl;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
+    const uint32_t t = t0 + lane;
+    bool child = false;
+    uint32_t nb = 0;
+    const uint32_t* w = win;
+    if (t < total) {
+      const int r = row_of(wr.end[wv], t);
+      const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
+      const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
+      w = win + (i0 + r) * stride;
+      if (m & kAlive) {
+        nb = m & kPosMask;
+        child = tds_child_ok(w, k, nb, la);
+      }
+    }
+    const uint64_t pos = wave_reserve(&a.st->wn[k + 1], child ? 1u : 0u);
+    if (child) {
+      if ((pos + 1) * stride <= out_room) {
+        uint32_t* d = out + pos * stride;
+        for (int p = 0; p <= k; ++p) d[p] = w[p];
+        d[k + 1] = nb;
+      } else {
+        atomicOr(&a.st->overflow, 1u);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 // Block-local index (single-block mode: block 0 finishes a small line alone).
@@ -364,7 +425,7 @@ static constexpr uint64_t kSmallLine = 16384;
 // ---- path / cycle lines (nem_1) ----------------------------------------
 // Positions 2..C+1 and post-processing; every participating wave calls it.
 __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
-                                          unsigned long long* s_hist) {
+                                          unsigned long long* s_hist, WaveRows& wr) {
   LineStats* st = a.st;
   uint64_t trav = 0, tokens = 0, lo = 0;
   for (int k = 1; k <= a.la->C; ++k) {
@@ -383,7 +444,7 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
         excl = par == kMulti ? kNone : par;
         trav += a.malive[u];
       }
-      tokens += tp_forward(a, u, s, excl, k, act);
+      tokens += tp_forward(a, wr, u, s, excl, k, act);
     }
     lo = hi;
     phase_sync(a, single);
@@ -401,7 +462,7 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
   }
 }
 
-__device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long long* s_hist) {
+__device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long long* s_hist, WaveRows& wr) {
   const GridIdx g = grid_idx();
   LineStats* st = a.st;
   uint64_t trav = 0, tokens = 0;
@@ -413,7 +474,7 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
     uint32_t s;
     const bool ok = select_source(a, i0 + lane_id(), nS, false, live, s);
     if (ok) trav += a.malive[s];
-    tokens += tp_forward(a, s, s, kNone, 0, ok);
+    tokens += tp_forward(a, wr, s, s, kNone, 0, ok);
   }
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
@@ -423,8 +484,8 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
   if (nsrc == 0) return;  // no tokens, nothing to post-process (every block agrees)
   const bool single = nsrc <= kSmallLine && ld_acq(&st->ftotal) <= kSmallLine;
   if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
-  if (!single) path_rest(a, g, false, s_hist);
-  else if (blockIdx.x == 0) path_rest(a, block_idx(), true, s_hist);
+  if (!single) path_rest(a, g, false, s_hist, wr);
+  else if (blockIdx.x == 0) path_rest(a, block_idx(), true, s_hist, wr);
 }
 
 // ---- TDS lines (tds_batch_1) -------------------------------------------
@@ -432,7 +493,7 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
 // stored from wbase[L] on (fresh, 128-B aligned memory per position); kept
 // walks are appended to the launch's kept buffer.
 __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
-                                         unsigned long long* s_hist) {
+                                         unsigned long long* s_hist, WaveRows& wr) {
   LineStats* st = a.st;
   const LineArgs& la = *a.la;
   const int stride = la.C + 2;
@@ -445,26 +506,18 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
     const uint32_t* win = a.wbuf + in_base;
     for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
       const uint64_t i = i0 + lane_id();
-      const bool act = i < nin;
-      const uint32_t* w = win + (act ? i : 0) * stride;
-      uint32_t cnt = 0;
-      uint64_t b = 0, L = 0;
-      if (act) {
+      uint64_t b = 0;
+      uint32_t L = 0;
+      if (i < nin) {
+        const uint32_t* w = win + i * stride;
         const uint32_t u = w[k];
         if (pos_ok(a.tpub[u], k, la) && enum_ok(w, k, u, la)) {
           b = a.offp[u];
           L = a.mlen[u];
           trav += a.malive[u];
-          cnt = tds_children(a, w, k, b, L, nullptr, stride);
         }
       }
-      const uint64_t pos = wave_reserve(&st->wn[k + 1], cnt);
-      if (cnt) {
-        if (out_base + (pos + cnt) * stride <= a.wcap)
-          tds_children(a, w, k, b, L, a.wbuf + out_base + pos * stride, stride);
-        else
-          atomicOr(&st->overflow, 1u);
-      }
+      tds_expand_wave(a, wr, win, i0, k, b, L, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride);
     }
     in_base = out_base;
     phase_sync(a, single);
@@ -516,7 +569,7 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   line_post(a, g, s_hist);
 }
 
-__device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long long* s_hist) {
+__device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long long* s_hist, WaveRows& wr) {
   const GridIdx g = grid_idx();
   LineStats* st = a.st;
   const int stride = a.la->C + 2;
@@ -528,28 +581,43 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
     if (!live) continue;  // wave-uniform
     uint32_t s;
     const bool ok = select_source(a, i0 + lane_id(), nS, true, live, s);
-    uint32_t cnt = 0;
-    uint64_t b = 0, L = 0;
+    uint64_t b = 0;
+    uint32_t L = 0;
     if (ok) {
       b = a.offp[s];
       L = a.mlen[s];
-      cnt = a.malive[s];
-      trav += cnt;
+      trav += a.malive[s];
     }
-    const uint64_t pos = wave_reserve(&st->wn[1], cnt);
-    if (cnt) {
-      if ((pos + cnt) * stride <= a.wcap) {
-        uint64_t o = pos;
-        for (uint64_t e = b; e < b + L; ++e) {
-          if (!(a.mcol[e] & kAlive)) continue;
-          a.wbuf[o * stride + 0] = s;
-          a.wbuf[o * stride + 1] = a.mcol[e] & kPosMask;
-          ++o;
+    // walks [s, w] for every alive w in M[s] (flattened over the wave's sources)
+    const int wv = threadIdx.x / kWave, lane = lane_id();
+    const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
+    const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+    if (!total) continue;
+    wr.beg[wv][lane] = b;
+    wr.end[wv][lane] = incl;
+    wr.s[wv][lane] = s;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
+      const uint32_t t = t0 + lane;
+      uint32_t m = 0, sr = 0;
+      if (t < total) {
+        const int r = row_of(wr.end[wv], t);
+        const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
+        m = a.mcol[wr.beg[wv][r] + (t - first)];
+        sr = wr.s[wv][r];
+      }
+      const bool alive = (m & kAlive) != 0;
+      const uint64_t pos = wave_reserve(&st->wn[1], alive ? 1u : 0u);
+      if (alive) {
+        if ((pos + 1) * stride <= a.wcap) {
+          a.wbuf[pos * stride + 0] = sr;
+          a.wbuf[pos * stride + 1] = m & kPosMask;
+        } else {
+          atomicOr(&st->overflow, 1u);
         }
-      } else {
-        atomicOr(&st->overflow, 1u);
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
   wave_add(&st->trav, trav);
   tree_barrier(a.gbar);
@@ -558,8 +626,8 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   if (nsrc == 0) return;  // no walks, nothing to post-process (every block agrees)
   const bool single = nsrc <= kSmallLine && ld_acq(&st->wn[1]) <= kSmallLine;
   if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
-  if (!single) tds_rest(a, g, false, s_hist);
-  else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist);
+  if (!single) tds_rest(a, g, false, s_hist, wr);
+  else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist, wr);
 }
 
 // NLC lines [pl_begin, pl_end) in order, one grid barrier at each line end
@@ -568,6 +636,7 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
 // interleaved LCC, beta.cpp:1163-1197, then relaunches).
 __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ WaveRows wr;
   for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
     const LineDesc& d = a.lines[pl];
     LineKernelArgs b = a;
@@ -575,8 +644,8 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     b.i0 = d.i0;
     b.st = a.st + pl;
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[0] = __builtin_amdgcn_s_memrealtime();
-    if (d.tds) tds_line(b, s_hist);
-    else path_line(b, s_hist);
+    if (d.tds) tds_line(b, s_hist, wr);
+    else path_line(b, s_hist, wr);
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[2] = __builtin_amdgcn_s_memrealtime();
     tree_barrier(a.gbar);
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[3] = __builtin_amdgcn_s_memrealtime();
@@ -711,14 +780,18 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   void* args[] = {&a};
   PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(c.line_grid),
                                           dim3(kLineBlock), args, 0, c.stream));
-  std::vector<LineStats> hs(nl - pl0);
-  unsigned done = 0;
-  unsigned long long kept_slots = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(hs.data(), c.d_lstats + pl0, hs.size() * sizeof(LineStats), hipMemcpyDeviceToHost,
+  // read-back through pinned memory: [done | kept slots | line stats]
+  const size_t sw = (sizeof(LineStats) + 7) / 8;
+  uint64_t* pin = pinned(c, 2 + (nl - pl0) * sw);
+  PM_HIP_CHECK(hipMemcpyAsync(pin, d_done, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(pin + 1, d_kept_ctr, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(pin + 2, c.d_lstats + pl0, (nl - pl0) * sizeof(LineStats), hipMemcpyDeviceToHost,
                               c.stream));
-  PM_HIP_CHECK(hipMemcpyAsync(&done, d_done, sizeof(done), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipMemcpyAsync(&kept_slots, d_kept_ctr, sizeof(kept_slots), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  std::vector<LineStats> hs(nl - pl0);
+  std::memcpy(hs.data(), pin + 2, hs.size() * sizeof(LineStats));
+  const unsigned done = static_cast<unsigned>(pin[0] & 0xFFFFFFFFull);
+  const unsigned long long kept_slots = pin[1];
   std::vector<uint32_t> kept;
   if (want_walks && kept_slots) {
     kept.resize(kept_slots);
