@@ -5,7 +5,10 @@
 // same result directory layout.
 
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <bitset>
@@ -301,6 +304,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
+  c.probe("lcc issued");
   // read-back through pinned memory: [nS | local counts | summed counts]
   uint64_t* pin = pinned(c, 1 + 2 * D * W);
   PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
@@ -310,6 +314,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   }
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.probe("lcc synced");
   std::vector<uint64_t> host(pin + 1 + D * W, pin + 1 + 2 * D * W);
   std::vector<uint64_t> local = c.comm ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
   const uint32_t nS = static_cast<uint32_t>(pin[0] & 0xFFFFFFFFull);
@@ -359,6 +364,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[D + 1], ev[D + 2]));
     c.lcc_first_ms = ms;
   }
+  c.probe("lcc parsed");
   if (asym)
     throw std::runtime_error(
         "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message); "
@@ -512,6 +518,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   c.device_seconds = 0.0;
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   const auto t_pattern = std::chrono::steady_clock::now();
+  c.probe("start");
   auto since = [](std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
   };
@@ -519,6 +526,8 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   // PM_PHASE_TIMES=1: per-phase host wall time on stderr (diagnostics)
   const bool phase_times = std::getenv("PM_PHASE_TIMES") != nullptr;
   c.fine_timing = files || phase_times;
+  c.probing = phase_times;
+  c.probes.clear();
   double ph_lcc = 0, ph_tp = 0, ph_post = 0, ph_count = 0;
   auto tick = [] { return std::chrono::steady_clock::now(); };
   uint64_t itr = 0;
@@ -704,10 +713,22 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     ++itr;
   } while (nf);
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.probe("end");
   const double secs = since(t_pattern);
   if (phase_times)
     std::fprintf(stderr, "[pm] run_beta %.3f ms: lcc %.3f, token passing %.3f, post %.3f, counts %.3f, device %.3f\n",
                  secs * 1e3, ph_lcc * 1e3, ph_tp * 1e3, ph_post * 1e3, ph_count * 1e3, c.device_seconds * 1e3);
+  if (phase_times && !c.probes.empty()) {
+    std::string line = "[pm] host:";
+    double prev = c.probes[0].second;
+    for (const auto& pr : c.probes) {
+      char buf[96];
+      std::snprintf(buf, sizeof(buf), " %s +%.1f", pr.first, (pr.second - prev) * 1e6);
+      line += buf;
+      prev = pr.second;
+    }
+    std::fprintf(stderr, "%s us\n", line.c_str());
+  }
   s.iterations = itr;
   s.terminated = terminated ? 1 : 0;
   s.seconds = secs;
@@ -919,6 +940,17 @@ pm_ctx* pm_create_shard(const pm_shard_desc* d, const char* pattern_dir, int dev
   }
 }
 
+// PM_SEGV_TRACE=1: backtrace of a host crash inside the shard threads (diagnostics)
+static void pm_segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "[pm] fatal signal, backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, int device, uint32_t nshards,
                              const uint64_t* labels, const char* result_dir, uint64_t max_iterations,
                              pm_run_stats* out) {
@@ -939,6 +971,7 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
       }
       if (cols[q].empty()) cols[q].push_back(0);
     }
+    if (std::getenv("PM_SEGV_TRACE")) signal(SIGSEGV, pm_segv_trace);
     pm::ThreadGroup grp(static_cast<int>(nshards));
     std::vector<pm_run_stats> st(nshards);
     std::vector<std::string> errs(nshards);

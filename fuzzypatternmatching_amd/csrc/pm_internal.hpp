@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -218,6 +219,13 @@ struct Ctx {
   size_t h_pin_words = 0;
   bool fine_timing = false;       // per-superstep events (result files / PM_PHASE_TIMES)
   bool tpub_clean = false;        // T_pub is zero outside the last search's slist entries
+  // PM_PHASE_TIMES: host timestamps of the driver loop (diagnostics)
+  bool probing = false;
+  std::vector<std::pair<const char*, double>> probes;
+  void probe(const char* what) {
+    if (probing)
+      probes.emplace_back(what, std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
+  }
 
   // vertex state (device, by position)
   uint16_t* d_tpub[2] = {nullptr, nullptr};  // template_vertices (T_pub), 0 = not in S

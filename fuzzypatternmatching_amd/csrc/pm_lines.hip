@@ -95,6 +95,8 @@ struct LineKernelArgs {
   const LineDesc* lines;
   int pl_begin, pl_end;
   unsigned* done;  // lines processed by the launch
+  uint32_t* act;   // S members at launch start (slist entries with T_pub != 0), built by k_lines
+  unsigned long long* nact;
 };
 
 __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
@@ -286,14 +288,16 @@ __device__ __forceinline__ GridIdx grid_idx() {
   return g;
 }
 
-// P1 for one 64-entry chunk of slist: returns the lane's source (ok) after
-// appending it to the source list and marking the token source map.
-__device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t i, uint32_t nS, bool tds,
-                                              uint64_t live, uint32_t& s) {
+// P1 for one entry of the active list: returns the lane's source (ok) after
+// appending it to the source list and marking the token source map.  The
+// list was built at launch start; a member whose T_pub became 0 since (post-
+// processing of an earlier line) fails the T_pub test.
+__device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t i, uint64_t nact, bool tds,
+                                              uint32_t& s) {
   bool ok = false;
   s = 0;
-  if (i < nS && ((live >> lane_id()) & 1ull)) {
-    s = a.slist[i];
+  if (i < nact) {
+    s = ld_acq(&a.act[i]);
     const uint16_t T = a.tpub[s];
     ok = T && pos_ok(T, 0, *a.la);
     if (ok && !tds && !a.la->VC && !((T >> a.la->ilast) & 1u)) ok = false;
@@ -304,6 +308,37 @@ __device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t 
     a.tsm[s] = 1;
   }
   return ok;
+}
+
+// Active list of the launch: the slist entries with T_pub != 0 (every later
+// source is one of them: S only shrinks), found through the live masks of the
+// last superstep, 64 mask words per wave (dead chunks cost one coalesced load).
+__device__ __forceinline__ void build_active(const LineKernelArgs& a) {
+  const GridIdx g = grid_idx();
+  const int lane = lane_id();
+  const uint32_t nS = *a.nS;
+  const uint64_t nch = (uint64_t(nS) + kWave - 1) / kWave;
+  for (uint64_t c0 = g.gw * kWave; c0 < nch; c0 += g.nw * kWave) {
+    const uint64_t ch = c0 + lane;
+    const uint64_t lm = ch < nch ? (a.smask ? a.smask[ch] : ~0ull) : 0ull;
+    uint64_t bal = __ballot(lm != 0);
+    while (bal) {
+      const int j = __ffsll(static_cast<long long>(bal)) - 1;
+      bal &= bal - 1;
+      const uint64_t live =
+          (uint64_t(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(lm >> 32), j))) << 32) |
+          static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(lm), j));
+      const uint64_t i = (c0 + j) * kWave + lane;
+      uint32_t v = 0;
+      bool ok = false;
+      if (i < nS && ((live >> lane) & 1ull)) {
+        v = a.slist[i];
+        ok = a.tpub[v] != 0;
+      }
+      const uint64_t pos = wave_reserve(a.nact, ok ? 1u : 0u);
+      if (ok) a.act[pos] = v;
+    }
+  }
 }
 
 // Pp: post-processing of unacked sources (k_tp_post), reporting the vertices
@@ -467,12 +502,10 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
   LineStats* st = a.st;
   uint64_t trav = 0, tokens = 0;
   // P1 + position 1: (v, s, parent = s) for v in M[s]
-  const uint32_t nS = *a.nS;
-  for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
-    const uint64_t live = a.smask ? a.smask[i0 / kWave] : ~0ull;
-    if (!live) continue;  // wave-uniform
+  const uint64_t nact = ld_acq(a.nact);
+  for (uint64_t i0 = g.gw * kWave; i0 < nact; i0 += g.nw * kWave) {
     uint32_t s;
-    const bool ok = select_source(a, i0 + lane_id(), nS, false, live, s);
+    const bool ok = select_source(a, i0 + lane_id(), nact, false, s);
     if (ok) trav += a.malive[s];
     tokens += tp_forward(a, wr, s, s, kNone, 0, ok);
   }
@@ -493,7 +526,7 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
 // stored from wbase[L] on (fresh, 128-B aligned memory per position); kept
 // walks are appended to the launch's kept buffer.
 __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
-                                         unsigned long long* s_hist, WaveRows& wr) {
+                                         unsigned long long* s_hist, WaveRows& wr, uint64_t kept_base) {
   LineStats* st = a.st;
   const LineArgs& la = *a.la;
   const int stride = la.C + 2;
@@ -524,7 +557,9 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   }
   // every final walk may be kept: its room must exist before any terminal effect
   const uint64_t nw = ld_acq(&st->wn[la.C + 1]);
-  const uint64_t kept0 = ld_acq(a.kept_ctr);
+  // kept slots used by the launch's earlier lines (read at line start: the
+  // terminal loop below adds to the counter while slower blocks still enter it)
+  const uint64_t kept0 = kept_base;
   if (ld_acq(&st->overflow) || kept0 + nw * stride > a.kept_cap) {
     if (g.tid == 0) atomicOr(&st->overflow, 1u);
     wave_add(&st->trav, trav);
@@ -575,12 +610,11 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   const int stride = a.la->C + 2;
   uint64_t trav = 0;
   // P1 + position 1 walks [s, w]; region 1 starts at slot 0
-  const uint32_t nS = *a.nS;
-  for (uint64_t i0 = g.gw * kWave; i0 < nS; i0 += g.nw * kWave) {
-    const uint64_t live = a.smask ? a.smask[i0 / kWave] : ~0ull;
-    if (!live) continue;  // wave-uniform
+  const uint64_t kept_base = ld_acq(a.kept_ctr);  // no kept walk of this line exists yet
+  const uint64_t nact = ld_acq(a.nact);
+  for (uint64_t i0 = g.gw * kWave; i0 < nact; i0 += g.nw * kWave) {
     uint32_t s;
-    const bool ok = select_source(a, i0 + lane_id(), nS, true, live, s);
+    const bool ok = select_source(a, i0 + lane_id(), nact, true, s);
     uint64_t b = 0;
     uint32_t L = 0;
     if (ok) {
@@ -626,8 +660,8 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   if (nsrc == 0) return;  // no walks, nothing to post-process (every block agrees)
   const bool single = nsrc <= kSmallLine && ld_acq(&st->wn[1]) <= kSmallLine;
   if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
-  if (!single) tds_rest(a, g, false, s_hist, wr);
-  else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist, wr);
+  if (!single) tds_rest(a, g, false, s_hist, wr, kept_base);
+  else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist, wr, kept_base);
 }
 
 // NLC lines [pl_begin, pl_end) in order, one grid barrier at each line end
@@ -637,6 +671,8 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
 __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ WaveRows wr;
+  build_active(a);
+  tree_barrier(a.gbar);
   for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
     const LineDesc& d = a.lines[pl];
     LineKernelArgs b = a;
@@ -710,6 +746,7 @@ static void upload_lines(Ctx& c) {
 
 size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
                        size_t max_lines) {
+  c.probe("lines entry");
   const size_t nl_all = c.pattern.lines.size();
   const size_t nl = pl0 < nl_all && max_lines < nl_all - pl0 ? pl0 + max_lines : nl_all;
   overflow = false;
@@ -771,15 +808,19 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   a.pl_end = static_cast<int>(nl);
   a.done = d_done;
   a.kept_ctr = d_kept_ctr;
+  a.nact = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 4);  // zeroed with d_done
   c.arena.reset();
-  const uint64_t room = (c.arena.cap - 8192) / sizeof(uint32_t);
+  a.act = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(c.nS_host, 1) * sizeof(uint32_t)));
+  const uint64_t room = (c.arena.cap - c.arena.used - 8192) / sizeof(uint32_t);
   a.kept_cap = room / 4;
   a.kept = static_cast<uint32_t*>(c.arena.get(a.kept_cap * sizeof(uint32_t)));
   a.wcap = (c.arena.cap - c.arena.used - 4096) / sizeof(uint32_t);
   a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
   void* args[] = {&a};
+  c.probe("lines launch");
   PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(c.line_grid),
                                           dim3(kLineBlock), args, 0, c.stream));
+  c.probe("lines launched");
   // read-back through pinned memory: [done | kept slots | line stats]
   const size_t sw = (sizeof(LineStats) + 7) / 8;
   uint64_t* pin = pinned(c, 2 + (nl - pl0) * sw);
@@ -788,6 +829,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   PM_HIP_CHECK(hipMemcpyAsync(pin + 2, c.d_lstats + pl0, (nl - pl0) * sizeof(LineStats), hipMemcpyDeviceToHost,
                               c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.probe("lines synced");
   std::vector<LineStats> hs(nl - pl0);
   std::memcpy(hs.data(), pin + 2, hs.size() * sizeof(LineStats));
   const unsigned done = static_cast<unsigned>(pin[0] & 0xFFFFFFFFull);
@@ -838,6 +880,8 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     out.stride = static_cast<uint32_t>(c.pattern.lines[pl].cycle_length + 2);
     if (pl >= 4 && want_walks && st.walks) {
       const uint64_t b = st.wbase[0];
+      if (b + st.walks * out.stride > kept.size())
+        throw std::runtime_error("internal: kept TDS walks out of range of the launch's buffer");
       out.walks.assign(kept.begin() + b, kept.begin() + b + st.walks * out.stride);
     }
     outs.push_back(std::move(out));
