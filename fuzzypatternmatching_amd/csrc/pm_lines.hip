@@ -171,10 +171,17 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
 // wave's 64 rows are concatenated and every lane takes every 64th entry, so a
 // long row costs one pass over the wave instead of a serial walk by one lane).
 static constexpr int kLineWaves = 16;  // kLineBlock / kWave
+static constexpr int kStage = 10;      // TDS walks of up to kStage positions are staged in LDS
 struct WaveRows {
   uint64_t beg[kLineWaves][kWave];
   uint32_t end[kLineWaves][kWave];  // inclusive scan of the row lengths
-  uint32_t s[kLineWaves][kWave], u[kLineWaves][kWave], x[kLineWaves][kWave];
+  union {
+    struct {
+      uint32_t s[kLineWaves][kWave], u[kLineWaves][kWave], x[kLineWaves][kWave];
+    } t;                                          // token rows (path lines, TDS sources)
+    uint32_t walk[kLineWaves][kWave * kStage];    // the wave's walks (TDS positions)
+  };
+  unsigned long long wn[20];  // walks per position of a single-block TDS line
 };
 
 // Lane owning concatenated entry t (end[] inclusive scan of the wave's rows).
@@ -207,9 +214,9 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
   if (!total) return 0;
   wr.beg[wv][lane] = b;
   wr.end[wv][lane] = incl;
-  wr.s[wv][lane] = s;
-  wr.u[wv][lane] = u;
-  wr.x[wv][lane] = excl;
+  wr.t.s[wv][lane] = s;
+  wr.t.u[wv][lane] = u;
+  wr.t.x[wv][lane] = excl;
   __builtin_amdgcn_wave_barrier();
   for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
     const uint32_t t = t0 + lane;
@@ -219,8 +226,8 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
       const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
       const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
       if (m & kAlive) {
-        const uint32_t w = m & kPosMask, sr = wr.s[wv][r], ur = wr.u[wv][r];
-        if (w != wr.x[wv][r]) {
+        const uint32_t w = m & kPosMask, sr = wr.t.s[wv][r], ur = wr.t.u[wv][r];
+        if (w != wr.t.x[wv][r]) {
           ++emitted;
           if (k + 1 == la.C + 1) {
             tp_terminal(a, w, sr, ur);
@@ -395,12 +402,14 @@ __device__ __forceinline__ bool tds_child_ok(const uint32_t* w, int k, uint32_t 
   return enum_ok(w, k + 1, nb, la);
 }
 
-// Flattened expansion of the wave's walks win[i0 .. i0 + 64) at position k
-// (rows b/L per lane, L = 0 for walks that fail the arrival checks): children
-// are appended to region out (counter wn[k + 1]).  All lanes must call it.
+// Flattened expansion of the wave's walks at position k (rows b/L per lane,
+// L = 0 for walks that fail the arrival checks): children are appended to
+// region out through counter ctr.  The walks are read from the wave's LDS
+// stage (stage) or from win[i0 ..].  All lanes must call it.
 __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRows& wr, const uint32_t* win,
                                                 uint64_t i0, int k, uint64_t b, uint32_t L, uint32_t* out,
-                                                uint64_t out_room, int stride) {
+                                                uint64_t out_room, int stride, bool stage,
+                                                unsigned long long* ctr) {
   const LineArgs& la = *a.la;
   const int wv = threadIdx.x / kWave, lane = lane_id();
   const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
@@ -418,13 +427,13 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
       const int r = row_of(wr.end[wv], t);
       const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
       const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
-      w = win + (i0 + r) * stride;
+      w = stage ? wr.walk[wv] + r * stride : win + (i0 + r) * stride;
       if (m & kAlive) {
         nb = m & kPosMask;
         child = tds_child_ok(w, k, nb, la);
       }
     }
-    const uint64_t pos = wave_reserve(&a.st->wn[k + 1], child ? 1u : 0u);
+    const uint64_t pos = wave_reserve(ctr, child ? 1u : 0u);
     if (child) {
       if ((pos + 1) * stride <= out_room) {
         uint32_t* d = out + pos * stride;
@@ -531,32 +540,56 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   const LineArgs& la = *a.la;
   const int stride = la.C + 2;
   uint64_t trav = 0, tokens = 0, in_base = 0;
+  // single block: the walk counters live in LDS (no global atomic per wave and round)
+  const bool stage = stride <= kStage;
+  if (single) {
+    if (threadIdx.x < 20) wr.wn[threadIdx.x] = threadIdx.x == 1 ? ld_acq(&st->wn[1]) : 0ull;
+    __syncthreads();
+  }
+  const int wv = threadIdx.x / kWave, lane = lane_id();
   for (int k = 1; k <= la.C; ++k) {
     if (ld_acq(&st->overflow)) break;
-    const uint64_t nin = ld_acq(&st->wn[k]);
+    const uint64_t nin = single ? wr.wn[k] : ld_acq(&st->wn[k]);
     const uint64_t out_base = (in_base + nin * stride + 31) & ~uint64_t(31);
     tokens += g.tid == 0 ? nin : 0;
     const uint32_t* win = a.wbuf + in_base;
+    unsigned long long* ctr = single ? &wr.wn[k + 1] : &st->wn[k + 1];
     for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
-      const uint64_t i = i0 + lane_id();
+      const uint64_t i = i0 + lane;
       uint64_t b = 0;
       uint32_t L = 0;
       if (i < nin) {
         const uint32_t* w = win + i * stride;
-        const uint32_t u = w[k];
-        if (pos_ok(a.tpub[u], k, la) && enum_ok(w, k, u, la)) {
-          b = a.offp[u];
-          L = a.mlen[u];
-          trav += a.malive[u];
+        uint32_t u;
+        if (stage) {  // the walk's positions (independent loads) into the wave's stage
+          uint32_t* sw = wr.walk[wv] + lane * stride;
+#pragma unroll
+          for (int p = 0; p < kStage; ++p)
+            if (p <= k) sw[p] = w[p];
+          u = sw[k];
+          w = sw;
+        } else {
+          u = w[k];
+        }
+        // the row of u is fetched together with its T_pub (used if the arrival checks pass)
+        const uint16_t T = a.tpub[u];
+        const uint64_t ob = a.offp[u];
+        const uint32_t ml = a.mlen[u], ma = a.malive[u];
+        if (pos_ok(T, k, la) && enum_ok(w, k, u, la)) {
+          b = ob;
+          L = ml;
+          trav += ma;
         }
       }
-      tds_expand_wave(a, wr, win, i0, k, b, L, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride);
+      __builtin_amdgcn_wave_barrier();
+      tds_expand_wave(a, wr, win, i0, k, b, L, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride,
+                      stage, ctr);
     }
     in_base = out_base;
     phase_sync(a, single);
   }
   // every final walk may be kept: its room must exist before any terminal effect
-  const uint64_t nw = ld_acq(&st->wn[la.C + 1]);
+  const uint64_t nw = single ? wr.wn[la.C + 1] : ld_acq(&st->wn[la.C + 1]);
   // kept slots used by the launch's earlier lines (read at line start: the
   // terminal loop below adds to the counter while slower blocks still enter it)
   const uint64_t kept0 = kept_base;
@@ -629,7 +662,7 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
     if (!total) continue;
     wr.beg[wv][lane] = b;
     wr.end[wv][lane] = incl;
-    wr.s[wv][lane] = s;
+    wr.t.s[wv][lane] = s;
     __builtin_amdgcn_wave_barrier();
     for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
       const uint32_t t = t0 + lane;
@@ -638,7 +671,7 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
         const int r = row_of(wr.end[wv], t);
         const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
         m = a.mcol[wr.beg[wv][r] + (t - first)];
-        sr = wr.s[wv][r];
+        sr = wr.t.s[wv][r];
       }
       const bool alive = (m & kAlive) != 0;
       const uint64_t pos = wave_reserve(&st->wn[1], alive ? 1u : 0u);
