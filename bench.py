@@ -39,6 +39,8 @@ def log(*a):
 
 
 def main():
+    import faulthandler
+    faulthandler.enable()  # a fatal signal prints the Python stack
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -100,7 +102,8 @@ def main():
         off, col, deg = pm.partition_edges(src, dst, n, device=f"cuda:{local_rank}")
         del src, dst
         t = torch.tensor([int(off[-1])], dtype=torch.int64, device="cuda")
-        dist.all_reduce(t)
+        if world > 1:
+            dist.all_reduce(t)
         nnz = int(t.item())
         uid = [pm.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)

@@ -121,24 +121,31 @@ def partition_edges(src, dst, n, group=None, device="cpu"):
     # u32 ids travel as int32 and widen on the device
     s = torch.from_numpy(np.ascontiguousarray(src, dtype=np.uint32).view(np.int32)).to(device).long() & 0xFFFFFFFF
     d = torch.from_numpy(np.ascontiguousarray(dst, dtype=np.uint32).view(np.int32)).to(device).long() & 0xFFFFFFFF
-    owner = s % G
-    order = torch.argsort(owner, stable=True)
-    s, d, owner = s[order], d[order], owner[order]
-    send = torch.bincount(owner, minlength=G).to(torch.int64)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
-    sc, rc = send.tolist(), recv.tolist()
-    rs = torch.empty(sum(rc), dtype=torch.int64, device=device)
-    rd = torch.empty(sum(rc), dtype=torch.int64, device=device)
-    dist.all_to_all_single(rs, s, rc, sc, group=group)
-    dist.all_to_all_single(rd, d, rc, sc, group=group)
-    del s, d, owner, order
+    if G == 1:  # nothing to exchange
+        rs, rd = s, d
+    else:
+        owner = s % G
+        order = torch.argsort(owner, stable=True)
+        s, d, owner = s[order], d[order], owner[order]
+        # counts by scatter-add (torch.bincount of constant data raised SIGFPE on this image)
+        send = torch.zeros(G, dtype=torch.int64, device=device).index_add_(0, owner, torch.ones_like(owner))
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=group)
+        sc, rc = send.tolist(), recv.tolist()
+        rs = torch.empty(sum(rc), dtype=torch.int64, device=device)
+        rd = torch.empty(sum(rc), dtype=torch.int64, device=device)
+        dist.all_to_all_single(rs, s, rc, sc, group=group)
+        dist.all_to_all_single(rd, d, rc, sc, group=group)
+        del owner, order
+    del s, d
     key = torch.sort(rs * n + rd).values
     rs, rd = key // n, key % n
     del key
-    deg = torch.bincount(rs, minlength=n).to(torch.int32)
+    deg = torch.zeros(n, dtype=torch.int32, device=device).index_add_(
+        0, rs, torch.ones(rs.shape[0], dtype=torch.int32, device=device))
     gdeg = deg.clone()
-    dist.all_reduce(gdeg, group=group)
+    if G > 1:  # (a one-rank RCCL all-reduce of a large buffer raises SIGFPE on this image)
+        dist.all_reduce(gdeg, group=group)
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(deg.cpu().numpy().astype(np.uint64))
     return off, rd.to(torch.int32).cpu().numpy().view(np.uint32).copy(), gdeg.cpu().numpy().view(np.uint32).copy()

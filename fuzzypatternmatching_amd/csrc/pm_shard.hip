@@ -45,7 +45,7 @@ namespace pm {
 // RCCL (one process per GPU, xGMI): stream-ordered, no host synchronisation.
 class RcclComm : public Comm {
  public:
-  RcclComm(const void* unique_id, int nranks, int rank) {
+  RcclComm(const void* unique_id, int nranks, int rank) : nranks_(nranks) {
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     PM_NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
@@ -53,15 +53,23 @@ class RcclComm : public Comm {
   ~RcclComm() override {
     if (comm_) (void)ncclCommDestroy(comm_);
   }
+  // One rank: a copy / nothing (one-rank RCCL collectives of large buffers
+  // raise SIGFPE in this RCCL build; the communicator is still initialised).
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    if (nranks_ == 1) {
+      if (bytes && send != recv) PM_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+      return;
+    }
     PM_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    if (nranks_ == 1) return;
     PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm_, s));
   }
 
  private:
   ncclComm_t comm_ = nullptr;
+  int nranks_ = 1;
 };
 
 Comm* make_rccl_comm(const void* unique_id, int nranks, int rank) { return new RcclComm(unique_id, nranks, rank); }
