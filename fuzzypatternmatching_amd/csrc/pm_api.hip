@@ -199,7 +199,8 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred};
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
+                  c->d_aown, c->d_axl, c->d_anum, c->d_asend, c->d_arecv, c->d_lstats_loc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete c->comm_owned;
@@ -596,40 +597,60 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         bool fused = false;
         auto t1 = tick();
         if (c.comm) {
-          // sharded: one line per launch over this shard's sources, then the
-          // line's sums and the post-processed T_pub of every shard
+          // sharded: one line per launch over this shard's sources; the line's
+          // sums and every shard's post-processed T_pub follow on the stream
           shard_replicate_m(c);
           std::vector<FusedLineOut> one;
           bool overflow = false;
-          if (c.fused_lines && run_lines_fused(c, pl, files, one, overflow, 1) == 1) {
+          const bool ok = c.fused_lines && run_lines_fused(c, pl, files, one, overflow, 1, true) == 1;
+          if (ok && !c.any_overflow) {
             fo = std::move(one[0]);
             tr = fo.tr;
             deleted = fo.deleted;
+            vc = cur_vc;
+            ec = cur_ec;
             for (uint32_t r = 0; r < c.nranks; ++r) {
               loc_vc[r] -= fo.rm_v[r];
               loc_ec[r] -= fo.rm_e[r];
+              vc[r] -= fo.grm_v[r];
+              ec[r] -= fo.grm_e[r];
             }
             walks.swap(fo.walks);
             stride = fo.stride;
           } else {
-            tr = pl >= 4 ? run_tds_line(c, line, walks, stride) : run_path_line(c, line);
-            deleted = launch_post_tp(c, line);
-            count_state(c, loc_vc, loc_ec);
-            stride = static_cast<uint32_t>(line.cycle_length + 2);
+            // some shard overflowed a capacity (or fused lines are off): shards
+            // that overflowed rerun the line on the exact-count path, the others
+            // keep their fused results; then host sums and a full T_pub exchange
+            if (ok) {
+              fo = std::move(one[0]);
+              tr = fo.ltr;
+              deleted = fo.ldeleted;
+              for (uint32_t r = 0; r < c.nranks; ++r) {
+                loc_vc[r] -= fo.rm_v[r];
+                loc_ec[r] -= fo.rm_e[r];
+              }
+              walks.swap(fo.walks);
+              stride = fo.stride;
+            } else {
+              tr = pl >= 4 ? run_tds_line(c, line, walks, stride) : run_path_line(c, line);
+              deleted = launch_post_tp(c, line);
+              count_state(c, loc_vc, loc_ec);
+              stride = static_cast<uint32_t>(line.cycle_length + 2);
+            }
+            std::vector<uint64_t> sums = {deleted, tr.sources, tr.acked, tr.edges, tr.tokens, tr.walks};
+            sums.insert(sums.end(), loc_vc.begin(), loc_vc.end());
+            sums.insert(sums.end(), loc_ec.begin(), loc_ec.end());
+            sums = shard_allreduce(c, sums);
+            deleted = sums[0] ? 1u : 0u;
+            tr.sources = sums[1];
+            tr.acked = sums[2];
+            tr.edges = sums[3];
+            tr.tokens = sums[4];
+            tr.walks = sums[5];
+            vc.assign(sums.begin() + 6, sums.begin() + 6 + c.nranks);
+            ec.assign(sums.begin() + 6 + c.nranks, sums.begin() + 6 + 2 * c.nranks);
+            shard_exchange_tpub(c);
           }
-          std::vector<uint64_t> sums = {deleted, tr.sources, tr.acked, tr.edges, tr.tokens, tr.walks};
-          sums.insert(sums.end(), loc_vc.begin(), loc_vc.end());
-          sums.insert(sums.end(), loc_ec.begin(), loc_ec.end());
-          sums = shard_allreduce(c, sums);
-          deleted = sums[0] ? 1u : 0u;
-          tr.sources = sums[1];
-          tr.acked = sums[2];
-          tr.edges = sums[3];
-          tr.tokens = sums[4];
-          tr.walks = sums[5];
-          vc.assign(sums.begin() + 6, sums.begin() + 6 + c.nranks);
-          ec.assign(sums.begin() + 6 + c.nranks, sums.begin() + 6 + 2 * c.nranks);
-          shard_exchange_tpub(c);
           if (files && pl >= 4) {
             std::vector<uint32_t> all;
             for (auto& part : shard_allgatherv(c, walks)) all.insert(all.end(), part.begin(), part.end());

@@ -213,6 +213,18 @@ struct Ctx {
   uint64_t* d_xred = nullptr;     // host-vector all-reduce staging
   size_t xred_cap = 0;
   bool m_dirty = true;            // M changed since the last replication
+  // S members of every shard at the last M replication (superset of S during
+  // token passing): the per-line T_pub exchange covers these only
+  uint32_t amax = 0;              // max |S list| over shards
+  std::vector<uint32_t> anum;     // |S list| per shard
+  uint32_t* d_aown = nullptr;     // this shard's S positions (amax)
+  uint32_t* d_axl = nullptr;      // nshards x amax
+  uint32_t* d_anum = nullptr;     // per shard (device)
+  uint16_t* d_asend = nullptr;    // amax
+  uint16_t* d_arecv = nullptr;    // nshards x amax
+  size_t acap = 0;
+  LineStats* d_lstats_loc = nullptr;  // this shard's copy of a summed line
+  bool any_overflow = false;
 
   // host side of the driver loop
   uint64_t* h_pin = nullptr;      // pinned staging for counter / line-stat read-backs
@@ -325,6 +337,11 @@ struct FusedLineOut {
   TpResult tr;
   uint32_t deleted = 0;
   std::vector<uint64_t> rm_v, rm_e;
+  // sum_shards: tr / deleted / grm_* are the sums over the shards, ltr /
+  // ldeleted / rm_* this shard's own values (equal otherwise)
+  TpResult ltr;
+  uint32_t ldeleted = 0;
+  std::vector<uint64_t> grm_v, grm_e;
   std::vector<uint32_t> walks;  // kept TDS walks (positions), when requested
   uint32_t stride = 0;
 };
@@ -334,8 +351,12 @@ struct FusedLineOut {
 // path).
 // max_lines bounds the lines of one launch (sharded searches run one line per
 // launch: the shards exchange T_pub between lines).
+// sum_shards (sharded, one line): the line's statistics are summed over the
+// shards and the T_pub of every shard's S members exchanged on the stream
+// before the single host synchronisation; c.any_overflow reports an overflow
+// on any shard (overflow: on this one).
 size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
-                       size_t max_lines = SIZE_MAX);
+                       size_t max_lines = SIZE_MAX, bool sum_shards = false);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);
@@ -347,7 +368,8 @@ uint64_t* pinned(Ctx& c, size_t words);  // pinned host staging (pm_api.hip)
 // Shard exchanges (pm_shard.hip); no-ops when nshards == 1.
 void shard_after_first(Ctx& c);      // after superstep 0: slists of all shards + T_pub
 void shard_exchange_tpub(Ctx& c);    // T_pub of every shard's slist entries
-void shard_replicate_m(Ctx& c);      // alive M rows of S into the remote region (if m_dirty)
+void shard_replicate_m(Ctx& c);      // alive M rows of S into the remote region (if m_dirty), S lists
+void shard_exchange_tpub_s(Ctx& c);  // T_pub of every shard's S list (token-passing phase)
 std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  // host vector, sum
 // Variable-size gather of a host u32 vector: every shard receives all blocks.
 std::vector<std::vector<uint32_t>> shard_allgatherv(Ctx& c, const std::vector<uint32_t>& v);

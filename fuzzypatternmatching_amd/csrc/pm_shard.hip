@@ -124,23 +124,29 @@ class ThreadComm : public Comm {
     DeviceReleased rel(g_);
     g_->ptrs[rank_] = send;
     g_->barrier();
+    // on the caller's stream, completed before the barrier: a device-to-device
+    // hipMemcpy may return before the copy is done, and the caller's
+    // non-blocking stream is not ordered after the null stream
     for (int q = 0; q < g_->n; ++q)
       if (bytes)
-        PM_HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + size_t(q) * bytes, g_->ptrs[q], bytes,
-                               hipMemcpyDeviceToDevice));
+        PM_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + size_t(q) * bytes, g_->ptrs[q], bytes,
+                                    hipMemcpyDeviceToDevice, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));
     g_->barrier();
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
     PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     std::vector<uint64_t> h(count), sum(count, 0);
-    if (count) PM_HIP_CHECK(hipMemcpy(h.data(), buf, count * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (count) PM_HIP_CHECK(hipMemcpyAsync(h.data(), buf, count * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));
     g_->hvec[rank_] = &h;
     g_->barrier();
     for (int q = 0; q < g_->n; ++q)
       for (size_t i = 0; i < count; ++i) sum[i] += (*g_->hvec[q])[i];
     g_->barrier();
-    if (count) PM_HIP_CHECK(hipMemcpy(buf, sum.data(), count * sizeof(uint64_t), hipMemcpyHostToDevice));
+    if (count) PM_HIP_CHECK(hipMemcpyAsync(buf, sum.data(), count * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));
   }
 
  private:
@@ -240,6 +246,15 @@ __global__ void k_m_unpack(const uint32_t* __restrict__ xslist, const uint32_t* 
   }
 }
 
+// This shard's S members (slist entries with T_pub != 0), unordered.
+__global__ void k_s_collect(const uint32_t* __restrict__ slist, uint32_t nS, const uint16_t* __restrict__ tpub,
+                            uint32_t* __restrict__ out, unsigned int* __restrict__ ctr) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t p = slist[i];
+    if (tpub[p]) out[atomicAdd(ctr, 1u)] = p;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 template <typename T>
@@ -299,6 +314,17 @@ void shard_exchange_tpub(Ctx& c) {
   c.comm->allgather(c.d_xsend, c.d_xrecv, size_t(maxS) * sizeof(uint16_t), c.stream);
   hipLaunchKernelGGL(k_unpack_tpub, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream, c.d_xslist, c.d_xnS,
                      maxS, G, c.shard, c.d_xrecv, c.d_tpub[c.cur]);
+  PM_HIP_CHECK(hipGetLastError());
+}
+
+void shard_exchange_tpub_s(Ctx& c) {
+  if (!c.comm) return;
+  const uint32_t G = c.nshards, maxA = std::max<uint32_t>(c.amax, 1), nA = c.anum[c.shard];
+  if (nA) hipLaunchKernelGGL(k_pack_tpub, dim3(xgrid(nA)), dim3(kXBlock), 0, c.stream, c.d_aown, nA, c.d_tpub[c.cur],
+                             c.d_asend);
+  c.comm->allgather(c.d_asend, c.d_arecv, size_t(maxA) * sizeof(uint16_t), c.stream);
+  hipLaunchKernelGGL(k_unpack_tpub, dim3(xgrid(uint64_t(G) * maxA)), dim3(kXBlock), 0, c.stream, c.d_axl, c.d_anum,
+                     maxA, G, c.shard, c.d_arecv, c.d_tpub[c.cur]);
   PM_HIP_CHECK(hipGetLastError());
 }
 
@@ -362,8 +388,20 @@ void shard_replicate_m(Ctx& c) {
   PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * maxS),
                                                 c.stream));
   hipLaunchKernelGGL(k_seg_starts, dim3(1), dim3(64 * ((G + 64) / 64)), 0, c.stream, xoff, maxS, G, seg);
-  std::vector<uint64_t> hseg(G + 1);
+  // this shard's S list (T_pub exchange of the token-passing phase)
+  if (c.acap < std::max<uint32_t>(nS, 1)) {
+    if (c.d_aown) (void)hipFree(c.d_aown);
+    c.acap = std::max<uint32_t>(nS, 1);
+    PM_HIP_CHECK(hipMalloc(&c.d_aown, c.acap * sizeof(uint32_t)));
+  }
+  auto* actr = static_cast<unsigned int*>(c.arena.get(sizeof(unsigned int)));
+  PM_HIP_CHECK(hipMemsetAsync(actr, 0, sizeof(unsigned int), c.stream));
+  if (nS)
+    hipLaunchKernelGGL(k_s_collect, dim3(xgrid(nS)), dim3(kXBlock), 0, c.stream, c.d_slist, nS, tpub, c.d_aown, actr);
+  std::vector<uint64_t> hseg(G + 2);
   PM_HIP_CHECK(hipMemcpyAsync(hseg.data(), seg, (G + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  unsigned int na = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&na, actr, sizeof(unsigned int), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   uint64_t maxT = 1;
   for (uint32_t g = 0; g < G; ++g) maxT = std::max(maxT, hseg[g + 1] - hseg[g]);
@@ -387,6 +425,39 @@ void shard_replicate_m(Ctx& c) {
   hipLaunchKernelGGL(k_m_unpack, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream, c.d_xslist, c.d_xnS,
                      xcnt, xoff, seg, maxS, G, c.shard, c.nq, maxT, c.d_offp, c.d_mlen, c.d_malive);
   PM_HIP_CHECK(hipGetLastError());
+  // every shard's S list
+  {
+    std::vector<uint64_t> an(G, 0);
+    an[c.shard] = na;
+    an = shard_allreduce(c, an);
+    c.anum.assign(G, 0);
+    uint32_t amax = 1;
+    for (uint32_t g = 0; g < G; ++g) {
+      c.anum[g] = static_cast<uint32_t>(an[g]);
+      amax = std::max(amax, c.anum[g]);
+    }
+    if (amax > c.amax || !c.d_axl) {
+      void* ptrs[] = {c.d_axl, c.d_anum, c.d_asend, c.d_arecv};
+      for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+      PM_HIP_CHECK(hipMalloc(&c.d_axl, size_t(G) * amax * sizeof(uint32_t)));
+      PM_HIP_CHECK(hipMalloc(&c.d_anum, G * sizeof(uint32_t)));
+      PM_HIP_CHECK(hipMalloc(&c.d_asend, size_t(amax) * sizeof(uint16_t)));
+      PM_HIP_CHECK(hipMalloc(&c.d_arecv, size_t(G) * amax * sizeof(uint16_t)));
+      if (c.acap < amax) {  // the send block is amax entries long
+        uint32_t* nb = nullptr;
+        PM_HIP_CHECK(hipMalloc(&nb, amax * sizeof(uint32_t)));
+        if (na) PM_HIP_CHECK(hipMemcpyAsync(nb, c.d_aown, na * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+        PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+        (void)hipFree(c.d_aown);
+        c.d_aown = nb;
+        c.acap = amax;
+      }
+    }
+    c.amax = amax;
+    PM_HIP_CHECK(hipMemcpyAsync(c.d_anum, c.anum.data(), G * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+    c.comm->allgather(c.d_aown, c.d_axl, size_t(amax) * sizeof(uint32_t), c.stream);
+  }
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.arena.reset();
   c.m_dirty = false;
