@@ -546,6 +546,8 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   auto record_lcc = [&](const LccOut& lo, uint64_t itr_) {
     loc_vc = lo.loc_vc;
     loc_ec = lo.loc_ec;
+    c.live_hint = 0;
+    for (auto x : loc_vc) c.live_hint += x;
     for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
       f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
       add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);

@@ -281,7 +281,8 @@ struct Ctx {
   uint64_t hcap = 0;
   uint32_t* d_front = nullptr;    // slots inserted by a fused path line (cleared by it)
   unsigned* d_gbar = nullptr;     // grid barrier state of the fused line kernels
-  unsigned line_grid = 0;
+  unsigned line_grid = 0;         // blocks of a full-chip line launch (one per CU)
+  uint64_t live_hint = ~0ull;     // S members on this context after the last LCC call (line grid size)
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
 
   // last token-passing call

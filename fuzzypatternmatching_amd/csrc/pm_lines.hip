@@ -704,7 +704,10 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
 __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ WaveRows wr;
+  unsigned long long* kst = reinterpret_cast<unsigned long long*>(a.gbar + kGbarWords + 8);  // diagnostics
+  if (blockIdx.x == 0 && threadIdx.x == 0) kst[0] = __builtin_amdgcn_s_memrealtime();
   build_active(a);
+  if (blockIdx.x == 0 && threadIdx.x == 0) kst[1] = __builtin_amdgcn_s_memrealtime();
   tree_barrier(a.gbar);
   for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
     const LineDesc& d = a.lines[pl];
@@ -853,7 +856,11 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
   void* args[] = {&a};
   c.probe("lines launch");
-  PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(c.line_grid),
+  // few state-map members: a smaller grid (dispatching the full one costs ~50 us
+  // before the first grid barrier completes)
+  const unsigned grid = static_cast<unsigned>(
+      std::max<uint64_t>(16, std::min<uint64_t>(c.line_grid, (c.live_hint + 255) / 256)));
+  PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(grid),
                                           dim3(kLineBlock), args, 0, c.stream));
   c.probe("lines launched");
   // read-back through pinned memory: [done | kept slots | line stats | summed stats]
@@ -884,6 +891,12 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     PM_HIP_CHECK(hipMemcpy(kept.data(), a.kept, kept_slots * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
+  if (std::getenv("PM_PHASE_TIMES")) {
+    unsigned long long ks[2] = {0, 0};
+    PM_HIP_CHECK(hipMemcpy(ks, c.d_gbar + kGbarWords + 8, sizeof(ks), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[pm] lines launch: active list %.1f us, to line start %.1f us\n", (ks[1] - ks[0]) * 0.01,
+                 (hs[0].tstamp[0] - ks[1]) * 0.01);
+  }
   if (std::getenv("PM_PHASE_TIMES"))
     for (unsigned j = 0; j + pl0 < done; ++j) {
       const LineStats& st = hs[j];

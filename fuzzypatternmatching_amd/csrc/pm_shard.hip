@@ -363,32 +363,10 @@ void shard_after_first(Ctx& c) {
 
 void shard_replicate_m(Ctx& c) {
   if (!c.comm || !c.m_dirty) return;
-  const uint32_t G = c.nshards, maxS = c.xmaxS, nS = c.xnS[c.shard];
-  c.arena.reset();
-  auto* cnt = static_cast<uint32_t*>(c.arena.get(size_t(maxS) * sizeof(uint32_t)));
-  auto* xcnt = static_cast<uint32_t*>(c.arena.get(size_t(G) * maxS * sizeof(uint32_t)));
-  auto* moff = static_cast<uint64_t*>(c.arena.get((size_t(maxS) + 1) * sizeof(uint64_t)));
-  auto* xoff = static_cast<uint64_t*>(c.arena.get((size_t(G) * maxS + 1) * sizeof(uint64_t)));
-  auto* seg = static_cast<uint64_t*>(c.arena.get((G + 1) * sizeof(uint64_t)));
+  const uint32_t G = c.nshards, nS = c.xnS[c.shard];
   const uint16_t* tpub = c.d_tpub[c.cur];
-  hipLaunchKernelGGL(k_m_counts, dim3(xgrid(maxS)), dim3(kXBlock), 0, c.stream, c.d_slist, nS, maxS, tpub, c.d_malive,
-                     cnt);
-  c.comm->allgather(cnt, xcnt, size_t(maxS) * sizeof(uint32_t), c.stream);
-  // exclusive scans (own counts; all shards' counts) with a total slot at the end
-  PM_HIP_CHECK(hipMemsetAsync(moff, 0, sizeof(uint64_t), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(xoff, 0, sizeof(uint64_t), c.stream));
-  size_t t1 = 0, t2 = 0;
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, t1, cnt, moff + 1, static_cast<int>(maxS), c.stream));
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, t2, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * maxS),
-                                                c.stream));
-  size_t tb = std::max(t1, t2);
-  void* tmp = c.arena.get(tb);
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, cnt, moff + 1, static_cast<int>(maxS), c.stream));
-  tb = std::max(t1, t2);
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * maxS),
-                                                c.stream));
-  hipLaunchKernelGGL(k_seg_starts, dim3(1), dim3(64 * ((G + 64) / 64)), 0, c.stream, xoff, maxS, G, seg);
-  // this shard's S list (T_pub exchange of the token-passing phase)
+  c.arena.reset();
+  // 1. this shard's S list (the only rows token passing reads from it), then every shard's
   if (c.acap < std::max<uint32_t>(nS, 1)) {
     if (c.d_aown) (void)hipFree(c.d_aown);
     c.acap = std::max<uint32_t>(nS, 1);
@@ -398,14 +376,68 @@ void shard_replicate_m(Ctx& c) {
   PM_HIP_CHECK(hipMemsetAsync(actr, 0, sizeof(unsigned int), c.stream));
   if (nS)
     hipLaunchKernelGGL(k_s_collect, dim3(xgrid(nS)), dim3(kXBlock), 0, c.stream, c.d_slist, nS, tpub, c.d_aown, actr);
-  std::vector<uint64_t> hseg(G + 2);
-  PM_HIP_CHECK(hipMemcpyAsync(hseg.data(), seg, (G + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  unsigned int na = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(&na, actr, sizeof(unsigned int), hipMemcpyDeviceToHost, c.stream));
+  uint64_t* pin = pinned(c, 4);
+  PM_HIP_CHECK(hipMemcpyAsync(pin, actr, sizeof(unsigned int), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  const uint32_t na = static_cast<uint32_t>(pin[0] & 0xFFFFFFFFull);
+  std::vector<uint64_t> an(G, 0);
+  an[c.shard] = na;
+  an = shard_allreduce(c, an);
+  c.anum.assign(G, 0);
+  uint32_t amax = 1;
+  for (uint32_t g = 0; g < G; ++g) {
+    c.anum[g] = static_cast<uint32_t>(an[g]);
+    amax = std::max(amax, c.anum[g]);
+  }
+  if (amax > c.amax || !c.d_axl) {
+    void* ptrs[] = {c.d_axl, c.d_anum, c.d_asend, c.d_arecv};
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+    PM_HIP_CHECK(hipMalloc(&c.d_axl, size_t(G) * amax * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMalloc(&c.d_anum, G * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMalloc(&c.d_asend, size_t(amax) * sizeof(uint16_t)));
+    PM_HIP_CHECK(hipMalloc(&c.d_arecv, size_t(G) * amax * sizeof(uint16_t)));
+  }
+  if (c.acap < amax) {  // the send block is amax entries long
+    uint32_t* nb = nullptr;
+    PM_HIP_CHECK(hipMalloc(&nb, amax * sizeof(uint32_t)));
+    if (na) PM_HIP_CHECK(hipMemcpyAsync(nb, c.d_aown, na * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    (void)hipFree(c.d_aown);
+    c.d_aown = nb;
+    c.acap = amax;
+  }
+  c.amax = amax;
+  PM_HIP_CHECK(hipMemcpyAsync(c.d_anum, c.anum.data(), G * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  c.comm->allgather(c.d_aown, c.d_axl, size_t(amax) * sizeof(uint32_t), c.stream);
+  // 2. alive-entry counts per S entry, every shard's, and their exclusive scans
+  auto* cnt = static_cast<uint32_t*>(c.arena.get(size_t(amax) * sizeof(uint32_t)));
+  auto* xcnt = static_cast<uint32_t*>(c.arena.get(size_t(G) * amax * sizeof(uint32_t)));
+  auto* moff = static_cast<uint64_t*>(c.arena.get((size_t(amax) + 1) * sizeof(uint64_t)));
+  auto* xoff = static_cast<uint64_t*>(c.arena.get((size_t(G) * amax + 1) * sizeof(uint64_t)));
+  auto* seg = static_cast<uint64_t*>(c.arena.get((G + 1) * sizeof(uint64_t)));
+  hipLaunchKernelGGL(k_m_counts, dim3(xgrid(amax)), dim3(kXBlock), 0, c.stream, c.d_aown, na, amax, tpub, c.d_malive,
+                     cnt);
+  c.comm->allgather(cnt, xcnt, size_t(amax) * sizeof(uint32_t), c.stream);
+  PM_HIP_CHECK(hipMemsetAsync(moff, 0, sizeof(uint64_t), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(xoff, 0, sizeof(uint64_t), c.stream));
+  size_t t1 = 0, t2 = 0;
+  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, t1, cnt, moff + 1, static_cast<int>(amax), c.stream));
+  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, t2, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * amax),
+                                                c.stream));
+  size_t tb = std::max(t1, t2);
+  void* tmp = c.arena.get(tb);
+  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, cnt, moff + 1, static_cast<int>(amax), c.stream));
+  tb = std::max(t1, t2);
+  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * amax),
+                                                c.stream));
+  hipLaunchKernelGGL(k_seg_starts, dim3(1), dim3(64 * ((G + 64) / 64)), 0, c.stream, xoff, amax, G, seg);
+  pin = pinned(c, G + 1);
+  PM_HIP_CHECK(hipMemcpyAsync(pin, seg, (G + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   uint64_t maxT = 1;
-  for (uint32_t g = 0; g < G; ++g) maxT = std::max(maxT, hseg[g + 1] - hseg[g]);
-  // the remote region follows this shard's own slots in d_mcol
+  for (uint32_t g = 0; g < G; ++g) maxT = std::max(maxT, pin[g + 1] - pin[g]);
+  // 3. the alive rows of every shard's S into the remote region after this shard's own slots
   const uint64_t need = c.nq + uint64_t(G) * maxT;
   if (need > c.mcap) {
     const uint64_t cap = std::max(need, c.mcap + c.mcap / 4);
@@ -418,46 +450,13 @@ void shard_replicate_m(Ctx& c) {
     c.mcap = cap;
   }
   auto* send = static_cast<uint32_t*>(c.arena.get(maxT * sizeof(uint32_t)));
-  if (nS)
-    hipLaunchKernelGGL(k_m_pack, dim3(xgrid(uint64_t(nS) * kWave)), dim3(kXBlock), 0, c.stream, c.d_slist, nS, tpub,
+  if (na)
+    hipLaunchKernelGGL(k_m_pack, dim3(xgrid(uint64_t(na) * kWave)), dim3(kXBlock), 0, c.stream, c.d_aown, na, tpub,
                        c.d_offp, c.d_mlen, c.d_mcol, moff, send);
   c.comm->allgather(send, c.d_mcol + c.nq, maxT * sizeof(uint32_t), c.stream);
-  hipLaunchKernelGGL(k_m_unpack, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream, c.d_xslist, c.d_xnS,
-                     xcnt, xoff, seg, maxS, G, c.shard, c.nq, maxT, c.d_offp, c.d_mlen, c.d_malive);
+  hipLaunchKernelGGL(k_m_unpack, dim3(xgrid(uint64_t(G) * amax)), dim3(kXBlock), 0, c.stream, c.d_axl, c.d_anum, xcnt,
+                     xoff, seg, amax, G, c.shard, c.nq, maxT, c.d_offp, c.d_mlen, c.d_malive);
   PM_HIP_CHECK(hipGetLastError());
-  // every shard's S list
-  {
-    std::vector<uint64_t> an(G, 0);
-    an[c.shard] = na;
-    an = shard_allreduce(c, an);
-    c.anum.assign(G, 0);
-    uint32_t amax = 1;
-    for (uint32_t g = 0; g < G; ++g) {
-      c.anum[g] = static_cast<uint32_t>(an[g]);
-      amax = std::max(amax, c.anum[g]);
-    }
-    if (amax > c.amax || !c.d_axl) {
-      void* ptrs[] = {c.d_axl, c.d_anum, c.d_asend, c.d_arecv};
-      for (void* p : ptrs)
-        if (p) (void)hipFree(p);
-      PM_HIP_CHECK(hipMalloc(&c.d_axl, size_t(G) * amax * sizeof(uint32_t)));
-      PM_HIP_CHECK(hipMalloc(&c.d_anum, G * sizeof(uint32_t)));
-      PM_HIP_CHECK(hipMalloc(&c.d_asend, size_t(amax) * sizeof(uint16_t)));
-      PM_HIP_CHECK(hipMalloc(&c.d_arecv, size_t(G) * amax * sizeof(uint16_t)));
-      if (c.acap < amax) {  // the send block is amax entries long
-        uint32_t* nb = nullptr;
-        PM_HIP_CHECK(hipMalloc(&nb, amax * sizeof(uint32_t)));
-        if (na) PM_HIP_CHECK(hipMemcpyAsync(nb, c.d_aown, na * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
-        PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-        (void)hipFree(c.d_aown);
-        c.d_aown = nb;
-        c.acap = amax;
-      }
-    }
-    c.amax = amax;
-    PM_HIP_CHECK(hipMemcpyAsync(c.d_anum, c.anum.data(), G * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-    c.comm->allgather(c.d_aown, c.d_axl, size_t(amax) * sizeof(uint32_t), c.stream);
-  }
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.arena.reset();
   c.m_dirty = false;
