@@ -54,7 +54,7 @@ def main():
                     help="directory: reuse / store the generated one-GPU graph (repeated profiling runs)")
     ap.add_argument("--sharded", action="store_true",
                     help="take the sharded (RCCL) path even at N=1 (rehearsal of the multi-GPU code on one GPU)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_lcc_first.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_final_pmc_lcc_first.json"))
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
