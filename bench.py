@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--graph-cache", default=os.environ.get("PM_GRAPH_CACHE"),
                     help="directory: reuse / store the generated one-GPU graph (repeated profiling runs)")
+    ap.add_argument("--gen", choices=["gpu", "host"], default="gpu",
+                    help="R-MAT generator: gpu (pm_rmat.hip, adjacency built in HBM) or host (host/rmat.hpp)")
     ap.add_argument("--sharded", action="store_true",
                     help="take the sharded (RCCL) path even at N=1 (rehearsal of the multi-GPU code on one GPU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_final_pmc_lcc_first.json"))
@@ -78,7 +80,13 @@ def main():
     pattern_dir = os.path.join(ROOT, "patterns", args.pattern)
     t0 = time.time()
     g = None
-    if not sharded:
+    if not sharded and args.gen == "gpu" and not args.graph_cache:
+        m, gen_s = pm.rmat_matcher(args.scale, args.p_gen, pattern_dir, device=0)
+        n, nnz = 1 << args.scale, (1 << args.scale) * 32
+        log(f"[rank {rank}] generated R-MAT S={args.scale} P_gen={args.p_gen} on the GPU: V={n} E={nnz} "
+            f"in {gen_s:.1f}s; context (layout, tiling) ready after {time.time() - t0:.1f}s")
+        t0 = time.time()
+    elif not sharded:
         cache = (os.path.join(args.graph_cache, f"rmat_s{args.scale}_p{args.p_gen}") if args.graph_cache else None)
         if cache and os.path.exists(cache + "_0_of_1"):
             g = pm.read_graph(cache)
@@ -168,6 +176,8 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         t0 = time.time()
+        if g is None:
+            g = pm.rmat_graph(args.scale, args.p_gen, device=0)
         so = oracle.run(g.off, g.col, pattern_dir, None, max_iterations=args.max_iterations)
         oe = so["lcc_edges"] + so["nlcc_edges"] + so["tds_edges"]
         cpu = {"value": round(oe / so["seconds"], 1), "unit": "edges/s", "cores": 1, "kind": "port",

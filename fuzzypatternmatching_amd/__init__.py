@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _abi
 
-__all__ = ["Graph", "rmat_graph", "rmat_edges", "pattern_summary", "write_graph", "read_graph", "PatternMatcher",
+__all__ = ["Graph", "rmat_graph", "rmat_matcher", "mt19937_jump_outputs", "rmat_edges", "pattern_summary", "write_graph", "read_graph", "PatternMatcher",
            "ShardedPatternMatcher", "partition_edges", "comm_unique_id", "run_beta_local_shards", "PMError"]
 
 DEFAULT_HUB_THRESHOLD = 1048576  # generate_rmat.cpp:106
@@ -83,14 +83,29 @@ def _take_host_csr(off_p, col_p, n):
     return off, col
 
 
-def rmat_graph(scale, p_gen=1, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
-    """Symmetrized R-MAT graph of generate_rmat.cpp with P_gen generator ranks."""
+def rmat_graph(scale, p_gen=1, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD, device=None):
+    """Symmetrized R-MAT graph of generate_rmat.cpp with P_gen generator ranks.
+
+    device=None: host generator (one thread per generator rank); device=k: the GPU
+    generator on device k (MT19937 jump-ahead substreams, same graph bit for bit)."""
     lib = _lib()
     off_p, col_p, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
-    if lib.pm_rmat_csr(scale, p_gen, ctypes.byref(off_p), ctypes.byref(col_p), ctypes.byref(n)) != 0:
+    if device is None:
+        rc = lib.pm_rmat_csr(scale, p_gen, ctypes.byref(off_p), ctypes.byref(col_p), ctypes.byref(n))
+    else:
+        rc = lib.pm_rmat_csr_gpu(scale, p_gen, device, ctypes.byref(off_p), ctypes.byref(col_p), ctypes.byref(n))
+    if rc != 0:
         raise _err()
     off, col = _take_host_csr(off_p, col_p, n.value)
     return Graph(off, col, True, nranks, hub_threshold)
+
+
+def mt19937_jump_outputs(seed, skip, count):
+    """Outputs skip .. skip+count-1 of std::mt19937(seed) by one GF(2) jump (host check)."""
+    out = np.zeros(max(count, 1), np.uint32)
+    if _lib().pm_mt19937_jump_outputs(seed, skip, out.ctypes.data, count) != 0:
+        raise _err()
+    return out[:count]
 
 
 def rmat_edges(scale, p_gen, first=0, stride=1):
@@ -274,6 +289,32 @@ class PatternMatcher:
         nbrs = np.zeros(max(ne.value, 1), np.uint32)
         self._check(_lib().pm_export_state(self._ctx, None, None, nbrs.ctypes.data, ctypes.byref(ne)))
         return tpub, mdeg, nbrs[: ne.value]
+
+
+class _DeviceGraph:
+    """Size of a graph that lives only in HBM (pm_create_rmat)."""
+
+    def __init__(self, n, nnz, nranks, hub_threshold):
+        self.n, self._nnz, self.nranks, self.hub_threshold = int(n), int(nnz), nranks, hub_threshold
+        self.symmetric = True
+
+    @property
+    def nnz(self):
+        return self._nnz
+
+
+def rmat_matcher(scale, p_gen, pattern_dir, device=0, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """PatternMatcher over an R-MAT graph generated on the device (the adjacency never
+    visits the host).  Returns (matcher, generation seconds)."""
+    secs = ctypes.c_double()
+    ctx = _lib().pm_create_rmat(scale, p_gen, pattern_dir.encode(), device, nranks, hub_threshold,
+                                ctypes.byref(secs))
+    if not ctx:
+        raise _err()
+    m = PatternMatcher.__new__(PatternMatcher)
+    m._ctx = ctx
+    m.graph = _DeviceGraph(1 << scale, (1 << scale) * 32, nranks, hub_threshold)
+    return m, secs.value
 
 
 class ShardedPatternMatcher(PatternMatcher):

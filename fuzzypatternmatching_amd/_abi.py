@@ -111,6 +111,10 @@ SIGNATURES = [
                                                 c_char_p, c_u64, ctypes.POINTER(RunStats)]),
     ("pm_rmat_edges", ctypes.c_int, [c_u64, c_u64, c_u64, c_u64, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                      ctypes.POINTER(c_u64)]),
+    ("pm_rmat_csr_gpu", ctypes.c_int, [c_u64, c_u64, ctypes.c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                                       ctypes.POINTER(c_u64)]),
+    ("pm_create_rmat", c_vp, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u64, ctypes.POINTER(ctypes.c_double)]),
+    ("pm_mt19937_jump_outputs", ctypes.c_int, [c_u32, c_u64, c_vp, c_u64]),
 ]
 
 _lib = None

@@ -25,7 +25,9 @@
 
 #include "../../include/pm_abi.h"
 #include "host/graph_store.hpp"
+#include "host/mt_jump.hpp"
 #include "pm_internal.hpp"
+#include "pm_rmat.hpp"
 #include "pm_shard.hpp"
 #include <thread>
 
@@ -78,6 +80,7 @@ struct CtxInput {
   uint64_t hub_threshold = 1048576;
   uint32_t nshards = 1, shard = 0;
   Comm* comm = nullptr;            // ownership passes to the context
+  bool col_on_device = false;      // col is device memory (GPU-built graph); off stays host
 };
 
 static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int device) {
@@ -170,7 +173,9 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
   // default labels = degree labels; the id-major adjacency is staged in the
   // M column buffer and permuted into the label-major d_colp
-  if (c->nnz) PM_HIP_CHECK(hipMemcpy(c->d_mcol, in.col, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (c->nnz)
+    PM_HIP_CHECK(hipMemcpy(c->d_mcol, in.col, c->nnz * sizeof(uint32_t),
+                           in.col_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
   launch_degree_labels(*c);
   c->labels_host.assign(c->n, 0);
   for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(c->deg_host[v]);
@@ -1086,6 +1091,96 @@ int pm_rmat_csr(uint64_t scale, uint64_t p_gen, uint64_t** off, uint32_t** col, 
     *col = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, g.col.size()) * sizeof(uint32_t)));
     std::memcpy(*off, g.off.data(), g.off.size() * sizeof(uint64_t));
     std::memcpy(*col, g.col.data(), g.col.size() * sizeof(uint32_t));
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+// GPU generator (pm_rmat.hip): the same CSR as pm_rmat_csr, built on `device`.
+int pm_rmat_csr_gpu(uint64_t scale, uint64_t p_gen, int device, uint64_t** off, uint32_t** col, uint64_t* n) {
+  hipStream_t s = nullptr;
+  pm::DevCsr g;
+  try {
+    pm::require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g = pm::rmat_csr_device(scale, p_gen, s);
+    uint64_t* o = static_cast<uint64_t*>(std::malloc((g.n + 1) * sizeof(uint64_t)));
+    uint32_t* c = static_cast<uint32_t*>(std::malloc(std::max<uint64_t>(1, g.nnz) * sizeof(uint32_t)));
+    if (!o || !c) {
+      std::free(o);
+      std::free(c);
+      throw std::runtime_error("pm_rmat_csr_gpu: out of host memory");
+    }
+    PM_HIP_CHECK(hipMemcpy(o, g.d_off, (g.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (g.nnz) PM_HIP_CHECK(hipMemcpy(c, g.d_col, g.nnz * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *off = o;
+    *col = c;
+    *n = g.n;
+    (void)hipFree(g.d_off);
+    (void)hipFree(g.d_col);
+    (void)hipStreamDestroy(s);
+    return 0;
+  } catch (const std::exception& e) {
+    if (g.d_off) (void)hipFree(g.d_off);
+    if (g.d_col) (void)hipFree(g.d_col);
+    if (s) (void)hipStreamDestroy(s);
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+// Context over an R-MAT graph generated on the device itself (no host copy of
+// the adjacency): the north_star S=28 one-GPU configuration.
+pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nranks,
+                       uint64_t hub_threshold, double* gen_seconds) {
+  hipStream_t s = nullptr;
+  pm::DevCsr g;
+  try {
+    pm::require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const auto t0 = std::chrono::steady_clock::now();
+    g = pm::rmat_csr_device(scale, p_gen, s);
+    if (gen_seconds) *gen_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<uint64_t> off(g.n + 1);
+    PM_HIP_CHECK(hipMemcpy(off.data(), g.d_off, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    (void)hipFree(g.d_off);
+    g.d_off = nullptr;
+    pm::CtxInput in;
+    in.n = g.n;
+    in.off = off.data();
+    in.col = g.d_col;
+    in.col_on_device = true;
+    in.symmetric = true;
+    in.nranks = nranks;
+    in.hub_threshold = hub_threshold;
+    pm_ctx* c = pm::create_ctx(in, pattern_dir, device);
+    (void)hipFree(g.d_col);
+    (void)hipStreamDestroy(s);
+    return c;
+  } catch (const std::exception& e) {
+    if (g.d_off) (void)hipFree(g.d_off);
+    if (g.d_col) (void)hipFree(g.d_col);
+    if (s) (void)hipStreamDestroy(s);
+    pm::g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+// Host check of the MT19937 jump-ahead machinery (host/mt_jump.hpp): the
+// first `count` outputs of std::mt19937(seed) after skipping `skip` outputs,
+// obtained by one polynomial jump instead of stepping.
+int pm_mt19937_jump_outputs(uint32_t seed, uint64_t skip, uint32_t* out, uint64_t count) {
+  try {
+    uint32_t w[pm::mtj::kN], wj[pm::mtj::kN];
+    pm::mtj::seed_window(seed, w);
+    pm::mtj::apply(pm::mtj::jump_poly(skip), w, wj);
+    std::vector<uint32_t> seq(pm::mtj::kN + count);
+    pm::mtj::extend(wj, seq.data(), seq.size());
+    for (uint64_t i = 0; i < count; ++i) out[i] = pm::mtj::temper(seq[pm::mtj::kN + i]);
     return 0;
   } catch (const std::exception& e) {
     pm::g_last_error = e.what();

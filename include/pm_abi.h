@@ -33,6 +33,11 @@
  *                                 MPI_COMM_WORLD set up by havoqgt_init, environment.hpp:136-228)
  *   pm_rmat_edges                 the edge stream of some generator ranks of generate_rmat
  *                                 (src/generate_rmat.cpp:202-213, rmat_edge_generator.hpp:218-261)
+ *   pm_rmat_csr_gpu               generate_rmat's graph construction (generate_rmat.cpp:196-213 ->
+ *                                 delegate_partitioned_graph ctor, ipp:70-167, CSR fill ipp:818-969)
+ *                                 built on the GPU: MT19937 jump-ahead substreams + radix-sorted CSR
+ *   pm_create_rmat                generate_rmat + graph open (beta.cpp:209-223) in one step with the
+ *                                 adjacency never leaving HBM (north_star scale-28 configuration)
  *
  * Conventions: plain C types; int status (0 = OK, negative = error with
  * pm_last_error()); device memory is owned by the context; host buffers are
@@ -157,6 +162,15 @@ int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t strid
                   uint64_t* m);
 int pm_rmat_csr(uint64_t scale, uint64_t p_gen, uint64_t** off, uint32_t** col, uint64_t* n);
 void pm_free_host(void* p);
+
+/* GPU generator: bit-identical to pm_rmat_csr (same stream, same sorted CSR), built on `device`. */
+int pm_rmat_csr_gpu(uint64_t scale, uint64_t p_gen, int device, uint64_t** off, uint32_t** col, uint64_t* n);
+/* Context over a GPU-generated R-MAT graph (degree labels, no host copy of the adjacency).
+ * gen_seconds (may be NULL) receives the generation + CSR build wall time. */
+pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nranks,
+                       uint64_t hub_threshold, double* gen_seconds);
+/* Host check of the MT19937 jump-ahead (no device): outputs skip .. skip+count-1 of mt19937(seed). */
+int pm_mt19937_jump_outputs(uint32_t seed, uint64_t skip, uint32_t* out, uint64_t count);
 int pm_write_graph(const char* base, uint64_t n, const uint64_t* off, const uint32_t* col, int symmetric,
                    uint32_t nranks, uint64_t hub_threshold);
 int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n, int* symmetric,

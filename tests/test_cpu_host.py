@@ -101,3 +101,12 @@ def test_graph_file_roundtrip_rmat(tmp_path):
     np.testing.assert_array_equal(h.off, g.off)
     np.testing.assert_array_equal(h.col, g.col)
     assert h.nranks == 3 and h.symmetric
+
+
+def test_mt19937_jump_ahead_matches_stepping():
+    # host/mt_jump.hpp: one GF(2) polynomial jump == stepping the engine (oracle's own MT19937)
+    import oracle
+    assert pm.mt19937_jump_outputs(5489, 9999, 1)[0] == 4123659995  # the standard's known answer
+    for seed, skip in [(5492, 123457), (7, 624), (11, 623), (13, 0), (5489 + 21, 5 * 28 * 4096 + 3)]:
+        got = list(pm.mt19937_jump_outputs(seed, skip, 3))
+        assert got == [oracle.mt19937_nth(seed, skip + i + 1) for i in range(3)]
