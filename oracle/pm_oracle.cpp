@@ -46,6 +46,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -314,8 +315,11 @@ struct VState {
 class Engine {
  public:
   Engine(uint64_t n, const uint64_t* off, const uint32_t* col, const uint64_t* labels, const Pattern& p,
-         uint32_t nranks, uint64_t hub_threshold)
+         uint32_t nranks, uint64_t hub_threshold, unsigned threads = 1)
       : n_(n), off_(off), col_(col), p_(p), nranks_(nranks ? nranks : 1) {
+    T_ = threads ? threads : 1;
+    blk_ = std::max<uint64_t>(1, (n + T_ - 1) / T_);
+    S_.resize(T_);
     label_.resize(n);
     for (uint64_t v = 0; v < n; ++v) {
       if (labels) {
@@ -361,124 +365,184 @@ class Engine {
   }
 
   // ---- one LCC call (label_propagation_pattern_matching_bsp :1033-1153)
+  //
+  // Run by T_ worker threads, each the "rank" of a contiguous block of
+  // vertex ids (the reference's MPI ranks own id % P; LCC results do not
+  // depend on the partition).  A superstep is the BSP of the
+  // reference: senders fill per-(sender, receiver) mailboxes, receivers drain
+  // the boxes addressed to them, then every rank verifies its own state map.
+  // Each vertex's state (active_, tpub_, M_, its S_ entry) is touched only by
+  // its owner thread.  T_ = 1 is the original sequential order exactly.
+  struct Msg {
+    uint64_t dst, src;
+    BitSet t;
+  };
+
   void lcc(bool init_step, bool& not_finished, uint64_t itr) {
     stats_.lcc_calls++;
+    const unsigned T = T_;
     for (uint64_t ss = 0; ss < p_.diameter; ++ss) {
       stats_.supersteps++;
       const bool first = (ss == 0 && init_step);
       auto t0 = std::chrono::steady_clock::now();
-      struct Msg {
-        uint64_t dst, src;
-        BitSet t;
-      };
-      std::vector<Msg> msgs;
+      std::vector<std::vector<std::vector<Msg>>> box(T, std::vector<std::vector<Msg>>(T));
+      std::vector<uint64_t> trav(T, 0);
       // senders: lppm_visitor::visit (:468-636), one visit per vertex
-      for (uint64_t v = 0; v < n_; ++v) {
-        if (!active_[v]) continue;
-        if (first) {
-          BitSet tl = label_match(v);
-          if (tl.none()) {
-            active_[v] = 0;
-            continue;
+      parallel([&](unsigned r) {
+        auto& out = box[r];
+        for (uint64_t v = lo(r); v < lo(r + 1); ++v) {
+          if (!active_[v]) continue;
+          if (first) {
+            BitSet tl = label_match(v);
+            if (tl.none()) {
+              active_[v] = 0;
+              continue;
+            }
+            tpub_[v] = (uint16_t)tl.to_ulong();
+            for (uint64_t e = off_[v]; e < off_[v + 1]; ++e) out[tid_of(col_[e])].push_back({col_[e], v, tl});
+            trav[r] += off_[v + 1] - off_[v];
+          } else {
+            if (S_[r].find(v) == S_[r].end()) continue;
+            BitSet tv(tpub_[v]);
+            if (tv.none()) continue;
+            for (auto& it : M_[v]) out[tid_of(it.first)].push_back({it.first, v, tv});
+            trav[r] += M_[v].size();
           }
-          tpub_[v] = (uint16_t)tl.to_ulong();
-          for (uint64_t e = off_[v]; e < off_[v + 1]; ++e) msgs.push_back({col_[e], v, tl});
-          stats_.lcc_edges += off_[v + 1] - off_[v];
-        } else {
-          if (S_.find(v) == S_.end()) continue;
-          BitSet tv(tpub_[v]);
-          if (tv.none()) continue;
-          for (auto& it : M_[v]) msgs.push_back({it.first, v, tv});
-          stats_.lcc_edges += M_[v].size();
         }
+      });
+      uint64_t nmsgs = 0;
+      for (unsigned r = 0; r < T; ++r) {
+        stats_.lcc_edges += trav[r];
+        for (unsigned q = 0; q < T; ++q) nmsgs += box[r][q].size();
       }
       // receivers: lppm_visitor::pre_visit (:149-459)
-      for (const auto& m : msgs) {
-        const uint64_t u = m.dst;
-        if (!active_[u]) continue;
-        BitSet tu;
-        if (first) {
-          tu = label_match(u);
-          if (tu.none()) {
-            active_[u] = 0;
-            continue;
+      parallel([&](unsigned r) {
+        auto& Sr = S_[r];
+        for (unsigned q = 0; q < T; ++q) {
+          for (const auto& m : box[q][r]) {
+            const uint64_t u = m.dst;
+            if (!active_[u]) continue;
+            BitSet tu;
+            if (first) {
+              tu = label_match(u);
+              if (tu.none()) {
+                active_[u] = 0;
+                continue;
+              }
+              if (m.t.none()) continue;
+              tpub_[u] = (uint16_t)tu.to_ulong();
+            } else {
+              auto f = Sr.find(u);
+              if (f == Sr.end()) continue;
+              if (m.t.none()) continue;
+              tu = BitSet(tpub_[u]);
+              if (tu.none()) continue;
+            }
+            // member verify_and_update_vertex_state (:647-816)
+            if (!valid_parent(tu, m.t)) continue;
+            auto f = Sr.find(u);
+            if (f == Sr.end()) {
+              f = Sr.insert({u, VState()}).first;
+              f->second.tstate = tu;
+            }
+            f->second.tn |= m.t;
+            auto fe = M_[u].find(m.src);
+            if (fe == M_[u].end()) {
+              if (first) M_[u].insert({m.src, 1});
+              // else: "did not find the expected item" -- TN already updated (:775 vs :801)
+            } else {
+              fe->second = 1;
+            }
           }
-          if (m.t.none()) continue;
-          tpub_[u] = (uint16_t)tu.to_ulong();
-        } else {
-          auto f = S_.find(u);
-          if (f == S_.end()) continue;
-          if (m.t.none()) continue;
-          tu = BitSet(tpub_[u]);
-          if (tu.none()) continue;
+          std::vector<Msg>().swap(box[q][r]);  // drained
         }
-        // member verify_and_update_vertex_state (:647-816)
-        if (!valid_parent(tu, m.t)) continue;
-        auto f = S_.find(u);
-        if (f == S_.end()) {
-          f = S_.insert({u, VState()}).first;
-          f->second.tstate = tu;
-        }
-        f->second.tn |= m.t;
-        auto fe = M_[u].find(m.src);
-        if (fe == M_[u].end()) {
-          if (first) M_[u].insert({m.src, 1});
-          // else: "did not find the expected item" -- TN already updated (:775 vs :801)
-        } else {
-          fe->second = 1;
-        }
-      }
+      });
       // global verify_and_update_vertex_state (:829-1027)
-      if (first) {
-        for (uint64_t v = 0; v < n_; ++v)
-          if (active_[v] && S_.find(v) == S_.end()) {
+      std::vector<uint8_t> any_removed(T, 0);
+      parallel([&](unsigned r) {
+        auto& Sr = S_[r];
+        if (first) {
+          for (uint64_t v = lo(r); v < lo(r + 1); ++v)
+            if (active_[v] && Sr.find(v) == Sr.end()) {
+              active_[v] = 0;
+              M_[v].clear();
+            }
+        }
+        std::vector<uint64_t> removed;
+        for (auto& kv : Sr) {
+          const uint64_t v = kv.first;
+          VState& st = kv.second;
+          for (size_t t = 0; t < 16; ++t) {
+            if (!st.tstate.test(t)) continue;
+            BitSet pe(p_.adj(t));
+            BitSet x = pe & st.tn;
+            if (!(pe == x && !x.none())) st.tstate.reset(t);
+          }
+          if (st.tstate.none()) {
+            removed.push_back(v);
             active_[v] = 0;
             M_[v].clear();
-          }
-      }
-      std::vector<uint64_t> removed;
-      for (auto& kv : S_) {
-        const uint64_t v = kv.first;
-        VState& st = kv.second;
-        for (size_t t = 0; t < 16; ++t) {
-          if (!st.tstate.test(t)) continue;
-          BitSet pe(p_.adj(t));
-          BitSet x = pe & st.tn;
-          if (!(pe == x && !x.none())) st.tstate.reset(t);
-        }
-        if (st.tstate.none()) {
-          removed.push_back(v);
-          active_[v] = 0;
-          M_[v].clear();
-        } else {
-          tpub_[v] = (uint16_t)st.tstate.to_ulong();
-          st.tn.reset();
-          for (auto it = M_[v].begin(); it != M_[v].end();) {
-            if (!it->second) {
-              it = M_[v].erase(it);
-            } else {
-              it->second = 0;
-              ++it;
+          } else {
+            tpub_[v] = (uint16_t)st.tstate.to_ulong();
+            st.tn.reset();
+            for (auto it = M_[v].begin(); it != M_[v].end();) {
+              if (!it->second) {
+                it = M_[v].erase(it);
+              } else {
+                it->second = 0;
+                ++it;
+              }
             }
           }
         }
-      }
-      if (!removed.empty()) not_finished = true;
-      for (auto v : removed) S_.erase(v);
+        if (!removed.empty()) any_removed[r] = 1;
+        for (auto v : removed) Sr.erase(v);
+      });
+      for (unsigned r = 0; r < T; ++r)
+        if (any_removed[r]) not_finished = true;
       double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       // outputs (:1103-1145)
       superstep_lines_.push_back(std::to_string(itr) + ", LP, " + std::to_string(ss) + ", " + fmt(secs));
-      emit_counts(itr, "LP", ss, msgs.size());
+      emit_counts(itr, "LP", ss, nmsgs);
     }
+  }
+
+  // worker threads of the LCC: contiguous id blocks
+  uint64_t lo(unsigned r) const { return std::min<uint64_t>(n_, uint64_t(r) * blk_); }
+  unsigned tid_of(uint64_t v) const { return static_cast<unsigned>(v / blk_); }
+  template <typename F>
+  void parallel(F&& f) {
+    if (T_ == 1) {
+      f(0u);
+      return;
+    }
+    std::vector<std::thread> pool;
+    for (unsigned r = 0; r < T_; ++r) pool.emplace_back([&f, r] { f(r); });
+    for (auto& th : pool) th.join();
+  }
+  VState* s_find(uint64_t v) {
+    auto& Sr = S_[tid_of(v)];
+    auto f = Sr.find(v);
+    return f == Sr.end() ? nullptr : &f->second;
+  }
+  template <typename F>
+  void s_for_each(F&& f) {
+    for (auto& Sr : S_)
+      for (auto& kv : Sr) f(kv);
+  }
+  uint64_t s_size() const {
+    uint64_t k = 0;
+    for (auto& Sr : S_) k += Sr.size();
+    return k;
   }
 
   void emit_counts(uint64_t itr, const char* tag, uint64_t idx, uint64_t msgs) {
     std::vector<uint64_t> vc(nranks_, 0), ec(nranks_, 0);
-    for (auto& kv : S_) {
+    s_for_each([&](const std::pair<const uint64_t, VState>& kv) {
       uint32_t r = owner(kv.first);
       vc[r]++;
       ec[r] += M_[kv.first].size();
-    }
+    });
     for (uint32_t r = 0; r < nranks_; ++r) {
       std::string pre = std::to_string(itr) + ", " + tag + ", " + std::to_string(idx) + ", ";
       vcount_[r].push_back(pre + std::to_string(vc[r]));
@@ -761,7 +825,7 @@ class Engine {
             deleted = true;
           }
           for (auto& s : tsm)
-            if (!active_[s.first]) S_.erase(s.first);
+            if (!active_[s.first]) S_[tid_of(s.first)].erase(s.first);
           superstep_lines_.push_back(std::to_string(itr) + ", TP, " + std::to_string(pl) + ", " + fmt(since(tp0)));
           emit_counts(itr, "TP", pl, msgcount);
           if (deleted && l.IL) {
@@ -780,9 +844,9 @@ class Engine {
     stats_.iterations = itr;
     stats_.terminated = terminated ? 1 : 0;
     stats_.seconds = secs;
-    stats_.final_vertices = S_.size();
+    stats_.final_vertices = s_size();
     uint64_t fe = 0;
-    for (auto& kv : S_) fe += M_[kv.first].size();
+    s_for_each([&](const std::pair<const uint64_t, VState>& kv) { fe += M_[kv.first].size(); });
     stats_.final_edges = fe;
     if (!out.empty()) write_results(out, itr, secs, subgraphs);
   }
@@ -803,8 +867,9 @@ class Engine {
     wr(d + "/result_step", step_lines_);
     wr(d + "/result_superstep", superstep_lines_);
     std::vector<std::vector<std::string>> av(nranks_), ae(nranks_);
-    for (auto& kv : S_) {
-      const uint64_t v = kv.first;
+    std::vector<uint64_t> members;
+    s_for_each([&](const std::pair<const uint64_t, VState>& kv) { members.push_back(kv.first); });
+    for (const uint64_t v : members) {
       const uint32_t r = owner(v);
       av[r].push_back(std::to_string(r) + ", " + std::to_string(v) + ", 0, " + std::to_string(label_[v]) + ", " +
                       BitSet(tpub_[v]).to_string());
@@ -843,7 +908,9 @@ class Engine {
   std::vector<uint64_t> label_;
   std::vector<uint8_t> active_;
   std::vector<uint16_t> tpub_;
-  std::unordered_map<uint64_t, VState> S_;
+  unsigned T_ = 1;  // LCC worker threads
+  uint64_t blk_ = 1;
+  std::vector<std::unordered_map<uint64_t, VState>> S_;  // state map, one per worker (owner of the ids)
   std::vector<std::unordered_map<uint64_t, uint8_t>> M_;
   std::vector<std::unordered_set<uint64_t>> seen_;
   std::vector<std::vector<std::string>> vcount_, ecount_, mcount_;
@@ -859,12 +926,13 @@ typedef oracle::Stats oracle_stats_t;
 // Runs the whole driver loop on a CSR (rows may be in any order within a row).
 // labels == NULL selects degree labels.  result_dir == NULL or "" skips files.
 // Returns 0 on success, -1 on error (message on stderr).
-int oracle_run_csr(uint64_t n, const uint64_t* off, const uint32_t* col, const uint64_t* labels,
-                   const char* pattern_dir, const char* result_dir, uint32_t nranks, uint64_t hub_threshold,
-                   uint64_t max_iterations, oracle_stats_t* stats) {
+// threads: LCC worker threads (rank-partitioned BSP, identical results for any count).
+int oracle_run_csr_mt(uint64_t n, const uint64_t* off, const uint32_t* col, const uint64_t* labels,
+                      const char* pattern_dir, const char* result_dir, uint32_t nranks, uint64_t hub_threshold,
+                      uint64_t max_iterations, uint32_t threads, oracle_stats_t* stats) {
   try {
     oracle::Pattern p = oracle::load_pattern(pattern_dir);
-    oracle::Engine eng(n, off, col, labels, p, nranks, hub_threshold);
+    oracle::Engine eng(n, off, col, labels, p, nranks, hub_threshold, threads);
     eng.run(result_dir ? result_dir : "", max_iterations);
     if (stats) *stats = eng.stats_;
     return 0;
@@ -872,6 +940,13 @@ int oracle_run_csr(uint64_t n, const uint64_t* off, const uint32_t* col, const u
     std::cerr << "oracle error: " << e.what() << std::endl;
     return -1;
   }
+}
+
+int oracle_run_csr(uint64_t n, const uint64_t* off, const uint32_t* col, const uint64_t* labels,
+                   const char* pattern_dir, const char* result_dir, uint32_t nranks, uint64_t hub_threshold,
+                   uint64_t max_iterations, oracle_stats_t* stats) {
+  return oracle_run_csr_mt(n, off, col, labels, pattern_dir, result_dir, nranks, hub_threshold, max_iterations, 1,
+                           stats);
 }
 
 uint64_t oracle_hash_nbits(uint64_t x, int n) { return oracle::hash_nbits(x, n); }
