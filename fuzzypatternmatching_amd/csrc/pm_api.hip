@@ -1259,6 +1259,25 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
   });
 }
 
+// Diagnostics: superstep-0 tiling of the current labels: out[0] real adjacency
+// entries of the scanned runs, [1] slots loaded (padding included), [2]
+// scanned rows, [3] tiles, [4] ranges, [5] heavy rows.
+int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n) {
+  PM_API_BODY(ctx, {
+    uint64_t st[6] = {0, 0, 0, ctx->ntiles, ctx->ktab.empty() ? 0 : ctx->ktab.size() - 1, ctx->nheavy};
+    std::vector<uint64_t> offp(ctx->n + 1), offr(ctx->n + 1);
+    PM_HIP_CHECK(hipMemcpy(offp.data(), ctx->d_offp, offp.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    PM_HIP_CHECK(hipMemcpy(offr.data(), ctx->d_offr, offr.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i + 1 < ctx->ktab.size(); ++i) {
+      const pm::KRange& R = ctx->ktab[i];
+      st[0] += offr[R.end] - offr[R.start];
+      st[1] += offp[R.end] - offp[R.start];
+      st[2] += R.end - R.start;
+    }
+    for (uint64_t i = 0; i < n && i < 6; ++i) out[i] = st[i];
+  });
+}
+
 int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen) {
   try {
     const pm::Pattern p = pm::load_pattern_dir(pattern_dir);

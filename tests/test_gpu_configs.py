@@ -1,0 +1,110 @@
+"""GPU parity at the BASELINE.json configurations (SURVEY.md 8(d) C2, C3, C5;
+C4 on one GPU behind PM_BIG=1): every result file of the HIP path compared with
+the oracle (run on all host threads) on the same R-MAT input.
+
+C2: S=24, P_gen=4, tree, degree labels, 1 and 4 ranks of output attribution.
+C3: S=26, P_gen=4, 4-cycle pattern (NLCC token-passing stress).
+C5: ingested text edge list (-u 1) + explicit -v label files (hash32(v) % 64)
+    through the CLIs at S=18 (text size), and hash labels through the library at
+    S=22.
+C4': S=28, P_gen=8, tree on ONE GPU (PM_BIG=1: ~100 GB of host memory for the
+    oracle; the 8-GPU sharding of C4 is covered by tests/test_gpu_shards.py).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import fuzzypatternmatching_amd as pm
+import oracle
+import pmtest
+
+pytestmark = pytest.mark.gpu
+
+TREE = os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern")
+CYCLE = os.path.join(pmtest.ROOT, "patterns", "rmat_log2_cycle4_pattern")
+BIN = os.path.join(pmtest.ROOT, "fuzzypatternmatching_amd", "csrc", "tools", "bin")
+
+_graphs = {}
+
+
+def _graph(scale, p_gen):
+    # GPU generator (bit-identical to the host stream, tests/test_gpu_rmat.py), one copy per session
+    key = (scale, p_gen)
+    if key not in _graphs:
+        _graphs.clear()
+        _graphs[key] = pm.rmat_graph(scale, p_gen, device=0)
+    return _graphs[key]
+
+
+def _check(g, pattern, tmp_path, labels=None, nranks=1, tag=""):
+    a, b = tmp_path / f"oracle{tag}", tmp_path / f"gpu{tag}"
+    so = oracle.run(g.off, g.col, pattern, str(a), labels=labels, nranks=nranks, threads=oracle.default_threads())
+    m = pm.PatternMatcher(pm.Graph(g.off, g.col, True, nranks), pattern, labels=labels)
+    sg = m.run_beta(str(b))
+    m.close()
+    diffs = pmtest.compare_result_dirs(str(a), str(b), nranks)
+    assert diffs == [], diffs[:5]
+    for k_g, k_o in (("iterations", "iterations"), ("terminated", "terminated"), ("final_vertices", "final_vertices"),
+                     ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"),
+                     ("tds_edges", "tds_edges"), ("walks", "paths")):
+        assert sg[k_g] == so[k_o], (k_g, sg[k_g], so[k_o])
+    return sg
+
+
+@pytest.mark.parametrize("nranks", [1, 4])
+def test_c2_s24_tree(nranks, tmp_path):
+    sg = _check(_graph(24, 4), TREE, tmp_path, nranks=nranks)
+    assert sg["lcc_edges"] > 10 ** 8  # superstep 0 scans every label-matching row
+
+
+def test_c3_s26_cycle4(tmp_path):
+    sg = _check(_graph(26, 4), CYCLE, tmp_path)
+    assert sg["nlcc_edges"] + sg["tds_edges"] > 0
+
+
+def test_c5_s22_hash_labels(tmp_path):
+    g = _graph(22, 4)
+    # alphabet 64: with 8 labels the 4-cycle walks through R-MAT hubs explode
+    # (S=14 already enumerates 1.2 M walks, S=16 runs for minutes on the oracle)
+    labels = pmtest.hash_labels(g.n, 64)
+    sg = _check(g, CYCLE, tmp_path, labels=labels, nranks=2)
+    assert sg["walks"] > 0
+
+
+def test_c5_ingested_edge_list_with_label_files(tmp_path):
+    """generate -> text edge list -> ingest_edge_list -u 1 -> -v label files -> run_pattern_matching_beta."""
+    scale, p_gen, nranks = 18, 4, 4
+    und = [oracle.rmat_rank_edges(scale, p_gen, r) for r in range(p_gen)]
+    u = np.concatenate([x[0] for x in und])
+    v = np.concatenate([x[1] for x in und])
+    txt = tmp_path / "edges.txt"
+    np.savetxt(txt, np.stack([u, v], 1), fmt="%d")
+    base = str(tmp_path / "ing")
+    r = subprocess.run([os.path.join(BIN, "ingest_edge_list"), "-o", base, "-u", "1", "-n", str(nranks), str(txt)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    g = pm.read_graph(base)
+    assert g.symmetric
+    # the ingested graph is the R-MAT graph (ids up to the max id seen)
+    h = _graph(scale, p_gen)
+    assert np.array_equal(g.col, h.col) and np.array_equal(g.off, h.off[: g.n + 1])
+    labels = pmtest.hash_labels(g.n, 64, salt=5)
+    for i, part in enumerate(np.array_split(np.arange(g.n), 3)):
+        with open(tmp_path / f"lab.{i}", "w") as f:
+            f.write("".join(f"{x} {labels[x]}\n" for x in part))
+    out = tmp_path / "gpu"
+    out.mkdir()
+    r = subprocess.run([os.path.join(BIN, "run_pattern_matching_beta"), "-i", base, "-v", str(tmp_path / "lab"),
+                        "-p", CYCLE, "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    ora = tmp_path / "oracle"
+    oracle.run(g.off, g.col, CYCLE, str(ora), labels=labels, nranks=nranks, threads=oracle.default_threads())
+    assert pmtest.compare_result_dirs(str(ora), str(out), nranks) == []
+
+
+@pytest.mark.skipif(os.environ.get("PM_BIG") != "1", reason="PM_BIG=1: S=28 one-GPU parity (~100 GB host memory)")
+def test_c4_s28_tree_one_gpu(tmp_path):
+    sg = _check(_graph(28, 8), TREE, tmp_path)
+    print(f"S=28 parity: {sg}")

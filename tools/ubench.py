@@ -1,6 +1,9 @@
-"""Superstep-0 kernel timing at several grid sizes (one process, interleaved rounds).
+"""Superstep-0 kernel timing: diagnostic variants / grid sizes (one process, interleaved rounds).
 
-usage: ubench.py SCALE [grid,grid,...]   (grid 0 = the library default)
+usage: ubench.py SCALE [P_GEN] [variant,variant,...]
+  variant < 16: diagnostic MODE (pm_kernels.hip k_lcc_first: 0 product, 1 no M stores,
+  8 loads + label test only, 2 skip G <= 64 tiles, 4 skip G >= 128 tiles); >= 16: product
+  kernel on a grid of that many blocks.  The graph is generated on the GPU.
 """
 import ctypes
 import os
@@ -12,10 +15,16 @@ import fuzzypatternmatching_amd as pm  # noqa: E402
 from fuzzypatternmatching_amd import _abi  # noqa: E402
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 22
-variants = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 8, 2, 4, 10, 12]
-g = pm.rmat_graph(scale, 4)
-m = pm.PatternMatcher(g, os.path.join(ROOT, "patterns", "rmat_log2_tree_pattern"))
+p_gen = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+variants = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 8, 2, 4]
+m, _ = pm.rmat_matcher(scale, p_gen, os.path.join(ROOT, "patterns", "rmat_log2_tree_pattern"))
 lib = _abi.load()
+st = (ctypes.c_uint64 * 6)()
+if lib.pm_debug_layout_stats(m._ctx, st, 6) != 0:
+    raise RuntimeError(lib.pm_last_error(m._ctx))
+real, slots, rows, tiles, ranges, heavy = list(st)
+print(f"S={scale} P_gen={p_gen}: scanned rows {rows}, real entries {real}, loaded slots {slots} "
+      f"(padding ratio {slots / max(real, 1):.3f}), tiles {tiles}, ranges {ranges}, heavy rows {heavy}", flush=True)
 res = {v: [] for v in variants}
 for rnd in range(5):
     for v in variants:
@@ -23,12 +32,14 @@ for rnd in range(5):
         if lib.pm_debug_time_lcc_first(m._ctx, v, 5, ctypes.byref(ms)) != 0:
             raise RuntimeError(lib.pm_last_error(m._ctx))
         res[v].append(ms.value)
-st = m.run_beta("", 64)
-nbytes = st["lcc_first_bytes"]
-print(f"S={scale}: superstep-0 algorithmic bytes {nbytes}, run_beta kernel {st['lcc_first_kernel_ms']:.4f} ms, "
-      f"step {st['seconds'] * 1e3:.3f} ms")
+s = m.run_beta("", 64)
+nbytes = s["lcc_first_bytes"]
+print(f"S={scale}: superstep-0 algorithmic bytes {nbytes}, run_beta kernel {s['lcc_first_kernel_ms']:.4f} ms, "
+      f"step {s['seconds'] * 1e3:.3f} ms, lcc edges {s['lcc_edges']}")
 for v in variants:
     xs = sorted(res[v])
     med = xs[len(xs) // 2]
     print(f"S={scale} variant {v:5d}: median {med*1e3:8.1f} us  min {xs[0]*1e3:8.1f} us  "
-          f"{nbytes / (med * 1e-3) / 1e9:8.1f} GB/s")
+          f"{nbytes / (med * 1e-3) / 1e9:8.1f} GB/s  real-entry read {real * 4 / (med * 1e-3) / 1e9:8.1f} GB/s  "
+          f"slot read {slots * 4 / (med * 1e-3) / 1e9:8.1f} GB/s", flush=True)
+m.close()
