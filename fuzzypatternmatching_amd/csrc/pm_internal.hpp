@@ -82,15 +82,16 @@ struct Arena {
 
 // Superstep-0 tiling of the padded label-major CSR (DESIGN.md "Data
 // layout"): one entry per (pattern label, degree class) run of rows.  kind
-// 0..10: rows of degree in (G/2, G], G = 1 << kind, stored in G padded slots,
-// so the run is a dense rows x G array and a tile is kTileEntries (G for
-// G > kTileEntries) consecutive slots; kind 11: rows above kHeavyDeg (stored
-// unpadded), one kHeavyDeg-entry segment per tile (HSeg list).
+// 0..kHeavyKind-1: rows of degree in (G/2, G], G = 1 << kind <= kHeavyDeg,
+// stored in G padded slots, so the run is a dense rows x G array and a tile
+// is kTileEntries consecutive slots holding 512 / G whole rows; kind
+// kHeavyKind: rows above kHeavyDeg (stored unpadded), one kHeavyDeg-entry
+// segment per tile (HSeg list).
 struct KRange {
   uint64_t qbase;       // first slot of the run
   uint32_t tile0;       // first tile of the run
   uint32_t start, end;  // row positions [start, end)
-  uint32_t aux;         // kind 11: first HSeg index
+  uint32_t aux;         // heavy kind: first HSeg index
   uint16_t tu, nm;      // template bits of the label and their neighbour mask
   uint32_t kind;
   // label runs whose template bits meet nm (the only neighbours that can
@@ -114,9 +115,9 @@ struct HSeg {
 };
 static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
 static constexpr uint32_t kTileEntries = 64 * kSub; // 512
-static constexpr uint32_t kHeavyDeg = 1024;
-static constexpr int kHeavyKind = 11;
-static constexpr int kMaxRanges = 16 * 12 + 1;
+static constexpr uint32_t kHeavyDeg = kTileEntries; // light rows fit in one tile
+static constexpr int kHeavyKind = 10;               // log2(kHeavyDeg) + 1
+static constexpr int kMaxRanges = 16 * (kHeavyKind + 1) + 1;
 // Active-edge map entries: neighbour position | kAlive | kFlag (cycle mark,
 // nem_1.hpp:764-770).  Positions use 30 bits (V < 2^30).
 static constexpr uint32_t kAlive = 1u << 31;

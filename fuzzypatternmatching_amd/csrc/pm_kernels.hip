@@ -280,86 +280,215 @@ __device__ __forceinline__ void k1_slice(uint32_t v, uint16_t tv, uint32_t j, ui
   if (cm) tnacc |= tv;
 }
 
-// Uniform parameters of the tile being processed.
-struct K1Tile {
-  uint64_t qbase, t0;
-  uint32_t start, nrows;
-  uint16_t tu, nm;
+// Uniform description of one superstep-0 tile, resolved from the KRange table.
+struct K1Desc {
+  uint64_t qbase;  // first slot of the run
+  uint32_t start;  // first row position of the run
+  uint32_t nrows;  // rows of the run
+  uint32_t rel;    // tile index inside the run
+  uint32_t kind;   // log2 G (light) or kHeavyKind
+  uint32_t r;      // KRange index
 };
 
-// G <= 64 slots per row, G = 1 << LG lanes per row, 64/G rows per sub-tile.
-// Compile-time G: the per-row OR reaches the row's first lane through DPP
-// row shifts (+ two cross-row shuffles for G = 32, 64), M positions and
-// counts come from one ballot per sub-tile.  The row verify runs after the
-// kSub sub-tiles, one row per lane (TN and count staged in LDS), so its
-// branches and state stores use full waves; survivor bit r of the tile
-// mask = row r of the tile.
-template <int LG, int MODE, bool WIDE>
-__device__ __forceinline__ void k1_light(uint32_t (&v)[kSub], const K1Tile& T, const RelRuns& rel_runs,
-                                         const uint32_t* s_runs, int nruns, const KeepArgs& keep,
-                                         const uint16_t* s_adj, const OwnerArgs& oa, const K1Out& o, BlockAcc& acc,
-                                         unsigned long long* s_hist, unsigned long long* tm, uint32_t* s_rows) {
-  constexpr int G = 1 << LG;
-  constexpr uint64_t gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
-  constexpr uint32_t R = kTileEntries >> LG;  // rows per tile
+// Advances the wave's range cursor r to the range holding tile t (tiles are
+// visited in increasing order by each wave) and returns the tile's description.
+__device__ __forceinline__ K1Desc k1_desc(const KRange* s_tab, uint32_t& r, uint32_t t) {
+  while (__builtin_amdgcn_readfirstlane(s_tab[r + 1].tile0) <= t) ++r;
+  K1Desc d;
+  d.r = r;
+  d.kind = __builtin_amdgcn_readfirstlane(s_tab[r].kind);
+  d.start = __builtin_amdgcn_readfirstlane(s_tab[r].start);
+  d.nrows = __builtin_amdgcn_readfirstlane(s_tab[r].end) - d.start;
+  d.rel = t - __builtin_amdgcn_readfirstlane(s_tab[r].tile0);
+  d.qbase = (uint64_t(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase >> 32))) << 32) |
+            __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase));
+  return d;
+}
+
+// The kSub x 64 slots of a light tile (kNone past the run): one load per
+// lane and sub-tile, all issued before any use.  The loads are unconditional
+// (a clamped in-bounds address, the value replaced afterwards; a heavy tile or
+// a tile past the end loads slot 0): a fixed count of loads per tile lets the
+// compiler wait for exactly the oldest tile's loads (vmcnt(16)) instead of
+// draining the counter.
+__device__ __forceinline__ void k1_load(uint32_t (&v)[kSub], const K1Desc& d, const uint32_t* __restrict__ colp,
+                                        bool valid) {
   const int lane = lane_id();
-  const int k = lane & (G - 1);
-  const int lead = lane & ~(G - 1);
-#pragma unroll 1
-  for (int q = 0; q < kSub; ++q) {
-    // rolled loop: the slice in use rotates into v[0] (no dynamic register indexing)
-    const uint32_t vq = v[0];
+  const uint64_t t0 = uint64_t(d.rel) * kTileEntries;
+  const uint64_t tend = valid && d.kind < static_cast<uint32_t>(kHeavyKind) ? uint64_t(d.nrows) << d.kind : 0;
+  const uint64_t base = tend ? d.qbase : 0;
+  const uint64_t last = tend ? tend - 1 : 0;
 #pragma unroll
-    for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
-    const uint16_t tv = vq != kNone ? tbits_rel<WIDE>(vq, rel_runs, s_runs, nruns) : uint16_t(0);
-    const uint32_t pv = dpp_wave_shr1(vq);
-    const bool ok = vq != kNone;
-    const bool first = ok && (k == 0 || pv != vq);
-    const bool cm = ok && (tv & T.nm) != 0;
-    const bool contrib = cm && first;
-    const uint64_t bal = __ballot(contrib);
-    const uint64_t gb = (bal >> lead) & gmask;  // this row's contribution bits
-    const uint32_t rt = static_cast<uint32_t>((q * kWave + lane) >> LG);  // row inside the tile
-    if (contrib && !(MODE & 1)) {
-      const uint64_t dst = T.qbase + ((T.t0 >> LG) + rt) * G + __builtin_popcountll(gb & ((1ull << k) - 1));
-      o.mcol[dst] = vq | kAlive;
-    }
-    uint32_t x = cm ? tv : 0u;
-    if (G >= 2) x |= dpp_row_shl<1>(x);
-    if (G >= 4) x |= dpp_row_shl<2>(x);
-    if (G >= 8) x |= dpp_row_shl<4>(x);
-    if (G >= 16) x |= dpp_row_shl<8>(x);
-    if (G >= 32) x |= __shfl_down(x, 16, kWave);
-    if (G >= 64) x |= __shfl_down(x, 32, kWave);
-    if (k == 0) s_rows[rt] = (x & T.nm) | (static_cast<uint32_t>(__builtin_popcountll(gb)) << 16);
+  for (int q = 0; q < kSub; ++q) {
+    const uint64_t s = t0 + q * kWave + lane;
+    v[q] = __builtin_nontemporal_load(colp + base + (s < tend ? s : last));
   }
-  __builtin_amdgcn_wave_barrier();
-  // verify, one row per lane
-  const uint32_t row0 = static_cast<uint32_t>(T.t0 >> LG);  // first row of the tile in the run
-#pragma unroll 1
-  for (uint32_t w0 = 0; w0 < static_cast<uint32_t>(kSub) * kWave; w0 += kWave) {
-    bool surv = false;
-    if (w0 < R) {
-      const uint32_t r = w0 + lane;
-      if (r < R && row0 + r < T.nrows) {
-        const uint32_t pk = s_rows[r];
-        const uint32_t c = pk >> 16;
-        surv = k1_finish_row(T.start + row0 + r, T.tu, static_cast<uint16_t>(pk & 0xFFFFu), c, c, s_adj, keep, oa,
-                             o, acc, s_hist);
+#pragma unroll
+  for (int q = 0; q < kSub; ++q)
+    if (t0 + q * kWave + lane >= tend) v[q] = kNone;
+}
+
+// Per-wave LDS staging of a light tile: per-row accumulators (TN | count << 16,
+// one word per row of the tile) and the tile's contributing entries in slot
+// order (neighbour position, slot), which become M rows once the verify has
+// decided which rows survive.
+struct K1Stage {
+  uint32_t acc[kTileEntries];
+  uint32_t lv[kTileEntries];
+  uint16_t ls[kTileEntries];
+  unsigned long long sm[kSub];  // survivor bits of the tile's rows
+};
+
+// Light tile (G = 1 << kind <= kTileEntries slots per row, 512 / G whole rows).
+// Phase A, per sub-tile: Tl(v) from the position (label runs), first
+// occurrence in the row from the left neighbour lane, one ballot; only the
+// few contributing lanes (a few percent of the slots) touch LDS: row OR /
+// count atomics and the staging list.  Phase B walks the staging list only.
+template <int MODE, bool WIDE>
+__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K1Desc& d, uint16_t tu, uint16_t nm,
+                                              const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
+                                              const KeepArgs& keep, const uint16_t* s_adj, const OwnerArgs& oa,
+                                              const K1Out& o, BlockAcc& acc, unsigned long long* s_hist,
+                                              unsigned long long* tm, K1Stage& st) {
+  const int lane = lane_id();
+  const uint32_t lg = d.kind;
+  const uint32_t gm = (1u << lg) - 1;
+  uint32_t nlist = 0;  // wave-uniform
+#pragma unroll
+  for (int q = 0; q < kSub; ++q) {
+    const uint32_t x = v[q];
+    const uint16_t tv = tbits_rel<WIDE>(x, rel_runs, s_runs, nruns);  // 0 for kNone (outside every run)
+    uint32_t pv = dpp_wave_shr1(x);
+    if (q > 0) {
+      const uint32_t carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[q - 1]), kWave - 1));
+      if (lane == 0) pv = carry;
+    }
+    const uint32_t j = q * kWave + lane;  // slot inside the tile
+    const uint32_t tn = tv & nm;
+    const bool contrib = tn != 0 && ((j & gm) == 0 || pv != x);
+    const uint64_t C = __ballot(contrib);
+    if (C) {
+      if (contrib) {
+        const uint32_t row = j >> lg;
+        atomicOr(&st.acc[row], tn);
+        atomicAdd(&st.acc[row], 1u << 16);
+        const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_popcountll(C & ((1ull << lane) - 1)));
+        st.lv[idx] = x;
+        st.ls[idx] = static_cast<uint16_t>(j);
       }
+      nlist += static_cast<uint32_t>(__builtin_popcountll(C));
     }
-    const uint64_t sm = __ballot(surv);
-    if (lane == 0 && !(MODE & 8)) tm[w0 / kWave] = sm;
   }
   __builtin_amdgcn_wave_barrier();
+  if (lane < kSub) st.sm[lane] = 0ull;
+  // phase B: one pass over the staging list (sorted by slot, so each row's
+  // entries are consecutive).  The first entry of a row (head) verifies it
+  // from its accumulator, complete after phase A; the row's entries learn the
+  // verdict from the head's ballot bit and, for a survivor, write M[u] in
+  // slot order.  Rows without a contribution never enter S.
+  const uint32_t row0 = d.rel * (kTileEntries >> lg);
+  uint32_t carry_head = 0, carry_row = kNone;
+  uint64_t carry_surv = 0;
+#pragma unroll 1
+  for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    const bool in = i < nlist;
+    const uint32_t j = in ? st.ls[i] : 0u;
+    const uint32_t x = in ? st.lv[i] : 0u;
+    const uint32_t row = in ? (j >> lg) : kNone;
+    uint32_t prow = dpp_wave_shr1(row);
+    if (lane == 0) prow = carry_row;
+    const bool head = in && row != prow;
+    bool surv = false;
+    if (head) {
+      const uint32_t pk = st.acc[row];
+      st.acc[row] = 0;
+      if (row0 + row < d.nrows)
+        surv = k1_finish_row(d.start + row0 + row, tu, static_cast<uint16_t>(pk & 0xFFFFu), pk >> 16, pk >> 16, s_adj,
+                             keep, oa, o, acc, s_hist);
+      if (surv) atomicOr(&st.sm[row >> 6], 1ull << (row & 63));
+    }
+    const uint64_t H = __ballot(head);
+    const uint64_t Sv = __ballot(surv);
+    const uint64_t hm = H & ((2ull << lane) - 1);  // heads at or below this lane
+    const uint32_t hl = hm ? 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(hm))) : 0u;
+    const uint32_t hidx = hm ? i0 + hl : carry_head;
+    const uint64_t mys = hm ? ((Sv >> hl) & 1ull) : carry_surv;
+    if (!(MODE & 1) && in && mys) o.mcol[d.qbase + (uint64_t(row0 + row) << lg) + (i - hidx)] = x | kAlive;
+    if (H) {
+      const uint32_t hlast = 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(H)));
+      carry_head = i0 + hlast;
+      carry_surv = (Sv >> hlast) & 1ull;
+    }
+    carry_row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), kWave - 1));
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < kSub) tm[lane] = st.sm[lane];  // survivor bit r = row r of the tile
+}
+
+// Heavy rows (above kHeavyDeg): one kHeavyDeg segment per tile, uncompacted M;
+// the segments' TN / counts meet in the hscr scratch and the last segment to
+// finish (ticket) runs the verify.  Rare: kept out of line.
+template <int MODE, bool WIDE>
+__device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t rix, uint32_t rel,
+                                                            const HSeg* __restrict__ hseg,
+                                                            const uint64_t* __restrict__ offp,
+                                                            const uint32_t* __restrict__ colp, const uint32_t* s_runs,
+                                                            int nruns, const uint16_t* s_adj, OwnerArgs oa, K1Out o,
+                                                            uint32_t* __restrict__ hscr, uint32_t nheavy,
+                                                            unsigned long long* s_hist, unsigned long long* tm) {
+  BlockAcc acc;
+  const int lane = lane_id();
+  const KRange& R = s_tab[rix];
+  const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.tu));
+  const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.nm));
+  const RelRuns rel_runs = load_rel(R);
+  const KeepArgs keep = load_keep(R);
+  const HSeg hs = hseg[__builtin_amdgcn_readfirstlane(R.aux) + rel];
+  const uint64_t b0 = offp[hs.row];
+  const uint32_t deg = static_cast<uint32_t>(offp[hs.row + 1] - b0);
+  const uint32_t j_beg = hs.seg * kHeavyDeg;
+  const uint32_t j_end = min(deg, j_beg + kHeavyDeg);
+  uint32_t cnt = 0, tnacc = 0;
+  uint32_t carry = j_beg ? colp[b0 + j_beg - 1] : kNone;
+  for (uint32_t j0 = j_beg; j0 < j_end; j0 += kSub * kWave) {
+    uint32_t v[kSub];
+#pragma unroll
+    for (int q = 0; q < kSub; ++q) {
+      const uint32_t j = j0 + q * kWave + lane;
+      v[q] = j < j_end ? colp[b0 + j] : kNone;
+    }
+#pragma unroll
+    for (int q = 0; q < kSub; ++q)
+      k1_slice<false, MODE>(v[q], tbits_rel<WIDE>(v[q], rel_runs, s_runs, nruns), j0 + q * kWave + lane, b0, nm, o,
+                            cnt, tnacc, carry);
+  }
+  const uint16_t TN = wave_or_bits(tnacc, nm, 0, ~0ull);
+  bool surv = false;
+  if (lane == 0 && !(MODE & 8)) {
+    uint32_t* h_tn = hscr;
+    uint32_t* h_cnt = hscr + nheavy;
+    uint32_t* h_done = hscr + 2 * nheavy;
+    if (TN) atomicOr(&h_tn[hs.h], static_cast<uint32_t>(TN));
+    if (cnt) atomicAdd(&h_cnt[hs.h], cnt);
+    __threadfence();
+    if (atomicAdd(&h_done[hs.h], 1u) == hs.nseg - 1) {
+      __threadfence();
+      const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
+      const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
+      surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
+    }
+  }
+  if (lane < kSub && !(MODE & 8)) tm[lane] = (lane == 0 && surv) ? 1ull : 0ull;
+  return acc;
 }
 
 // MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores,
-// bit1 skips G <= 64 tiles, bit2 skips G >= 128 tiles, bit3 drops every
-// store except a checksum of the loaded slots.  WIDE: some range has more
-// than four relevant label runs (tbits_rel scans them all).
+// bit1 skips light tiles, bit2 skips heavy tiles, bit3 keeps only the loads
+// and the label test (checksum).  WIDE: some range has more than four
+// relevant label runs (tbits_rel scans them all).
 template <int MODE, bool WIDE = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_lcc_first(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, unsigned long long* __restrict__ tmask,
@@ -369,7 +498,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
   __shared__ uint32_t s_runs[3 * 16];
-  __shared__ uint32_t s_rows[kWpb][kTileEntries];  // light tiles: TN | count << 16 per row
+  __shared__ K1Stage s_stage[kWpb];
   for (uint32_t i = threadIdx.x; i <= nr; i += blockDim.x) s_tab[i] = ktab[i];
   load_adj(s_adj, pa);
   if (threadIdx.x < 16) {
@@ -379,152 +508,53 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     s_runs[3 * l + 2] = lr.tu[l];
   }
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform
+  K1Stage& st = s_stage[wid];
+  for (int i = threadIdx.x % kWave; i < static_cast<int>(kTileEntries); i += kWave) st.acc[i] = 0;
   __syncthreads();
   BlockAcc acc;
   const int lane = lane_id();
   const uint32_t W = gridDim.x * kWpb;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform
   const int nruns = lr.n;
   uint32_t r = 0;
-  for (uint32_t t = blockIdx.x * kWpb + wid; t < ntiles; t += W) {
-    while (__builtin_amdgcn_readfirstlane(s_tab[r + 1].tile0) <= t) ++r;
-    const uint32_t kind = __builtin_amdgcn_readfirstlane(s_tab[r].kind);
-    const uint32_t start = __builtin_amdgcn_readfirstlane(s_tab[r].start);
-    const uint32_t nrows = __builtin_amdgcn_readfirstlane(s_tab[r].end) - start;
-    const uint32_t rel = t - __builtin_amdgcn_readfirstlane(s_tab[r].tile0);
-    const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(s_tab[r].tu));
-    const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(s_tab[r].nm));
-    const uint64_t qbase = (uint64_t(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase >> 32))) << 32) |
-                           __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase));
+  uint32_t t = blockIdx.x * kWpb + wid;
+  // the next tile's slots are in flight while the current one is processed
+  uint32_t vc[kSub], vn[kSub];
+  K1Desc cur{};
+  if (t < ntiles) cur = k1_desc(s_tab, r, t);
+  k1_load(vc, cur, colp, t < ntiles);
+  while (t < ntiles) {
+    const uint32_t tn = t + W;
+    K1Desc nxt{};
+    if (tn < ntiles) nxt = k1_desc(s_tab, r, tn);
+    k1_load(vn, nxt, colp, tn < ntiles);
+    const KRange& R = s_tab[cur.r];
     unsigned long long* tm = tmask + uint64_t(t) * kSub;
-    const RelRuns rel_runs = load_rel(s_tab[r]);
-    const KeepArgs keep = load_keep(s_tab[r]);
-    const uint32_t hseg_at = __builtin_amdgcn_readfirstlane(s_tab[r].aux);
-#define PM_TB(x) ((x) != kNone ? tbits_rel<WIDE>((x), rel_runs, s_runs, nruns) : uint16_t(0))
-    if (kind <= 6) {
-      if (MODE & 2) continue;
-      // ---- G <= 64: G lanes per row, 64/G rows per sub-tile
-      const int lg = static_cast<int>(kind);
-      const uint64_t t0 = uint64_t(rel) * kTileEntries;          // slot offset of the tile in the run
-      const uint64_t tend = uint64_t(nrows) << lg;              // slots of the run
-      uint32_t v[kSub];
-#pragma unroll
-      for (int q = 0; q < kSub; ++q) {
-        const uint64_t s = t0 + q * kWave + lane;
-        v[q] = s < tend ? colp[qbase + s] : kNone;
-      }
+    if (cur.kind < static_cast<uint32_t>(kHeavyKind)) {
+      const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.tu));
+      const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.nm));
+      const RelRuns rel_runs = load_rel(R);
       if (MODE & 8) {
 #pragma unroll
-        for (int q = 0; q < kSub; ++q) acc.vs += v[q] ^ PM_TB(v[q]);
-        continue;
+        for (int q = 0; q < kSub; ++q) acc.vs += vc[q] ^ tbits_rel<WIDE>(vc[q], rel_runs, s_runs, nruns);
+      } else if (!(MODE & 2)) {
+        const KeepArgs keep = load_keep(R);
+        k1_light_tile<MODE, WIDE>(vc, cur, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
       }
-      const K1Tile T{qbase, t0, start, nrows, tu, nm};
-#define PM_K1L(LG) \
-  k1_light<LG, MODE, WIDE>(v, T, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, s_rows[wid])
-      switch (lg) {
-        case 0: PM_K1L(0); break;
-        case 1: PM_K1L(1); break;
-        case 2: PM_K1L(2); break;
-        case 3: PM_K1L(3); break;
-        case 4: PM_K1L(4); break;
-        case 5: PM_K1L(5); break;
-        default: PM_K1L(6); break;
-      }
-#undef PM_K1L
-    } else if (kind <= 10) {
-      if (MODE & 4) continue;
-      // ---- G = 128..1024: consecutive 64-slot slices of one row at a time
-      const int lg = static_cast<int>(kind);
-      const uint32_t spr = 1u << (lg - 6);                       // slices per row
-      const uint32_t te = kTileEntries > (1u << lg) ? kTileEntries : (1u << lg);
-      const uint64_t t0 = uint64_t(rel) * te;
-      const uint64_t tend = uint64_t(nrows) << lg;
-      uint64_t smask = 0;
-      uint32_t cnt = 0, tnacc = 0, carry = kNone;
-      for (uint32_t b0 = 0; b0 < te / kWave; b0 += kSub) {
-        uint32_t v[kSub];
-#pragma unroll
-        for (int q = 0; q < kSub; ++q) {
-          const uint64_t s = t0 + (b0 + q) * kWave + lane;
-          v[q] = s < tend ? colp[qbase + s] : kNone;
-        }
-        if (MODE & 8) {
-#pragma unroll
-          for (int q = 0; q < kSub; ++q) acc.vs += v[q] ^ PM_TB(v[q]);
-          continue;
-        }
-#pragma unroll 1
-        for (int q = 0; q < kSub; ++q) {
-          const uint32_t vq = v[0];
-#pragma unroll
-          for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
-          const uint64_t s0 = t0 + (b0 + q) * kWave;             // first slot of the slice
-          const uint32_t rr = static_cast<uint32_t>(s0 >> lg);
-          const uint32_t sl = (b0 + q) & (spr - 1);
-          if (sl == 0) {
-            cnt = 0;
-            tnacc = 0;
-            carry = kNone;
-          }
-          k1_slice<true, MODE>(vq, PM_TB(vq), sl * kWave + lane, qbase + (uint64_t(rr) << lg), nm, o, cnt, tnacc,
-                               carry);
-          if (sl == spr - 1) {
-            const uint16_t TN = wave_or_bits(tnacc, nm, 0, ~0ull);
-            bool surv = false;
-            if (lane == 0 && rr < nrows) surv = k1_finish_row(start + rr, tu, TN, cnt, cnt, s_adj, keep, oa, o, acc, s_hist);
-            if (__ballot(surv)) smask |= 1ull << (rr - static_cast<uint32_t>(t0 >> lg));
-          }
-        }
-      }
-      if (lane < kSub && !(MODE & 8)) tm[lane] = lane == 0 ? smask : 0ull;
-    } else {
-      if (MODE & 4) continue;
-      // ---- heavy rows: one kHeavyDeg segment per tile, uncompacted M
-      const HSeg hs = hseg[hseg_at + rel];
-      const uint64_t b0 = offp[hs.row];
-      const uint32_t deg = static_cast<uint32_t>(offp[hs.row + 1] - b0);
-      const uint32_t j_beg = hs.seg * kHeavyDeg;
-      const uint32_t j_end = min(deg, j_beg + kHeavyDeg);
-      uint32_t cnt = 0, tnacc = 0;
-      uint32_t carry = j_beg ? colp[b0 + j_beg - 1] : kNone;
-      for (uint32_t j0 = j_beg; j0 < j_end; j0 += kSub * kWave) {
-        uint32_t v[kSub];
-#pragma unroll
-        for (int q = 0; q < kSub; ++q) {
-          const uint32_t j = j0 + q * kWave + lane;
-          v[q] = j < j_end ? colp[b0 + j] : kNone;
-        }
-#pragma unroll 1
-        for (int q = 0; q < kSub; ++q) {
-          const uint32_t vq = v[0];
-#pragma unroll
-          for (int i = 0; i < kSub - 1; ++i) v[i] = v[i + 1];
-          k1_slice<false, MODE>(vq, PM_TB(vq), j0 + q * kWave + lane, b0, nm, o, cnt, tnacc, carry);
-        }
-      }
-      const uint16_t TN = wave_or_bits(tnacc, nm, 0, ~0ull);
-      bool surv = false;
-      if (lane == 0 && !(MODE & 8)) {
-        uint32_t* h_tn = hscr;
-        uint32_t* h_cnt = hscr + nheavy;
-        uint32_t* h_done = hscr + 2 * nheavy;
-        if (TN) atomicOr(&h_tn[hs.h], static_cast<uint32_t>(TN));
-        if (cnt) atomicAdd(&h_cnt[hs.h], cnt);
-        __threadfence();
-        if (atomicAdd(&h_done[hs.h], 1u) == hs.nseg - 1) {
-          __threadfence();
-          const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
-          const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
-          surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
-        }
-      }
-      if (lane < kSub && !(MODE & 8)) tm[lane] = (lane == 0 && surv) ? 1ull : 0ull;
+    } else if (!(MODE & 4)) {
+      const BlockAcc h = k1_heavy_tile<MODE, WIDE>(s_tab, cur.r, cur.rel, hseg, offp, colp, s_runs, nruns, s_adj, oa,
+                                                   o, hscr, nheavy, s_hist, tm);
+      acc.vs += h.vs;
+      acc.es += h.es;
+      acc.removed |= h.removed;
     }
+    t = tn;
+    cur = nxt;
+#pragma unroll
+    for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
   }
-#undef PM_TB
   flush_block(acc, oa, s_hist, s_red, pp);
 }
-
 // slist from the superstep-0 survivor masks: an exclusive scan of the mask
 // popcounts (hipcub) gives each word's base; bits decode to row positions
 // through the tiling.
@@ -548,11 +578,8 @@ __global__ void k_slist_write(const KRange* __restrict__ ktab, uint32_t nr, cons
       const int b = __ffsll(static_cast<long long>(m)) - 1;
       m &= m - 1;
       uint32_t row;
-      if (R.kind <= 6) {  // bit r of the tile = row r of the tile
+      if (R.kind < static_cast<uint32_t>(kHeavyKind)) {  // bit r of the tile = row r of the tile
         row = R.start + rel * (kTileEntries >> R.kind) + q * kWave + b;
-      } else if (R.kind <= 10) {
-        const uint32_t te = kTileEntries > (1u << R.kind) ? kTileEntries : (1u << R.kind);
-        row = R.start + static_cast<uint32_t>((uint64_t(rel) * te) >> R.kind) + b;
       } else {
         row = hseg[R.aux + rel].row;
       }
@@ -842,10 +869,11 @@ __global__ void k_owner_keys(const uint32_t* __restrict__ ids, uint64_t n, uint3
     key[i] = ids[i] % nshards;
 }
 
-// degree class: 0 for degree 0, 1 + k for padded degree 1 << k (k <= 10), 12 above kHeavyDeg
+// degree class: 0 for degree 0, 1 + k for padded degree 1 << k (k < kHeavyKind),
+// kHeavyKind + 1 above kHeavyDeg
 __host__ __device__ inline uint32_t degree_class(uint64_t d) {
   if (d == 0) return 0;
-  if (d > kHeavyDeg) return 12;
+  if (d > kHeavyDeg) return kHeavyKind + 1;
   uint32_t k = 0;
   while ((1ull << k) < d) ++k;
   return 1 + k;
@@ -942,9 +970,9 @@ void build_tiling(Ctx& c) {
   const int nl = static_cast<int>(labs.size());
   // Run boundaries in the label-major order (host binary searches over
   // perm_host): B[0] = first position with the label, B[1 + k] = first with
-  // padded degree >= 1 << k (k = 0..10), B[12] = first with degree >
-  // kHeavyDeg, B[13] = one past the label's last position.
-  static constexpr int kLB = 14;
+  // padded degree >= 1 << k (k < kHeavyKind), B[1 + kHeavyKind] = first with
+  // degree > kHeavyDeg, B[kLB - 1] = one past the label's last position.
+  static constexpr int kLB = kHeavyKind + 3;
   const uint64_t n = c.n;
   auto lab_at = [&](uint64_t i) { return c.labels_host[c.perm_host[i]]; };
   auto cls_at = [&](uint64_t i) { return degree_class(c.deg_host[c.perm_host[i]]); };
@@ -960,9 +988,9 @@ void build_tiling(Ctx& c) {
     uint64_t* B = bounds.data() + l * kLB;
     const uint64_t L = labs[l];
     B[0] = first_where(0, n, [&](uint64_t i) { return lab_at(i) >= L; });
-    B[13] = first_where(B[0], n, [&](uint64_t i) { return lab_at(i) > L; });
-    for (uint32_t k = 0; k <= 11; ++k)
-      B[1 + k] = first_where(B[0], B[13], [&](uint64_t i) { return cls_at(i) >= 1 + k; });
+    B[kLB - 1] = first_where(B[0], n, [&](uint64_t i) { return lab_at(i) > L; });
+    for (uint32_t k = 0; k <= static_cast<uint32_t>(kHeavyKind); ++k)
+      B[1 + k] = first_where(B[0], B[kLB - 1], [&](uint64_t i) { return cls_at(i) >= 1 + k; });
   }
   // this shard's sub-run of [a, b) (positions are owner-sorted inside a run)
   auto owned = [&](uint64_t a, uint64_t b) {
@@ -981,7 +1009,7 @@ void build_tiling(Ctx& c) {
   c.lr.n = nl;
   for (int l = 0; l < nl; ++l) {
     c.lr.lo[l] = static_cast<uint32_t>(bounds[l * kLB + 0]);
-    c.lr.len[l] = static_cast<uint32_t>(bounds[l * kLB + 13] - bounds[l * kLB + 0]);
+    c.lr.len[l] = static_cast<uint32_t>(bounds[l * kLB + kLB - 1] - bounds[l * kLB + 0]);
     c.lr.tu[l] = tus[l];
   }
   std::vector<KRange> tab;
@@ -995,11 +1023,11 @@ void build_tiling(Ctx& c) {
     uint16_t nm = 0;
     for (int t = 0; t < 16; ++t)
       if ((tu >> t) & 1u) nm |= c.pa.adj[t];
-    const uint64_t first_nz = B[1], hi = B[13];
+    const uint64_t first_nz = B[1], hi = B[kLB - 1];
     if (hi <= first_nz) continue;
     // other shards' rows are empty in offr
     c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
-    // kind k = [B[1+k], B[2+k]) for k = 0..10 (padded degree 1 << k); kind 11 = [B[12], hi)
+    // kind k = [B[1+k], B[2+k]) for k < kHeavyKind (padded degree 1 << k); kHeavyKind = [B[1+kHeavyKind], hi)
     for (int kind = 0; kind <= kHeavyKind; ++kind) {
       const auto ab = owned(B[1 + kind], kind == kHeavyKind ? hi : B[2 + kind]);
       const uint64_t a = ab.first, b = ab.second;
