@@ -137,7 +137,8 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_offl = in.gdeg ? dalloc<uint64_t>(c->n + 1) : c->d_off;
   c->d_offp = dalloc<uint64_t>(c->n + 1);
   c->d_offr = dalloc<uint64_t>(c->n + 1);
-  c->d_colp = dalloc<uint32_t>(c->nq);
+  // slot buffers carry kTileEntries entries of tail padding (superstep-0 tile loads read whole tiles)
+  c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries);
   c->d_perm = dalloc<uint32_t>(c->n);
   c->d_pos = dalloc<uint32_t>(c->n);
   c->d_labs = dalloc<uint64_t>(c->n);
@@ -151,7 +152,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_tpub[0] = dalloc<uint16_t>(c->n);
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
-  c->d_mcol = dalloc<uint32_t>(c->nq);
+  c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries);
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
   c->d_slist = dalloc<uint32_t>(c->n);
@@ -179,9 +180,11 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   launch_degree_labels(*c);
   c->labels_host.assign(c->n, 0);
   for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(c->deg_host[v]);
+  const auto t_lay = std::chrono::steady_clock::now();
   build_label_layout(*c, c->d_mcol, false, c->d_colp);
   build_tiling(*c);
   PM_HIP_CHECK(hipStreamSynchronize(c->stream));
+  c->layout_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_lay).count();
   return c.release();
 }
 
@@ -219,10 +222,13 @@ static void destroy_ctx(pm_ctx* c) {
 // New labels: rebuild the label-major layout from the current one (the M
 // column buffer is free between searches and receives the new adjacency).
 static void relayout(Ctx& c) {
+  const auto t_lay = std::chrono::steady_clock::now();
   build_label_layout(c, c.d_colp, true, c.d_mcol);
   std::swap(c.d_colp, c.d_mcol);
   c.mcap = c.nq;  // d_mcol is the former d_colp (nq entries, no remote region)
   build_tiling(c);
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.layout_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_lay).count();
   c.lcc_started = false;
   c.tpub_clean = false;  // positions changed: the next reset clears T_pub entirely
 }
@@ -378,14 +384,16 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   return out;
 }
 
-// Algorithmic bytes of the fused superstep-0 kernel (roofline):
-// matching rows: row offset (8 B); per scanned entry: 4 B neighbour id + 2 B
-// Tl gather; survivors: perm (4 B) + T_state, T_pub (2+2 B) + mlen, malive
-// (4+4 B); per distinct contributing neighbour: 4 B id + 1 B state written.
+// Algorithmic bytes of the fused superstep-0 kernel (DESIGN.md
+// roofline): 4 B neighbour id per scanned adjacency entry, 12 B per scanned
+// (label-matching) row (8 B row offset + 2 B T + 2 B TN), 12 B of state per
+// survivor (T_state, T_pub, |M| written, mlen) and 4 B per kept M entry.  The
+// 2 B neighbour-T gather of the survey's model is not counted: the label-major
+// layout derives a neighbour's template bits from its position, no load.
 static uint64_t lcc_first_bytes(const Ctx& c, uint64_t scanned, uint64_t survivors, uint64_t edges,
                                 uint64_t matching_rows) {
   (void)c;
-  return matching_rows * 8 + scanned * (4 + 2) + survivors * 16 + edges * (4 + 1);
+  return scanned * 4 + matching_rows * 12 + survivors * 12 + edges * 4;
 }
 
 struct DriverFiles {
@@ -1230,8 +1238,8 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
 const char* pm_build_arch(void) { return "gfx950"; }
 
 // Diagnostics: times `reps` launches of the superstep-0 kernel on the current
-// labels (state is reset first).  variant < 16: diagnostic MODE of the
-// kernel on the default grid; variant >= 16: the product kernel on a grid of
+// labels (state is reset first).  variant < 256: diagnostic MODE of the
+// kernel on the default grid; variant >= 256: the product kernel on a grid of
 // `variant` blocks.
 int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
   PM_API_BODY(ctx, {
@@ -1239,9 +1247,9 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     hipEvent_t a, b;
     PM_HIP_CHECK(hipEventCreate(&a));
     PM_HIP_CHECK(hipEventCreate(&b));
-    const unsigned grid = variant >= 16 ? std::min<unsigned>(static_cast<unsigned>(variant), pm::kPartGridMax)
-                                        : ctx->k1_grid;
-    const int mode = variant >= 16 ? 0 : variant;
+    const unsigned grid = variant >= 256 ? std::min<unsigned>(static_cast<unsigned>(variant), pm::kPartGridMax)
+                                         : ctx->k1_grid;
+    const int mode = variant >= 256 ? 0 : variant;
     pm::ensure_counts(*ctx, 1);
     pm::lcc_first_prepare(*ctx);
     pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
@@ -1261,10 +1269,12 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
 
 // Diagnostics: superstep-0 tiling of the current labels: out[0] real adjacency
 // entries of the scanned runs, [1] slots loaded (padding included), [2]
-// scanned rows, [3] tiles, [4] ranges, [5] heavy rows.
+// scanned rows, [3] tiles, [4] ranges, [5] heavy rows, [6] microseconds of
+// the last label-major layout + tiling build (one-time, outside any search).
 int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n) {
   PM_API_BODY(ctx, {
-    uint64_t st[6] = {0, 0, 0, ctx->ntiles, ctx->ktab.empty() ? 0 : ctx->ktab.size() - 1, ctx->nheavy};
+    uint64_t st[7] = {0, 0, 0, ctx->ntiles, ctx->ktab.empty() ? 0 : ctx->ktab.size() - 1, ctx->nheavy,
+                      static_cast<uint64_t>(ctx->layout_seconds * 1e6)};
     std::vector<uint64_t> offp(ctx->n + 1), offr(ctx->n + 1);
     PM_HIP_CHECK(hipMemcpy(offp.data(), ctx->d_offp, offp.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
     PM_HIP_CHECK(hipMemcpy(offr.data(), ctx->d_offr, offr.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
@@ -1274,7 +1284,7 @@ int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n) {
       st[1] += offp[R.end] - offp[R.start];
       st[2] += R.end - R.start;
     }
-    for (uint64_t i = 0; i < n && i < 6; ++i) out[i] = st[i];
+    for (uint64_t i = 0; i < n && i < 7; ++i) out[i] = st[i];
   });
 }
 

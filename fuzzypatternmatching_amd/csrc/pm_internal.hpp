@@ -108,10 +108,12 @@ struct KRange {
   uint32_t nkeep;
 };
 struct HSeg {
-  uint32_t row;   // row position
-  uint32_t seg;   // segment index inside the row
-  uint32_t h;     // heavy-row ordinal (scratch slot)
-  uint32_t nseg;  // segments of the row
+  uint32_t row;    // row position
+  uint32_t seg;    // segment index inside the row
+  uint32_t h;      // heavy-row ordinal (scratch slot)
+  uint32_t nseg;   // segments of the row
+  uint32_t range;  // KRange index
+  uint32_t tile;   // tile index (survivor mask slot)
 };
 static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
 static constexpr uint32_t kTileEntries = 64 * kSub; // 512
@@ -190,6 +192,7 @@ struct Ctx {
   bool k1_wide = false;           // some range has more than four relevant label runs
   HSeg* d_hseg = nullptr;
   uint32_t nheavy = 0;            // heavy rows (scratch slots)
+  uint32_t nhseg = 0;             // heavy segments (one superstep-0 tile each)
   uint32_t* d_hscr = nullptr;     // 3 x nheavy: TN, distinct count, segments done
   uint64_t ss0_trav = 0;          // adjacency entries of label-matching rows
   uint64_t ss0_rows = 0;          // label-matching rows with degree > 0
@@ -296,6 +299,7 @@ struct Ctx {
   float lcc_first_ms = 0.f;
   uint64_t lcc_first_bytes = 0;
   double device_seconds = 0.0;
+  double layout_seconds = 0.0;    // last label-major layout + tiling build (one-time setup)
 
   std::string err;
 };

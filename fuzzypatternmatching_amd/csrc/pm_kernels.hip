@@ -307,25 +307,22 @@ __device__ __forceinline__ K1Desc k1_desc(const KRange* s_tab, uint32_t& r, uint
 
 // The kSub x 64 slots of a light tile (kNone past the run): one load per
 // lane and sub-tile, all issued before any use.  The loads are unconditional
-// (a clamped in-bounds address, the value replaced afterwards; a heavy tile or
-// a tile past the end loads slot 0): a fixed count of loads per tile lets the
-// compiler wait for exactly the oldest tile's loads (vmcnt(16)) instead of
-// draining the counter.
+// and use one uniform base + the lane offset (the slot buffers carry
+// kTileEntries entries of tail padding, so a partial tile, a heavy tile or a
+// tile past the end reads in bounds; such slots are replaced by kNone).
 __device__ __forceinline__ void k1_load(uint32_t (&v)[kSub], const K1Desc& d, const uint32_t* __restrict__ colp,
                                         bool valid) {
   const int lane = lane_id();
   const uint64_t t0 = uint64_t(d.rel) * kTileEntries;
-  const uint64_t tend = valid && d.kind < static_cast<uint32_t>(kHeavyKind) ? uint64_t(d.nrows) << d.kind : 0;
-  const uint64_t base = tend ? d.qbase : 0;
-  const uint64_t last = tend ? tend - 1 : 0;
+  const bool light = valid && d.kind < static_cast<uint32_t>(kHeavyKind);
+  const uint64_t tend = light ? uint64_t(d.nrows) << d.kind : 0;
+  const uint32_t rem = tend > t0 ? static_cast<uint32_t>(min<uint64_t>(tend - t0, kTileEntries)) : 0u;
+  const uint32_t* tp = colp + (rem ? d.qbase + t0 : 0);
 #pragma unroll
-  for (int q = 0; q < kSub; ++q) {
-    const uint64_t s = t0 + q * kWave + lane;
-    v[q] = __builtin_nontemporal_load(colp + base + (s < tend ? s : last));
-  }
+  for (int q = 0; q < kSub; ++q) v[q] = __builtin_nontemporal_load(tp + q * kWave + lane);
 #pragma unroll
   for (int q = 0; q < kSub; ++q)
-    if (t0 + q * kWave + lane >= tend) v[q] = kNone;
+    if (static_cast<uint32_t>(q * kWave + lane) >= rem) v[q] = kNone;
 }
 
 // Per-wave LDS staging of a light tile: per-row accumulators (TN | count << 16,
@@ -334,16 +331,37 @@ __device__ __forceinline__ void k1_load(uint32_t (&v)[kSub], const K1Desc& d, co
 // decided which rows survive.
 struct K1Stage {
   uint32_t acc[kTileEntries];
-  uint32_t lv[kTileEntries];
-  uint16_t ls[kTileEntries];
+  uint2 list[kTileEntries];     // (neighbour position, slot inside the tile)
   unsigned long long sm[kSub];  // survivor bits of the tile's rows
 };
 
+// A wave-uniform 64-bit value held in scalar registers.
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  return (uint64_t(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32))) << 32) |
+         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+}
+
+// Lanes whose slot starts a row, for G = 1 << lg <= 64 slots per row.
+__device__ __forceinline__ uint64_t row_start_mask(uint32_t lg) {
+  switch (lg) {
+    case 0: return ~0ull;
+    case 1: return 0x5555555555555555ull;
+    case 2: return 0x1111111111111111ull;
+    case 3: return 0x0101010101010101ull;
+    case 4: return 0x0001000100010001ull;
+    case 5: return 0x0000000100000001ull;
+    default: return 1ull;
+  }
+}
+
 // Light tile (G = 1 << kind <= kTileEntries slots per row, 512 / G whole rows).
-// Phase A, per sub-tile: Tl(v) from the position (label runs), first
-// occurrence in the row from the left neighbour lane, one ballot; only the
-// few contributing lanes (a few percent of the slots) touch LDS: row OR /
-// count atomics and the staging list.  Phase B walks the staging list only.
+// Phase A, per sub-tile, all in wave masks: a lane's neighbour can contribute
+// iff its position lies in one of the range's relevant label runs (one
+// compare per run, the masks OR-ed on the scalar unit) and it is the first
+// occurrence in its row (row start, or differs from the left neighbour lane);
+// only the contributing lanes (a few percent of the slots) are appended to
+// the LDS staging list.  Phase B over the list only: row TN / count
+// accumulated in LDS, heads verify their row, survivors' entries write M[u].
 template <int MODE, bool WIDE>
 __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K1Desc& d, uint16_t tu, uint16_t nm,
                                               const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
@@ -353,39 +371,65 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
   const int lane = lane_id();
   const uint32_t lg = d.kind;
   const uint32_t gm = (1u << lg) - 1;
+  const uint64_t rs_light = uniform64(row_start_mask(lg));
+  const uint32_t nrel = WIDE ? 0u : min(rel_runs.nrel, 4u);
   uint32_t nlist = 0;  // wave-uniform
 #pragma unroll
   for (int q = 0; q < kSub; ++q) {
     const uint32_t x = v[q];
-    const uint16_t tv = tbits_rel<WIDE>(x, rel_runs, s_runs, nruns);  // 0 for kNone (outside every run)
+    uint64_t cm = 0;
+    if (WIDE) {
+      cm = __ballot((tbits_rel<true>(x, rel_runs, s_runs, nruns) & nm) != 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (static_cast<uint32_t>(i) < nrel) cm |= __ballot(x - rel_runs.lo[i] < rel_runs.len[i]);
+    }
     uint32_t pv = dpp_wave_shr1(x);
     if (q > 0) {
       const uint32_t carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[q - 1]), kWave - 1));
       if (lane == 0) pv = carry;
     }
-    const uint32_t j = q * kWave + lane;  // slot inside the tile
-    const uint32_t tn = tv & nm;
-    const bool contrib = tn != 0 && ((j & gm) == 0 || pv != x);
-    const uint64_t C = __ballot(contrib);
+    uint64_t rs = rs_light;
+    if (lg > 6) rs = ((q * kWave) & gm) == 0 ? 1ull : 0ull;
+    const uint64_t C = cm & (rs | __ballot(pv != x));
     if (C) {
-      if (contrib) {
-        const uint32_t row = j >> lg;
-        atomicOr(&st.acc[row], tn);
-        atomicAdd(&st.acc[row], 1u << 16);
-        const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_popcountll(C & ((1ull << lane) - 1)));
-        st.lv[idx] = x;
-        st.ls[idx] = static_cast<uint16_t>(j);
+      if ((C >> lane) & 1ull) {
+        const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_amdgcn_mbcnt_hi(
+                                         static_cast<uint32_t>(C >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C), 0)));
+        st.list[idx] = make_uint2(x, static_cast<uint32_t>(q * kWave + lane));
       }
-      nlist += static_cast<uint32_t>(__builtin_popcountll(C));
+      nlist = __builtin_amdgcn_readfirstlane(nlist + static_cast<uint32_t>(__builtin_popcountll(C)));
+    }
+  }
+  if (lane < kSub) st.sm[lane] = 0ull;
+  if ((MODE & 16) || nlist == 0) {  // MODE 16 (diagnostic): phase A only
+    if (lane < kSub && !(MODE & 64)) tm[lane] = 0ull;  // MODE 64: without this store
+    return;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // phase B1: row TN (neighbour-mask bits of the contributors' template bits) and count
+#pragma unroll 1
+  for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    if (i < nlist) {
+      const uint2 e = st.list[i];
+      const uint32_t row = e.y >> lg;
+      atomicOr(&st.acc[row], static_cast<uint32_t>(tbits_rel<WIDE>(e.x, rel_runs, s_runs, nruns) & nm));
+      atomicAdd(&st.acc[row], 1u << 16);
     }
   }
   __builtin_amdgcn_wave_barrier();
-  if (lane < kSub) st.sm[lane] = 0ull;
-  // phase B: one pass over the staging list (sorted by slot, so each row's
-  // entries are consecutive).  The first entry of a row (head) verifies it
-  // from its accumulator, complete after phase A; the row's entries learn the
-  // verdict from the head's ballot bit and, for a survivor, write M[u] in
-  // slot order.  Rows without a contribution never enter S.
+  if (MODE & 32) {  // diagnostic: phase A + B1 only
+    if (lane < kSub) tm[lane] = 0ull;
+#pragma unroll 1
+    for (uint32_t i = lane; i < nlist; i += kWave) st.acc[st.list[i].y >> lg] = 0;
+    return;
+  }
+  // phase B2: the list is in slot order, so each row's entries are
+  // consecutive; the first (head) verifies the row, and the row's entries
+  // learn the verdict from the head's ballot bit (survivors write M[u] in
+  // slot order at the start of u's padded row)
   const uint32_t row0 = d.rel * (kTileEntries >> lg);
   uint32_t carry_head = 0, carry_row = kNone;
   uint64_t carry_surv = 0;
@@ -393,9 +437,8 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
   for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
     const bool in = i < nlist;
-    const uint32_t j = in ? st.ls[i] : 0u;
-    const uint32_t x = in ? st.lv[i] : 0u;
-    const uint32_t row = in ? (j >> lg) : kNone;
+    const uint2 e = in ? st.list[i] : make_uint2(0u, 0u);
+    const uint32_t row = in ? (e.y >> lg) : kNone;
     uint32_t prow = dpp_wave_shr1(row);
     if (lane == 0) prow = carry_row;
     const bool head = in && row != prow;
@@ -414,7 +457,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
     const uint32_t hl = hm ? 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(hm))) : 0u;
     const uint32_t hidx = hm ? i0 + hl : carry_head;
     const uint64_t mys = hm ? ((Sv >> hl) & 1ull) : carry_surv;
-    if (!(MODE & 1) && in && mys) o.mcol[d.qbase + (uint64_t(row0 + row) << lg) + (i - hidx)] = x | kAlive;
+    if (!(MODE & 1) && in && mys) o.mcol[d.qbase + (uint64_t(row0 + row) << lg) + (i - hidx)] = e.x | kAlive;
     if (H) {
       const uint32_t hlast = 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(H)));
       carry_head = i0 + hlast;
@@ -430,7 +473,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
 // the segments' TN / counts meet in the hscr scratch and the last segment to
 // finish (ticket) runs the verify.  Rare: kept out of line.
 template <int MODE, bool WIDE>
-__device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t rix, uint32_t rel,
+__device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t hi,
                                                             const HSeg* __restrict__ hseg,
                                                             const uint64_t* __restrict__ offp,
                                                             const uint32_t* __restrict__ colp, const uint32_t* s_runs,
@@ -439,12 +482,12 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t 
                                                             unsigned long long* s_hist, unsigned long long* tm) {
   BlockAcc acc;
   const int lane = lane_id();
-  const KRange& R = s_tab[rix];
+  const HSeg hs = hseg[hi];
+  const KRange& R = s_tab[__builtin_amdgcn_readfirstlane(hs.range)];
   const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.tu));
   const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.nm));
   const RelRuns rel_runs = load_rel(R);
   const KeepArgs keep = load_keep(R);
-  const HSeg hs = hseg[__builtin_amdgcn_readfirstlane(R.aux) + rel];
   const uint64_t b0 = offp[hs.row];
   const uint32_t deg = static_cast<uint32_t>(offp[hs.row + 1] - b0);
   const uint32_t j_beg = hs.seg * kHeavyDeg;
@@ -485,13 +528,14 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t 
 
 // MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores,
 // bit1 skips light tiles, bit2 skips heavy tiles, bit3 keeps only the loads
-// and the label test (checksum).  WIDE: some range has more than four
+// and the label test (checksum), bit4 stops light tiles after phase A, bit5
+// after phase B1.  WIDE: some range has more than four
 // relevant label runs (tbits_rel scans them all).
 template <int MODE, bool WIDE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
-    K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, unsigned long long* __restrict__ tmask,
+    K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, uint32_t nhseg, unsigned long long* __restrict__ tmask,
     Partials pp) {
   extern __shared__ KRange s_tab[];  // nr + 1 entries (dynamic LDS)
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
@@ -541,18 +585,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) 
         const KeepArgs keep = load_keep(R);
         k1_light_tile<MODE, WIDE>(vc, cur, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
       }
-    } else if (!(MODE & 4)) {
-      const BlockAcc h = k1_heavy_tile<MODE, WIDE>(s_tab, cur.r, cur.rel, hseg, offp, colp, s_runs, nruns, s_adj, oa,
-                                                   o, hscr, nheavy, s_hist, tm);
-      acc.vs += h.vs;
-      acc.es += h.es;
-      acc.removed |= h.removed;
-    }
+    }  // heavy tiles: the loop below
     t = tn;
     cur = nxt;
 #pragma unroll
     for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
   }
+  // heavy rows, one segment per wave at a time (a separate loop: no slot
+  // buffers live, so the light loop's register budget is its own)
+  if (!(MODE & 4))
+    for (uint32_t hi = blockIdx.x * kWpb + wid; hi < nhseg; hi += W) {
+      const BlockAcc h = k1_heavy_tile<MODE, WIDE>(s_tab, hi, hseg, offp, colp, s_runs, nruns, s_adj, oa, o, hscr,
+                                                   nheavy, s_hist, tmask + uint64_t(hseg[hi].tile) * kSub);
+      acc.vs += h.vs;
+      acc.es += h.es;
+      acc.removed |= h.removed;
+    }
   flush_block(acc, oa, s_hist, s_red, pp);
 }
 // slist from the superstep-0 survivor masks: an exclusive scan of the mask
@@ -1072,7 +1120,10 @@ void build_tiling(Ctx& c) {
         for (uint64_t i = a; i < b; ++i) {
           const uint64_t deg = o[i - a + 1] - o[i - a];
           const uint32_t ns = static_cast<uint32_t>((deg + kHeavyDeg - 1) / kHeavyDeg);
-          for (uint32_t sgm = 0; sgm < ns; ++sgm) hs.push_back(HSeg{static_cast<uint32_t>(i), sgm, nheavy, ns});
+          for (uint32_t sgm = 0; sgm < ns; ++sgm) {
+            const uint32_t tile = tiles + static_cast<uint32_t>(hs.size() - R.aux);
+            hs.push_back(HSeg{static_cast<uint32_t>(i), sgm, nheavy, ns, static_cast<uint32_t>(tab.size()), tile});
+          }
           ++nheavy;
         }
         nt = hs.size() - R.aux;
@@ -1098,6 +1149,7 @@ void build_tiling(Ctx& c) {
     if (R.nrel > 4) c.k1_wide = true;
   c.ntiles = tiles;
   c.nheavy = nheavy;
+  c.nhseg = static_cast<uint32_t>(hs.size());
   if (c.d_ktab) (void)hipFree(c.d_ktab);
   if (c.d_hseg) (void)hipFree(c.d_hseg);
   if (c.d_hscr) (void)hipFree(c.d_hscr);
@@ -1131,7 +1183,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
 #define PM_K1_ARGS                                                                                                    \
   dim3(grid), dim3(kBlock), c.ktab.size() * sizeof(KRange), c.stream, c.d_ktab,                                    \
       static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,                                                  \
-      c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c), c.d_hscr, c.nheavy,                                  \
+      c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c), c.d_hscr, c.nheavy, c.nhseg,                         \
       reinterpret_cast<unsigned long long*>(c.d_tmask), partials(c, d_slot)
   switch (variant) {
     case 0:
@@ -1144,6 +1196,9 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 8: hipLaunchKernelGGL(k_lcc_first<8>, PM_K1_ARGS); break;
     case 10: hipLaunchKernelGGL(k_lcc_first<10>, PM_K1_ARGS); break;
     case 12: hipLaunchKernelGGL(k_lcc_first<12>, PM_K1_ARGS); break;
+    case 16: hipLaunchKernelGGL(k_lcc_first<16>, PM_K1_ARGS); break;
+    case 32: hipLaunchKernelGGL(k_lcc_first<32>, PM_K1_ARGS); break;
+    case 80: hipLaunchKernelGGL(k_lcc_first<80>, PM_K1_ARGS); break;
     default: throw std::runtime_error("unknown superstep-0 kernel variant");
   }
 #undef PM_K1_ARGS

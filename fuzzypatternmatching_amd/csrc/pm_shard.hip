@@ -442,7 +442,7 @@ void shard_replicate_m(Ctx& c) {
   if (need > c.mcap) {
     const uint64_t cap = std::max(need, c.mcap + c.mcap / 4);
     uint32_t* nb = nullptr;
-    PM_HIP_CHECK(hipMalloc(&nb, cap * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMalloc(&nb, (cap + kTileEntries) * sizeof(uint32_t)));  // + tail padding (k1_load)
     if (c.nq) PM_HIP_CHECK(hipMemcpyAsync(nb, c.d_mcol, c.nq * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
     PM_HIP_CHECK(hipStreamSynchronize(c.stream));
     (void)hipFree(c.d_mcol);

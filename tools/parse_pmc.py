@@ -1,11 +1,15 @@
-"""Summarise rocprofv3 --pmc passes of k_lcc_first into profiles/<round>_pmc_lcc_first.json.
+"""Summarise rocprofv3 --pmc passes of k_lcc_first (tools/gpu_pmc_k1.sh) into a JSON file.
 
-HBM bytes per launch follow MI355X_MICROARCH.md section HBM / cdna_hip_programming.md 7:
-FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per
-TCC_EA0_RDREQ, i.e. half of a 128-B request, so reads are doubled:
+usage: parse_pmc.py GPURUN_OUT TAG SCALE P_GEN OUT.json
+
+HBM bytes per launch follow MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B read
+request, so reads are doubled:
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
-(the doc calls the x2 exact for 16-B-per-lane streams and uncalibrated for
-other widths; both raw and corrected values are recorded).
+(the guide calls the x2 exact for 16-B-per-lane streams; this kernel reads
+4 B per lane in 256-B wave rows; both raw and corrected values are kept).
+Each pass is its own rocprofv3 run; counters are averaged over the
+k_lcc_first dispatches of the pass (the first, warm-up launch included).
 """
 import csv
 import glob
@@ -18,33 +22,30 @@ def counters(d):
     out = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r.get("Counter_Name")
-            val = float(r.get("Counter_Value", 0))
-            disp = r.get("Dispatch_Id")
-            out.setdefault(name, {}).setdefault(disp, 0.0)
-            out[name][disp] += val
+            if "k_lcc_first" not in r.get("Kernel_Name", "k_lcc_first"):
+                continue
+            out.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
+            out[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: sum(v.values()) / max(1, len(v)) for k, v in out.items()}
 
 
 def main():
-    base, tag, scale = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    base, tag, scale, p_gen, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
     vals = {}
-    for i in (1, 2, 3):
-        vals.update(counters(os.path.join(base, f"{tag}_{i}")))
-    fetch = vals.get("FETCH_SIZE")
-    write = vals.get("WRITE_SIZE")
-    res = {"kernel": "k_lcc_first", "scale": scale, "p_gen": 4, "pattern": "rmat_log2_tree_pattern",
-           "fetch_size_kib": fetch, "write_size_kib": write,
-           "tcc_hit": vals.get("TCC_HIT_sum"), "tcc_miss": vals.get("TCC_MISS_sum")}
+    for d in sorted(glob.glob(os.path.join(base, f"{tag}_[0-9]*"))):
+        if os.path.isdir(d):
+            vals.update(counters(d))
+    fetch, write = vals.get("FETCH_SIZE"), vals.get("WRITE_SIZE")
+    res = {"kernel": "k_lcc_first", "scale": scale, "p_gen": p_gen, "pattern": "rmat_log2_tree_pattern",
+           "fetch_size_kib": fetch, "write_size_kib": write, "counters": vals}
     if fetch is not None and write is not None:
         res["hbm_bytes_per_launch"] = int((2 * fetch + write) * 1024)
         res["hbm_bytes_per_launch_raw"] = int((fetch + write) * 1024)
-    if res["tcc_hit"] is not None and res["tcc_miss"]:
-        res["l2_hit_rate"] = res["tcc_hit"] / (res["tcc_hit"] + res["tcc_miss"])
-    os.makedirs("profiles", exist_ok=True)
-    out = os.path.join(base, f"{tag}_summary.json")
+    h, m = vals.get("TCC_HIT_sum"), vals.get("TCC_MISS_sum")
+    if h is not None and m:
+        res["l2_hit_rate"] = h / (h + m)
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res))
+    print(json.dumps({k: v for k, v in res.items() if k != "counters"}))
 
 
 if __name__ == "__main__":
