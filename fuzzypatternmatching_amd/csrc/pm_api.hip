@@ -83,6 +83,36 @@ struct CtxInput {
   bool col_on_device = false;      // col is device memory (GPU-built graph); off stays host
 };
 
+// In-rows of a directed CSR (rows sorted by source id, duplicates adjacent):
+// superstep 0 pulls along in-edges, i.e. exactly the messages the reference
+// pushes along out-edges (nonunique_ee.hpp:555-560, SURVEY A.6 hazard 10).
+static void transpose_csr(uint64_t n, const uint64_t* off, const uint32_t* col, std::vector<uint64_t>& toff,
+                          std::vector<uint32_t>& tcol) {
+  toff.assign(n + 1, 0);
+  for (uint64_t e = 0; e < off[n]; ++e) {
+    if (col[e] >= n) throw std::runtime_error("edge target out of range");
+    ++toff[col[e] + 1];
+  }
+  for (uint64_t v = 0; v < n; ++v) toff[v + 1] += toff[v];
+  tcol.resize(off[n]);
+  std::vector<uint64_t> at(toff.begin(), toff.end() - 1);
+  for (uint64_t v = 0; v < n; ++v)
+    for (uint64_t e = off[v]; e < off[v + 1]; ++e) tcol[at[col[e]]++] = static_cast<uint32_t>(v);
+}
+
+// Degree labels (vertex_data_db_degree.hpp:109) from the global out-degrees.
+static void set_degree_labels(Ctx& c) {
+  c.labels_host.assign(c.n, 0);
+  for (uint64_t v = 0; v < c.n; ++v) c.labels_host[v] = degree_label(c.deg_host[v]);
+  if (c.symmetric) {
+    launch_degree_labels(c);  // d_off holds the (global) degrees
+  } else {
+    PM_HIP_CHECK(hipMemcpyAsync(c.d_labels, c.labels_host.data(), c.n * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                c.stream));
+  }
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
 static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int device) {
   std::unique_ptr<Comm> comm(in.comm);
   if (!in.off || !in.col) throw std::runtime_error("pm_create: null graph");
@@ -102,9 +132,21 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->shard = in.shard;
   c->comm = comm.get();
   c->comm_owned = comm.release();
-  if (!c->symmetric)
-    throw std::runtime_error("directed (non-symmetric) input graphs are not supported by the GPU path yet");
   if (c->n >= (1ull << 30)) throw std::runtime_error("more than 2^30 vertices (30-bit positions in M entries)");
+  // the rows superstep 0 scans: the CSR itself, or its in-rows for a directed graph
+  std::vector<uint64_t> tin_off;
+  std::vector<uint32_t> tin_col;
+  const uint64_t* soff = in.off;
+  const uint32_t* scol = in.col;
+  if (!c->symmetric) {
+    if (in.nshards > 1) throw std::runtime_error("directed input graphs are supported on one shard only");
+    if (in.col_on_device) throw std::runtime_error("directed input graphs must be host resident");
+    transpose_csr(c->n, in.off, in.col, tin_off, tin_col);
+    soff = tin_off.data();
+    scol = tin_col.data();
+    c->rdeg_host.resize(c->n);
+    for (uint64_t v = 0; v < c->n; ++v) c->rdeg_host[v] = static_cast<uint32_t>(soff[v + 1] - soff[v]);
+  }
   c->pattern = load_pattern_dir(pattern_dir);
   const PatternGraph& pg = c->pattern.graph;
   if (pg.diameter == 0) throw std::runtime_error("pattern_stat: diameter is 0 or missing");
@@ -128,10 +170,10 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
     goff.assign(c->n + 1, 0);
     for (uint64_t v = 0; v < c->n; ++v) goff[v + 1] = goff[v] + in.gdeg[v];
   }
-  const uint64_t* off_all = in.gdeg ? goff.data() : in.off;
+  const uint64_t* off_all = in.gdeg ? goff.data() : soff;
   // device graph + state; padded slot count of the rows scanned here (label independent)
   c->nq = 0;
-  for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(in.off[v + 1] - in.off[v]);
+  for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(soff[v + 1] - soff[v]);
   c->mcap = c->nq;
   c->d_off = dalloc<uint64_t>(c->n + 1);
   c->d_offl = in.gdeg ? dalloc<uint64_t>(c->n + 1) : c->d_off;
@@ -143,7 +185,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_pos = dalloc<uint32_t>(c->n);
   c->d_labs = dalloc<uint64_t>(c->n);
   PM_HIP_CHECK(hipMemcpy(c->d_off, off_all, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
-  if (in.gdeg) PM_HIP_CHECK(hipMemcpy(c->d_offl, in.off, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  if (in.gdeg) PM_HIP_CHECK(hipMemcpy(c->d_offl, soff, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   if (!c->hubs_host.empty()) {
     c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
     PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
@@ -172,14 +214,15 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
+  // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
+  // asymmetric M then aborts the search: tests use it to find such inputs)
+  if (const char* e = std::getenv("PM_FORCE_PULL")) c->force_pull = std::string(e) == "1" && c->symmetric;
   // default labels = degree labels; the id-major adjacency is staged in the
   // M column buffer and permuted into the label-major d_colp
   if (c->nnz)
-    PM_HIP_CHECK(hipMemcpy(c->d_mcol, in.col, c->nnz * sizeof(uint32_t),
+    PM_HIP_CHECK(hipMemcpy(c->d_mcol, scol, c->nnz * sizeof(uint32_t),
                            in.col_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
-  launch_degree_labels(*c);
-  c->labels_host.assign(c->n, 0);
-  for (uint64_t v = 0; v < c->n; ++v) c->labels_host[v] = degree_label(c->deg_host[v]);
+  set_degree_labels(*c);
   const auto t_lay = std::chrono::steady_clock::now();
   build_label_layout(*c, c->d_mcol, false, c->d_colp);
   build_tiling(*c);
@@ -206,7 +249,7 @@ static void destroy_ctx(pm_ctx* c) {
   void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
-                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base,
+                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn,
                   c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
                   c->d_aown, c->d_axl, c->d_anum, c->d_asend, c->d_arecv, c->d_lstats_loc};
   for (void* p : ptrs)
@@ -311,7 +354,10 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       shard_after_first(c);  // sharded: every shard's slist, then T_pub
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
-      launch_lcc_step(c, slot);
+      // pull form while M is known symmetric (the first call on a symmetric
+      // graph: no cycle flag set yet); push form otherwise (one shard only)
+      if (!c.comm && !c.force_pull && (!c.symmetric || !init_step)) launch_lcc_push(c, slot);
+      else launch_lcc_step(c, slot);
       shard_exchange_tpub(c);
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
@@ -379,8 +425,8 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   c.probe("lcc parsed");
   if (asym)
     throw std::runtime_error(
-        "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message); "
-        "the push-form LCC kernel needed for this case is not implemented yet");
+        "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message) in a pull-form "
+        "superstep (sharded search, or PM_FORCE_PULL=1)");
   return out;
 }
 
@@ -857,11 +903,7 @@ const char* pm_last_error(const pm_ctx* ctx) {
 
 int pm_vertex_data_degree(pm_ctx* ctx) {
   PM_API_BODY(ctx, {
-    pm::launch_degree_labels(*ctx);
-    std::vector<uint64_t> off(ctx->n + 1);
-    PM_HIP_CHECK(hipMemcpy(off.data(), ctx->d_off, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    for (uint64_t v = 0; v < ctx->n; ++v) ctx->labels_host[v] = pm::degree_label(off[v + 1] - off[v]);
-    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    pm::set_degree_labels(*ctx);
     pm::relayout(*ctx);
   });
 }

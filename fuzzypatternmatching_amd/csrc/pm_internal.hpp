@@ -171,7 +171,9 @@ struct Ctx {
   // row keeps the id order of the input, so duplicates stay adjacent).
   uint64_t* d_off = nullptr;      // id-major offsets of the whole graph (degrees: labels, layout), V+1
   uint64_t* d_offl = nullptr;     // id-major offsets of this shard's rows (== d_off unsharded), V+1
-  std::vector<uint32_t> deg_host; // global degree by vertex id (tiling bounds)
+  std::vector<uint32_t> deg_host; // global (out-)degree by vertex id: labels, hubs, ss0 senders' entries
+  std::vector<uint32_t> rdeg_host;// directed graphs: in-degree (length of the row superstep 0 scans)
+  uint32_t row_degree(uint64_t v) const { return rdeg_host.empty() ? deg_host[v] : rdeg_host[v]; }
   uint64_t nq = 0;                // padded slots (label independent)
   uint64_t* d_offp = nullptr;     // label-major padded row starts, V+1
   uint64_t* d_offr = nullptr;     // label-major unpadded offsets (degree sums), V+1
@@ -259,6 +261,7 @@ struct Ctx {
   int smask_cur = 0;
   bool smask_valid = false;       // false right after superstep 0 (all entries live)
   uint32_t* d_flags = nullptr;    // [0] not_finished, [1] asymmetric edge state, [2] deleted
+  uint32_t* d_tn = nullptr;       // TN per position for the push-form supersteps (allocated on first use)
   uint64_t* d_counts = nullptr;   // per-slot per-rank counts (vertices, edges) + traversed
   uint64_t* d_part = nullptr;     // per-block counter partials (kPartGridMax x slot_words)
   uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile
@@ -288,6 +291,7 @@ struct Ctx {
   unsigned line_grid = 0;         // blocks of a full-chip line launch (one per CU)
   uint64_t live_hint = ~0ull;     // S members on this context after the last LCC call (line grid size)
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
+  bool force_pull = false;        // PM_FORCE_PULL=1 (diagnostics): pull-form LCC in every call
 
   // last token-passing call
   uint32_t* d_sources = nullptr;
@@ -321,6 +325,9 @@ void lcc_first_prepare(Ctx& c);  // zeroes the heavy-row scratch before a launch
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot);  // variant != 0: diagnostics
 unsigned lcc_first_grid(const Ctx& c);
 void launch_lcc_step(Ctx& c, uint64_t* d_slot);
+// Push form of a later superstep (send + verify launches): directed inputs and
+// LCC calls after the first (M may be asymmetric there).
+void launch_lcc_push(Ctx& c, uint64_t* d_slot);
 void launch_count_state(Ctx& c, uint64_t* d_slot);
 // Zero T_pub (both buffers) at the slist entries of the last search (every
 // nonzero T_pub entry is one of them, plus the other shards' when sharded).

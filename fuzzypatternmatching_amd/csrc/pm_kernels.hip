@@ -845,6 +845,114 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   flush_block(acc, oa, s_hist, s_red, pp);
 }
 
+// ---------------------------------------------------------------------------
+// K2', push form of a later LCC superstep (directed inputs, and every LCC call
+// after the first, where a cycle terminal's edge flag may have broken the
+// symmetry of M; nonunique_ee.hpp:571-633 senders, :412-443 + :647-816
+// receivers, :886-977 verify).  Two launches per superstep:
+//   send:   every v of S (T_pub(v) != 0) delivers T_pub(v) to each alive u of
+//           M[v]; a receiver u in S with a valid parent gets TN(u) |= T_pub(v)
+//           (atomic OR, before the edge check, hazard 5) and, when v is in
+//           M[u] (rows are in neighbour-id order: binary search), that entry's
+//           flag is set;
+//   verify: keep_bits(T_state, TN); survivors keep their flagged entries,
+//           flags cleared; an emptied vertex leaves S.
+// Rows are walked by one lane each (M rows are short after superstep 0).
+__device__ __forceinline__ int64_t m_find(const uint32_t* __restrict__ mcol, uint64_t b, uint32_t len,
+                                          const uint32_t* __restrict__ perm, uint32_t vid) {
+  uint64_t lo = b, hi = b + len;
+  while (lo < hi) {  // first entry whose neighbour id >= vid
+    const uint64_t mid = (lo + hi) >> 1;
+    if (perm[mcol[mid] & kPosMask] < vid) lo = mid + 1; else hi = mid;
+  }
+  return lo < b + len ? static_cast<int64_t>(lo) : -1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_lcc_push_send(
+    const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
+    const uint16_t* __restrict__ tcur, PatArgs pa, const uint32_t* __restrict__ perm, uint32_t* __restrict__ mcol,
+    const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive, uint32_t* __restrict__ tn,
+    unsigned long long* __restrict__ trav_out) {
+  __shared__ uint16_t s_adj[16];
+  load_adj(s_adj, pa);
+  __syncthreads();
+  const uint32_t nS = *nSp;
+  uint64_t trav = 0;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t v = slist[i];
+    const uint16_t Tv = tcur[v];
+    if (!Tv) continue;
+    trav += malive[v];
+    const uint64_t b = offp[v];
+    const uint32_t L = mlen[v];
+    const uint32_t vid = perm[v];
+    for (uint32_t j = 0; j < L; ++j) {
+      const uint32_t m = mcol[b + j];
+      if (!(m & kAlive)) continue;
+      const uint32_t u = m & kPosMask;
+      const uint16_t Tu = tcur[u];
+      if (!Tu || !(Tv & nbr_mask(Tu, s_adj))) continue;  // u not in S, or not a valid parent
+      atomicOr(&tn[u], static_cast<uint32_t>(Tv));
+      const int64_t e = m_find(mcol, offp[u], mlen[u], perm, vid);
+      if (e >= 0) {
+        const uint32_t x = mcol[e];
+        if ((x & kPosMask) == v && (x & kAlive)) atomicOr(&mcol[e], kFlag);
+      }
+    }
+  }
+  block_atomic_add(trav_out, trav);  // the superstep's traversed-entries word
+}
+
+__global__ __launch_bounds__(kBlock) void k_lcc_push_verify(
+    const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
+    const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
+    OwnerArgs oa, uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen, uint32_t* __restrict__ malive,
+    uint32_t* __restrict__ tn, Partials pp) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  __shared__ uint16_t s_adj[16];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  load_adj(s_adj, pa);
+  __syncthreads();
+  BlockAcc acc;
+  const uint32_t nS = *nSp;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t u = slist[i];
+    if (!tcur[u]) {
+      tnxt[u] = 0;
+      continue;
+    }
+    const uint16_t T = keep_bits(tst[u], static_cast<uint16_t>(tn[u]), s_adj);
+    tn[u] = 0;
+    if (!T) {
+      tnxt[u] = 0;
+      malive[u] = 0;
+      acc.removed = 1;
+      continue;
+    }
+    tst[u] = T;
+    tnxt[u] = T;
+    const uint64_t b = offp[u];
+    const uint32_t L = mlen[u];
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < L; ++j) {
+      const uint32_t m = mcol[b + j];
+      if (!(m & kAlive)) continue;
+      const bool keep = (m & kFlag) != 0;
+      mcol[b + j] = (m & kPosMask) | (keep ? kAlive : 0u);
+      cnt += keep ? 1u : 0u;
+    }
+    malive[u] = cnt;
+    if (oa.nranks <= 1) {
+      acc.vs += 1;
+      acc.es += cnt;
+    } else {
+      acc_owner(s_hist, oa, u, cnt);
+    }
+  }
+  flush_block(acc, oa, s_hist, s_red, pp);
+}
+
 // Counts of the current state (after token-passing post-processing).
 __global__ __launch_bounds__(kBlock) void k_count_state(const uint32_t* __restrict__ slist,
                                                         const uint32_t* __restrict__ nSp,
@@ -1023,7 +1131,7 @@ void build_tiling(Ctx& c) {
   static constexpr int kLB = kHeavyKind + 3;
   const uint64_t n = c.n;
   auto lab_at = [&](uint64_t i) { return c.labels_host[c.perm_host[i]]; };
-  auto cls_at = [&](uint64_t i) { return degree_class(c.deg_host[c.perm_host[i]]); };
+  auto cls_at = [&](uint64_t i) { return degree_class(c.row_degree(c.perm_host[i])); };
   auto first_where = [](uint64_t lo, uint64_t hi, auto&& pred) {  // first i in [lo, hi) with pred(i)
     while (lo < hi) {
       const uint64_t m = (lo + hi) >> 1;
@@ -1072,9 +1180,13 @@ void build_tiling(Ctx& c) {
     for (int t = 0; t < 16; ++t)
       if ((tu >> t) & 1u) nm |= c.pa.adj[t];
     const uint64_t first_nz = B[1], hi = B[kLB - 1];
+    // every label-matching vertex sends along its out-edges: the scanned rows'
+    // entries (other shards' rows are empty in offr); directed graphs scan
+    // in-rows, so the senders' out-degrees are summed instead
+    if (!c.symmetric)
+      for (uint64_t i = B[0]; i < hi; ++i) c.ss0_trav += c.deg_host[c.perm_host[i]];
     if (hi <= first_nz) continue;
-    // other shards' rows are empty in offr
-    c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
+    if (c.symmetric) c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
     // kind k = [B[1+k], B[2+k]) for k < kHeavyKind (padded degree 1 << k); kHeavyKind = [B[1+kHeavyKind], hi)
     for (int kind = 0; kind <= kHeavyKind; ++kind) {
       const auto ab = owned(B[1 + kind], kind == kHeavyKind ? hi : B[2 + kind]);
@@ -1256,6 +1368,24 @@ size_t slist_scan_tmp_bytes(uint64_t words) {
   PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, static_cast<uint64_t*>(nullptr),
                                                 static_cast<int>(std::max<uint64_t>(words, 1)), hipStream_t(0)));
   return tmp;
+}
+
+void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
+  if (!c.d_tn) {
+    PM_HIP_CHECK(hipMalloc(&c.d_tn, c.n * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMemsetAsync(c.d_tn, 0, c.n * sizeof(uint32_t), c.stream));
+  }
+  const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
+  const unsigned grid = grid_for(c.nS_host, kBlock, 8192);
+  hipLaunchKernelGGL(k_lcc_push_send, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS,
+                     c.d_tpub[c.cur], c.pa, c.d_perm, c.d_mcol, c.d_mlen, c.d_malive, c.d_tn,
+                     reinterpret_cast<unsigned long long*>(d_slot + 2 * P));
+  hipLaunchKernelGGL(k_lcc_push_verify, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS,
+                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
+                     c.d_malive, c.d_tn, partials(c, d_slot));
+  PM_HIP_CHECK(hipGetLastError());
+  c.cur ^= 1;
+  c.smask_valid = false;  // the pull kernel's live masks are not maintained here
 }
 
 void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
