@@ -260,6 +260,8 @@ def main():
 
 if __name__ == "__main__":
     rc = main()
+    if os.environ.get("PM_DUMP_MAPS"):  # diagnostics: shared-object map for symbolising a crash at exit
+        sys.stderr.write(open("/proc/self/maps").read())
     sys.stdout.flush()
     sys.stderr.flush()
     if "rocprof" not in os.environ.get("LD_PRELOAD", ""):

@@ -81,6 +81,7 @@ struct CtxInput {
   uint32_t nshards = 1, shard = 0;
   Comm* comm = nullptr;            // ownership passes to the context
   bool col_on_device = false;      // col is device memory (GPU-built graph); off stays host
+  uint32_t inprocess_shards = 1;   // shards of this process on the same device (ThreadComm groups)
 };
 
 // In-rows of a directed CSR (rows sorted by source id, duplicates adjacent):
@@ -153,8 +154,14 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   for (int t = 0; t < kMaxTemplateVertices; ++t) c->pa.adj[t] = pg.adj[t];
   c->pa.K = static_cast<int32_t>(pg.vertex_data.size());
   for (int t = 0; t < c->pa.K; ++t) c->pa.plabel[t] = pg.vertex_data[t];
-  for (const auto& l : c->pattern.lines)
-    if (l.selected_vertices) throw std::runtime_error("pattern_nlc selected_vertices=1 is not supported yet");
+  bool any_sv = false;
+  for (size_t pl = 0; pl < c->pattern.lines.size(); ++pl) {
+    const auto& l = c->pattern.lines[pl];
+    if (!l.selected_vertices) continue;
+    any_sv = true;
+    if (pl >= 4 || l.valid_cycle)  // the reference applies it in nem_1 path checks only
+      throw std::runtime_error("pattern_nlc selected_vertices=1 is supported on path lines (index < 4, valid_cycle 0)");
+  }
   // global degrees (labels, hubs, layout order) and offsets of the rows scanned here
   c->deg_host.resize(c->n);
   for (uint64_t v = 0; v < c->n; ++v) {
@@ -209,11 +216,13 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   size_t free_b = 0, total_b = 0;
   PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
   size_t arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
-  if (c->nshards > 1) arena = std::min<size_t>(arena, size_t(8) << 30);  // in-process groups share one device
+  if (in.inprocess_shards > 1)  // in-process shard groups share one device
+    arena = std::min<size_t>(arena, std::max<size_t>(size_t(1) << 30, free_b / (2 * in.inprocess_shards)));
   arena = std::max<size_t>(arena, size_t(64) << 20);
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
+  if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
   // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
   // asymmetric M then aborts the search: tests use it to find such inputs)
   if (const char* e = std::getenv("PM_FORCE_PULL")) c->force_pull = std::string(e) == "1" && c->symmetric;
@@ -249,9 +258,9 @@ static void destroy_ctx(pm_ctx* c) {
   void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
-                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn,
+                  c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
                   c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
-                  c->d_aown, c->d_axl, c->d_anum, c->d_asend, c->d_arecv, c->d_lstats_loc};
+                  };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete c->comm_owned;
@@ -292,7 +301,7 @@ static void reset_state(Ctx& c) {
   c.nS_host = 0;
   c.lcc_started = false;
   c.nsources = 0;
-  c.m_dirty = true;
+  c.npseen = 0;
 }
 
 // Per-superstep outputs of one LCC call.
@@ -377,7 +386,6 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   std::vector<uint64_t> local = c.comm ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
   const uint32_t nS = static_cast<uint32_t>(pin[0] & 0xFFFFFFFFull);
   c.nS_host = nS;
-  c.m_dirty = true;
   LccOut out;
   bool asym = false;
   {
@@ -658,60 +666,26 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         bool fused = false;
         auto t1 = tick();
         if (c.comm) {
-          // sharded: one line per launch over this shard's sources; the line's
-          // sums and every shard's post-processed T_pub follow on the stream
-          shard_replicate_m(c);
-          std::vector<FusedLineOut> one;
-          bool overflow = false;
-          const bool ok = c.fused_lines && run_lines_fused(c, pl, files, one, overflow, 1, true) == 1;
-          if (ok && !c.any_overflow) {
-            fo = std::move(one[0]);
-            tr = fo.tr;
-            deleted = fo.deleted;
-            vc = cur_vc;
-            ec = cur_ec;
-            for (uint32_t r = 0; r < c.nranks; ++r) {
-              loc_vc[r] -= fo.rm_v[r];
-              loc_ec[r] -= fo.rm_e[r];
-              vc[r] -= fo.grm_v[r];
-              ec[r] -= fo.grm_e[r];
-            }
-            walks.swap(fo.walks);
-            stride = fo.stride;
-          } else {
-            // some shard overflowed a capacity (or fused lines are off): shards
-            // that overflowed rerun the line on the exact-count path, the others
-            // keep their fused results; then host sums and a full T_pub exchange
-            if (ok) {
-              fo = std::move(one[0]);
-              tr = fo.ltr;
-              deleted = fo.ldeleted;
-              for (uint32_t r = 0; r < c.nranks; ++r) {
-                loc_vc[r] -= fo.rm_v[r];
-                loc_ec[r] -= fo.rm_e[r];
-              }
-              walks.swap(fo.walks);
-              stride = fo.stride;
-            } else {
-              tr = pl >= 4 ? run_tds_line(c, line, walks, stride) : run_path_line(c, line);
-              deleted = launch_post_tp(c, line);
-              count_state(c, loc_vc, loc_ec);
-              stride = static_cast<uint32_t>(line.cycle_length + 2);
-            }
-            std::vector<uint64_t> sums = {deleted, tr.sources, tr.acked, tr.edges, tr.tokens, tr.walks};
-            sums.insert(sums.end(), loc_vc.begin(), loc_vc.end());
-            sums.insert(sums.end(), loc_ec.begin(), loc_ec.end());
-            sums = shard_allreduce(c, sums);
-            deleted = sums[0] ? 1u : 0u;
-            tr.sources = sums[1];
-            tr.acked = sums[2];
-            tr.edges = sums[3];
-            tr.tokens = sums[4];
-            tr.walks = sums[5];
-            vc.assign(sums.begin() + 6, sums.begin() + 6 + c.nranks);
-            ec.assign(sums.begin() + 6 + c.nranks, sums.begin() + 6 + 2 * c.nranks);
-            shard_exchange_tpub(c);
-          }
+          // sharded: the per-position path with the token / walk exchange
+          // (shard_route), then post-processing of this shard's sources, the
+          // sums over the shards and the T_pub of every shard's slist
+          tr = pl >= 4 ? run_tds_line(c, line, walks, stride) : run_path_line(c, line);
+          deleted = launch_post_tp(c, line);
+          count_state(c, loc_vc, loc_ec);
+          stride = static_cast<uint32_t>(line.cycle_length + 2);
+          std::vector<uint64_t> sums = {deleted, tr.sources, tr.acked, tr.edges, tr.tokens, tr.walks};
+          sums.insert(sums.end(), loc_vc.begin(), loc_vc.end());
+          sums.insert(sums.end(), loc_ec.begin(), loc_ec.end());
+          sums = shard_allreduce(c, sums);
+          deleted = sums[0] ? 1u : 0u;
+          tr.sources = sums[1];
+          tr.acked = sums[2];
+          tr.edges = sums[3];
+          tr.tokens = sums[4];
+          tr.walks = sums[5];
+          vc.assign(sums.begin() + 6, sums.begin() + 6 + c.nranks);
+          ec.assign(sums.begin() + 6 + c.nranks, sums.begin() + 6 + 2 * c.nranks);
+          shard_exchange_tpub(c);
           if (files && pl >= 4) {
             std::vector<uint32_t> all;
             for (auto& part : shard_allgatherv(c, walks)) all.insert(all.end(), part.begin(), part.end());
@@ -994,6 +968,15 @@ int pm_comm_unique_id(uint8_t* out, uint64_t len) {
   }
 }
 
+int pm_debug_rccl_selftest(int device, uint64_t bytes, int op) {
+  try {
+    return pm::rccl_selftest(device, bytes, op);
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
 pm_ctx* pm_create_shard(const pm_shard_desc* d, const char* pattern_dir, int device, const uint8_t* unique_id) {
   try {
     if (!d || !unique_id) throw std::runtime_error("pm_create_shard: null argument");
@@ -1070,6 +1053,7 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
         in.nshards = nshards;
         in.shard = q;
         in.comm = pm::make_thread_comm(&grp, static_cast<int>(q));
+        in.inprocess_shards = nshards;
         ctx = pm::create_ctx(in, pattern_dir, device);
         if (labels) {
           ctx->labels_host.assign(labels, labels + n);

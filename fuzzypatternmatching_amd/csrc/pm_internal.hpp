@@ -52,7 +52,7 @@ struct LineArgs {
   int32_t C;            // cycle length: walk positions 0..C+1
   int32_t VC;           // valid cycle (expect target vertex)
   uint16_t ilast;       // pattern_indices.back()
-  uint16_t pad;
+  uint16_t sv;          // pattern_selected_vertices (nem_1.hpp:155-170, 409-436, 697-719)
 };
 
 // Collectives between the shards of one sharded search.  All
@@ -65,6 +65,11 @@ struct Comm {
   // recv receives nshards consecutive `bytes` blocks, block g = shard g's send
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   virtual void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) = 0;
+  // all-to-all of variable blocks: block g of send (sbytes[g] bytes, blocks
+  // consecutive) goes to shard g; recv holds the blocks from shards 0..G-1
+  // consecutively (rbytes[g] from shard g).  Host byte counts, device buffers.
+  virtual void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
+                         hipStream_t s) = 0;
 };
 
 // Device scratch arena (bump allocator, reset per NLC line).
@@ -201,15 +206,15 @@ struct Ctx {
   uint64_t ss0_trav_all = 0;      // ss0_trav summed over the shards
 
   // sharding: shard `shard` of `nshards` owns the rows of ids v % nshards ==
-  // shard (superstep-0 scans, M rows, LCC updates, NLCC sources); T_pub is
-  // replicated and refreshed after every state change by an all-gather of
-  // the owned slist entries, and before token passing the alive M rows of S
-  // are all-gathered into the remote region of d_mcol (rows of other shards'
-  // vertices then start there: d_offp of a remote position is overwritten).
+  // shard (superstep-0 scans, M rows, LCC updates, NLCC sources and every
+  // token / walk at such a vertex); T_pub is replicated and refreshed after
+  // every state change by an all-gather of the owned slist entries; NLCC
+  // tokens and TDS walks move to the owner of their next vertex after every
+  // position (shard_route: one all-to-all per position).
   uint32_t nshards = 1, shard = 0;
   Comm* comm = nullptr;
   Comm* comm_owned = nullptr;     // deleted with the context
-  uint64_t mcap = 0;              // capacity (entries) of d_colp and d_mcol: nq + remote region
+  uint64_t mcap = 0;              // capacity (entries) of d_colp and d_mcol (nq; + kTileEntries tail padding)
   uint32_t xmaxS = 0;             // max |slist| over shards (exchange block size)
   std::vector<uint32_t> xnS;      // |slist| per shard
   uint32_t* d_xslist = nullptr;   // nshards x xmaxS slist positions of every shard
@@ -218,19 +223,6 @@ struct Ctx {
   uint16_t* d_xrecv = nullptr;    // nshards x xmaxS
   uint64_t* d_xred = nullptr;     // host-vector all-reduce staging
   size_t xred_cap = 0;
-  bool m_dirty = true;            // M changed since the last replication
-  // S members of every shard at the last M replication (superset of S during
-  // token passing): the per-line T_pub exchange covers these only
-  uint32_t amax = 0;              // max |S list| over shards
-  std::vector<uint32_t> anum;     // |S list| per shard
-  uint32_t* d_aown = nullptr;     // this shard's S positions (amax)
-  uint32_t* d_axl = nullptr;      // nshards x amax
-  uint32_t* d_anum = nullptr;     // per shard (device)
-  uint16_t* d_asend = nullptr;    // amax
-  uint16_t* d_arecv = nullptr;    // nshards x amax
-  size_t acap = 0;
-  LineStats* d_lstats_loc = nullptr;  // this shard's copy of a summed line
-  bool any_overflow = false;
 
   // host side of the driver loop
   uint64_t* h_pin = nullptr;      // pinned staging for counter / line-stat read-backs
@@ -293,7 +285,14 @@ struct Ctx {
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
   bool force_pull = false;        // PM_FORCE_PULL=1 (diagnostics): pull-form LCC in every call
 
-  // last token-passing call
+  // token-source sets (vertex_token_source_set, nem_1.hpp:131-139, 270-285) of
+  // the last path line as sorted (source << 32 | vertex) keys: a
+  // selected-vertices line starts from the entries of active vertices with its
+  // last label (beta.cpp:823-850); every other line starts empty
+  unsigned long long* d_pseen = nullptr;
+  uint64_t npseen = 0, pseen_cap = 0;
+
+  // last token-passing call (selected-vertices lines: the vertices verified)
   uint32_t* d_sources = nullptr;
   uint64_t nsources = 0;
   std::vector<std::vector<std::string>> walk_lines;  // per rank, last TDS line
@@ -350,11 +349,6 @@ struct FusedLineOut {
   TpResult tr;
   uint32_t deleted = 0;
   std::vector<uint64_t> rm_v, rm_e;
-  // sum_shards: tr / deleted / grm_* are the sums over the shards, ltr /
-  // ldeleted / rm_* this shard's own values (equal otherwise)
-  TpResult ltr;
-  uint32_t ldeleted = 0;
-  std::vector<uint64_t> grm_v, grm_e;
   std::vector<uint32_t> walks;  // kept TDS walks (positions), when requested
   uint32_t stride = 0;
 };
@@ -362,14 +356,10 @@ struct FusedLineOut {
 // outs).  It stops after a line that deleted with interleave_lp set, or before
 // a line that overflowed (overflow = true: rerun that line on the exact-count
 // path).
-// max_lines bounds the lines of one launch (sharded searches run one line per
-// launch: the shards exchange T_pub between lines).
-// sum_shards (sharded, one line): the line's statistics are summed over the
-// shards and the T_pub of every shard's S members exchanged on the stream
-// before the single host synchronisation; c.any_overflow reports an overflow
-// on any shard (overflow: on this one).
+// max_lines bounds the lines of one launch.  One shard only (sharded searches
+// run the per-position path with token exchange).
 size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
-                       size_t max_lines = SIZE_MAX, bool sum_shards = false);
+                       size_t max_lines = SIZE_MAX);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);
@@ -381,9 +371,10 @@ uint64_t* pinned(Ctx& c, size_t words);  // pinned host staging (pm_api.hip)
 // Shard exchanges (pm_shard.hip); no-ops when nshards == 1.
 void shard_after_first(Ctx& c);      // after superstep 0: slists of all shards + T_pub
 void shard_exchange_tpub(Ctx& c);    // T_pub of every shard's slist entries
-void shard_replicate_m(Ctx& c);      // alive M rows of S into the remote region (if m_dirty), S lists
-void shard_exchange_tpub_s(Ctx& c);  // T_pub of every shard's S list (token-passing phase)
 std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  // host vector, sum
+// Owner-bucketed all-to-all of n records of `words` u32 (destination: owner
+// of the position in word kw); returns the records received (arena memory).
+uint32_t* shard_route(Ctx& c, const uint32_t* items, uint64_t n, int words, int kw, uint64_t& nout);
 // Variable-size gather of a host u32 vector: every shard receives all blocks.
 std::vector<std::vector<uint32_t>> shard_allgatherv(Ctx& c, const std::vector<uint32_t>& v);
 

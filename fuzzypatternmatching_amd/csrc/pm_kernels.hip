@@ -1456,6 +1456,7 @@ LineArgs make_line_args(const Ctx& c, const NlcLine& line) {
   la.C = static_cast<int32_t>(line.cycle_length);
   la.VC = line.valid_cycle ? 1 : 0;
   la.ilast = static_cast<uint16_t>(line.indices.back());
+  la.sv = line.selected_vertices ? 1 : 0;
   for (int k = 0; k < n; ++k) {
     la.I[k] = static_cast<uint16_t>(line.indices[k]);
     const uint64_t t = line.indices[k];
@@ -1474,9 +1475,18 @@ struct SourcePred {
   __device__ bool operator()(uint32_t u) const {
     const uint16_t T = tpub[u];
     if (!T || !pos_ok(T, 0, la)) return false;
-    if (!tds && !la.VC && !((T >> la.ilast) & 1u)) return false;
+    if (!tds && !la.VC && !la.sv && !((T >> la.ilast) & 1u)) return false;
     return true;
   }
+};
+
+// Selected-vertices lines verify the active vertices with the line's last
+// label (nem_1.hpp:409-436; they initiate no tokens).
+struct DestPred {
+  const uint16_t* tpub;
+  const uint64_t* labs;
+  uint64_t last;
+  __device__ bool operator()(uint32_t u) const { return tpub[u] != 0 && labs[u] == last; }
 };
 
 __global__ void k_mark_sources(const uint32_t* __restrict__ sources, const int* __restrict__ nsrc,
@@ -1609,20 +1619,37 @@ __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, con
 
 // Terminal position C+1 (nem_1.hpp:661-791): path -> ack the source when the
 // walk does not end on it; cycle -> mark the source and the closing edge.
+// Acknowledgement of source s (tsm[s] = 2).  Sharded: a source owned by
+// another shard is appended to `acks` instead (routed to its owner after the
+// terminal step).
+struct AckSink {
+  const uint32_t* perm;
+  uint32_t G, me;
+  uint32_t* acks;
+  unsigned long long* nacks;
+};
+__device__ __forceinline__ void ack_source(uint32_t s, uint8_t* tsm, const AckSink& a) {
+  if (a.G > 1 && perm_owner(a.perm, s, a.G) != a.me) {
+    a.acks[atomicAdd(a.nacks, 1ull)] = s;
+  } else {
+    tsm[s] = 2;
+  }
+}
+
 __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts,
                               const uint32_t* __restrict__ tp, uint64_t ntok, LineArgs la,
                               const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
                               uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
-                              const uint32_t* __restrict__ perm, uint8_t* __restrict__ tsm) {
+                              const uint32_t* __restrict__ perm, uint8_t* __restrict__ tsm, AckSink ak) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntok; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = tu[i], s = ts[i];
     if (!pos_ok(tpub[u], la.C + 1, la)) continue;
     if (!la.VC) {
       if (u == s) continue;
-      if (tpub[s]) tsm[s] = 2;  // ack visitor needs an active source (nem_1.hpp:101, :326-336)
+      if (tpub[s]) ack_source(s, tsm, ak);  // ack visitor needs an active source (nem_1.hpp:101, :326-336)
     } else {
       if (u != s) continue;
-      tsm[s] = 2;
+      tsm[s] = 2;  // u == s: this shard owns s
       // mark M[s][parent]: rows hold positions in neighbour-id order
       const uint32_t p = tp[i], pid = perm[p];
       uint64_t lo = offp[s], hi = offp[s] + mlen[s];
@@ -1635,7 +1662,49 @@ __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* _
   }
 }
 
-// ---- TDS ----------------------------------------------------------------
+// Selected-vertices terminal (nem_1.hpp:680-719): a path reaching a verified
+// vertex u from source s confirms u iff s is in u's token-source set.  The
+// reference registers u when its own init visit runs and, on one rank, drains
+// every source's tokens before visiting the next vertex
+// (visitor_queue.hpp:221-251): u is registered for s's tokens iff id(u) <
+// id(s) ("selected vertices").
+__global__ void k_tp_terminal_sv(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts, uint64_t ntok,
+                                 LineArgs la, const uint16_t* __restrict__ tpub, const uint32_t* __restrict__ perm,
+                                 uint8_t* __restrict__ tsm, SeenSet seen) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntok; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t u = tu[i], s = ts[i];
+    if (u == s || !pos_ok(tpub[u], la.C + 1, la)) continue;
+    if (tsm[u] == 0 || perm[u] >= perm[s]) continue;  // not a registered selected vertex yet
+    const unsigned long long key = (static_cast<unsigned long long>(s) << 32) | u;
+    bool found = false;
+    for (int l = 0; l < seen.count && !found; ++l) found = sorted_contains(seen.keys[l], seen.n[l], key);
+    if (found) tsm[u] = 2;
+  }
+}
+
+__global__ void k_set_acked(const uint32_t* __restrict__ acks, uint64_t n, uint8_t* __restrict__ tsm) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    tsm[acks[i]] = 2;
+}
+
+// Tokens (u, s, p) between the three-array form and interleaved records.
+__global__ void k_tok_pack(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts,
+                           const uint32_t* __restrict__ tp, uint64_t n, uint32_t* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    out[3 * i] = tu[i];
+    out[3 * i + 1] = ts[i];
+    out[3 * i + 2] = tp[i];
+  }
+}
+__global__ void k_tok_unpack(const uint32_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ tu,
+                             uint32_t* __restrict__ ts, uint32_t* __restrict__ tp) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    tu[i] = in[3 * i];
+    ts[i] = in[3 * i + 1];
+    tp[i] = in[3 * i + 2];
+  }
+}
+
 __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
                            const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
                            const uint32_t* __restrict__ mlen, int stride,
@@ -1702,7 +1771,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
 // Terminal position C+1 (tds_batch_1.hpp:641-758).
 __global__ void k_tds_terminal(const uint32_t* __restrict__ win, uint64_t nw, int stride, LineArgs la,
                                const uint16_t* __restrict__ tpub, uint8_t* __restrict__ tsm,
-                               uint8_t* __restrict__ keep) {
+                               uint8_t* __restrict__ keep, AckSink ak) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nw; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t* w = win + i * stride;
     const int k = la.C + 1;
@@ -1712,7 +1781,7 @@ __global__ void k_tds_terminal(const uint32_t* __restrict__ win, uint64_t nw, in
       if (!la.VC) {
         if (u != s) {
           kp = 1;
-          if (tpub[s]) tsm[s] = 2;
+          if (tpub[s]) ack_source(s, tsm, ak);
         }
       } else if (u == s) {
         kp = 1;
@@ -1722,8 +1791,6 @@ __global__ void k_tds_terminal(const uint32_t* __restrict__ win, uint64_t nw, in
     keep[i] = kp;
   }
 }
-
-// Post-processing of unacked sources (beta.cpp:964-1000).
 __global__ void k_tp_post(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint8_t* __restrict__ tsm,
                           uint16_t* __restrict__ tpub, int i0, unsigned long long* __restrict__ out) {
   uint64_t acked = 0, deleted = 0;
@@ -1772,61 +1839,206 @@ static uint64_t exclusive_scan_u32_to_u64(Ctx& c, const uint32_t* in, uint64_t* 
   return total;
 }
 
-static void ensure_sources(Ctx& c, const LineArgs& la, int tds, unsigned long long* d_nsrc) {
+// d_sources / c.nsources: the token_source_map keys of the line (marked 1 in
+// tsm): its sources, or for a selected-vertices line the vertices it
+// verifies, whose token initiators are returned in *init / *ninit (arena).
+static void ensure_sources(Ctx& c, const LineArgs& la, int tds, const NlcLine& line, uint32_t** init = nullptr,
+                           uint64_t* ninit = nullptr) {
   // previous line's sources are cleared from tsm first
   if (c.d_sources && c.nsources) {
     hipLaunchKernelGGL(k_clear_tsm, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
                        c.nsources, c.d_tsm);
   }
-  (void)d_nsrc;
   SourcePred pred{c.d_tpub[c.cur], la, tds};
-  int* d_ns = arena_alloc<int>(c, 1);
-  size_t tmp = 0;
+  DestPred dpred{c.d_tpub[c.cur], c.d_labs, line.labels.back()};
+  int* d_ns = arena_alloc<int>(c, 2);
+  uint32_t* ilist = la.sv ? arena_alloc<uint32_t>(c, std::max<uint32_t>(c.nS_host, 1)) : nullptr;
+  size_t tmp = 0, tmp2 = 0;
   const int nitems = static_cast<int>(std::max<uint32_t>(c.nS_host, 1));
-  PM_HIP_CHECK(hipMemsetAsync(d_ns, 0, sizeof(int), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(d_ns, 0, 2 * sizeof(int), c.stream));
   if (c.nS_host) {
     PM_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
-    void* d_tmp = c.arena.get(tmp);
-    PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
+    PM_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp2, c.d_slist, c.d_sources, d_ns, nitems, dpred, c.stream));
+    void* d_tmp = c.arena.get(std::max(tmp, tmp2));
+    if (la.sv) {
+      PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp, c.d_slist, ilist, d_ns + 1, nitems, pred, c.stream));
+      tmp2 = std::max(tmp, tmp2);
+      PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp2, c.d_slist, c.d_sources, d_ns, nitems, dpred, c.stream));
+    } else {
+      PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
+    }
     hipLaunchKernelGGL(k_mark_sources, dim3(grid_for(c.nS_host, kBlock, 1024)), dim3(kBlock), 0, c.stream,
                        c.d_sources, d_ns, c.d_tsm);
     PM_HIP_CHECK(hipGetLastError());
   }
-  int ns = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(&ns, d_ns, sizeof(ns), hipMemcpyDeviceToHost, c.stream));
+  int ns[2] = {0, 0};
+  PM_HIP_CHECK(hipMemcpyAsync(ns, d_ns, sizeof(ns), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  c.nsources = static_cast<uint64_t>(ns);
+  c.nsources = static_cast<uint64_t>(ns[0]);
+  if (init) {
+    *init = la.sv ? ilist : c.d_sources;
+    *ninit = la.sv ? static_cast<uint64_t>(ns[1]) : c.nsources;
+  }
+}
+
+// Token-source sets across lines: the start of a line keeps (selected-vertices
+// line) or drops (any other line) the previous line's entries.
+__global__ void k_pseen_keep(const unsigned long long* __restrict__ keys, uint64_t n, const uint16_t* __restrict__ tpub,
+                             const uint64_t* __restrict__ labs, uint64_t last, uint8_t* __restrict__ keep) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t u = static_cast<uint32_t>(keys[i] & 0xFFFFFFFFull);
+    keep[i] = tpub[u] != 0 && labs[u] == last;
+  }
+}
+
+static uint64_t pseen_start(Ctx& c, const NlcLine& line, const unsigned long long** out) {
+  *out = nullptr;
+  if (!line.selected_vertices || c.npseen == 0) return 0;
+  auto* keep = arena_alloc<uint8_t>(c, c.npseen);
+  auto* kept = arena_alloc<unsigned long long>(c, c.npseen);
+  auto* d_n = arena_alloc<int>(c, 1);
+  hipLaunchKernelGGL(k_pseen_keep, dim3(grid_for(c.npseen, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_pseen,
+                     c.npseen, c.d_tpub[c.cur], c.d_labs, line.labels.back(), keep);
+  size_t tmp = 0;
+  PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, tmp, c.d_pseen, keep, kept, d_n, static_cast<int>(c.npseen),
+                                             c.stream));
+  void* d_tmp = c.arena.get(tmp);
+  PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(d_tmp, tmp, c.d_pseen, keep, kept, d_n, static_cast<int>(c.npseen),
+                                             c.stream));
+  int n = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&n, d_n, sizeof(n), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  *out = kept;
+  return static_cast<uint64_t>(n);
+}
+
+// End of a line: the sets become the line's start entries plus every
+// (source, vertex) a relay accepted during the line (sorted, unique).
+static void pseen_end(Ctx& c, const SeenSet& seen) {
+  uint64_t total = 0;
+  for (int l = 0; l < seen.count; ++l) total += seen.n[l];
+  c.npseen = 0;
+  if (!total) return;
+  auto* cat = arena_alloc<unsigned long long>(c, total);
+  uint64_t o = 0;
+  for (int l = 0; l < seen.count; ++l) {
+    if (seen.n[l])
+      PM_HIP_CHECK(hipMemcpyAsync(cat + o, seen.keys[l], seen.n[l] * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToDevice, c.stream));
+    o += seen.n[l];
+  }
+  auto* sorted = arena_alloc<unsigned long long>(c, total);
+  size_t tmp = 0;
+  PM_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, cat, sorted, static_cast<int>(total), 0, 64, c.stream));
+  void* d_tmp = c.arena.get(tmp);
+  PM_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp, cat, sorted, static_cast<int>(total), 0, 64, c.stream));
+  if (c.pseen_cap < total) {
+    if (c.d_pseen) (void)hipFree(c.d_pseen);
+    c.pseen_cap = std::max<uint64_t>(total, 2 * c.pseen_cap);
+    PM_HIP_CHECK(hipMalloc(&c.d_pseen, c.pseen_cap * sizeof(unsigned long long)));
+  }
+  auto* d_n = arena_alloc<int>(c, 1);
+  tmp = 0;
+  PM_HIP_CHECK(hipcub::DeviceSelect::Unique(nullptr, tmp, sorted, c.d_pseen, d_n, static_cast<int>(total), c.stream));
+  d_tmp = c.arena.get(tmp);
+  PM_HIP_CHECK(hipcub::DeviceSelect::Unique(d_tmp, tmp, sorted, c.d_pseen, d_n, static_cast<int>(total), c.stream));
+  int n = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&n, d_n, sizeof(n), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  c.npseen = static_cast<uint64_t>(n);
+}
+
+// Sharded searches: tokens and walks travel to the shard owning their next
+// vertex after every position (shard_route: one all-to-all per position, the
+// BSP form of the visitor queue's mailbox), so that the (vertex, source)
+// dedup, M[u] and the terminal checks are always local; acknowledgements of
+// another shard's source travel to its owner after the terminal step.
+static void route_tokens(Ctx& c, uint32_t*& tu, uint32_t*& ts, uint32_t*& tp, uint64_t& ntok) {
+  if (!c.comm) return;
+  auto* rec = arena_alloc<uint32_t>(c, std::max<uint64_t>(ntok, 1) * 3);
+  if (ntok)
+    hipLaunchKernelGGL(k_tok_pack, dim3(grid_for(ntok, kBlock, 4096)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
+                       rec);
+  uint64_t nr = 0;
+  const uint32_t* got = shard_route(c, rec, ntok, 3, 0, nr);
+  tu = arena_alloc<uint32_t>(c, std::max<uint64_t>(nr, 1));
+  ts = arena_alloc<uint32_t>(c, std::max<uint64_t>(nr, 1));
+  tp = arena_alloc<uint32_t>(c, std::max<uint64_t>(nr, 1));
+  if (nr)
+    hipLaunchKernelGGL(k_tok_unpack, dim3(grid_for(nr, kBlock, 4096)), dim3(kBlock), 0, c.stream, got, nr, tu, ts, tp);
+  PM_HIP_CHECK(hipGetLastError());
+  ntok = nr;
+}
+
+static AckSink ack_sink(Ctx& c, uint64_t cap) {
+  AckSink a{c.d_perm, c.comm ? c.nshards : 1u, c.shard, nullptr, nullptr};
+  if (c.comm) {
+    a.nacks = arena_alloc<unsigned long long>(c, 1);
+    a.acks = arena_alloc<uint32_t>(c, cap);
+    PM_HIP_CHECK(hipMemsetAsync(a.nacks, 0, sizeof(unsigned long long), c.stream));
+  }
+  return a;
+}
+
+static void route_acks(Ctx& c, const AckSink& a) {
+  if (!c.comm) return;
+  unsigned long long n = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&n, a.nacks, sizeof(n), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  uint64_t nr = 0;
+  const uint32_t* got = shard_route(c, a.acks, n, 1, 0, nr);
+  if (nr)
+    hipLaunchKernelGGL(k_set_acked, dim3(grid_for(nr, kBlock, 4096)), dim3(kBlock), 0, c.stream, got, nr, c.d_tsm);
+  PM_HIP_CHECK(hipGetLastError());
 }
 
 TpResult run_path_line(Ctx& c, const NlcLine& line) {
   TpResult res;
   c.arena.reset();
+  const bool sharded = c.comm != nullptr;
   const LineArgs la = make_line_args(c, line);
-  auto* d_nsrc = arena_alloc<unsigned long long>(c, 2);
-  auto* d_trav = d_nsrc + 1;
-  PM_HIP_CHECK(hipMemsetAsync(d_nsrc, 0, 2 * sizeof(unsigned long long), c.stream));
-  ensure_sources(c, la, 0, d_nsrc);
+  auto* d_trav = arena_alloc<unsigned long long>(c, 1);
+  PM_HIP_CHECK(hipMemsetAsync(d_trav, 0, sizeof(unsigned long long), c.stream));
+  SeenSet seen{};
+  seen.count = 0;
+  const unsigned long long* p0 = nullptr;
+  const uint64_t np0 = pseen_start(c, line, &p0);  // the token-source sets this line starts from
+  if (np0) {
+    seen.keys[0] = p0;
+    seen.n[0] = np0;
+    seen.count = 1;
+  }
+  uint32_t* init = nullptr;  // token initiators
+  uint64_t ninit = 0;
+  ensure_sources(c, la, 0, line, &init, &ninit);
   res.sources = c.nsources;
-  if (c.nsources == 0) return res;
+  if (ninit == 0 && !sharded) {
+    pseen_end(c, seen);
+    return res;
+  }
   const uint16_t* tpub = c.d_tpub[c.cur];
   // level 1 tokens
-  auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
-  auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
-  hipLaunchKernelGGL(k_row_alive, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, 1, 0, c.d_offp, c.d_malive, cnt);
-  uint64_t ntok = exclusive_scan_u32_to_u64(c, cnt, obase, c.nsources);
+  auto* cnt = arena_alloc<uint32_t>(c, ninit);
+  auto* obase = arena_alloc<uint64_t>(c, ninit + 1);
+  hipLaunchKernelGGL(k_row_alive, dim3(grid_for(ninit, kBlock, 4096)), dim3(kBlock), 0, c.stream, init, ninit, 1, 0,
+                     c.d_offp, c.d_malive, cnt);
+  uint64_t ntok = exclusive_scan_u32_to_u64(c, cnt, obase, ninit);
   uint64_t trav_init = ntok;  // sources scan all of M[s]
   auto* tu = arena_alloc<uint32_t>(c, ntok);
   auto* ts = arena_alloc<uint32_t>(c, ntok);
   auto* tp = arena_alloc<uint32_t>(c, ntok);
-  hipLaunchKernelGGL(k_tp_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mlen, tu, ts, tp);
+  hipLaunchKernelGGL(k_tp_init, dim3(grid_for(ninit, kBlock, 4096)), dim3(kBlock), 0, c.stream, init, ninit, obase,
+                     c.d_offp, c.d_mcol, c.d_mlen, tu, ts, tp);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += ntok;
-  SeenSet seen{};
-  seen.count = 0;
+  route_tokens(c, tu, ts, tp, ntok);
   const int C = la.C;
-  for (int k = 1; k <= C && ntok > 0; ++k) {
+  // sharded: every shard runs every position (the token exchange is collective)
+  for (int k = 1; k <= C && (ntok > 0 || sharded); ++k) {
+    if (ntok == 0) {  // sharded, nothing here at this position: take part in the exchange
+      route_tokens(c, tu, ts, tp, ntok);
+      continue;
+    }
     auto* keys = arena_alloc<unsigned long long>(c, ntok);
     hipLaunchKernelGGL(k_tp_filter, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, ntok, k,
                        la, tpub, keys);
@@ -1862,7 +2074,9 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     }
     if (nf == 0) {
       ntok = 0;
-      break;
+      if (!sharded) break;
+      route_tokens(c, tu, ts, tp, ntok);
+      continue;
     }
     auto* ecnt = arena_alloc<uint32_t>(c, nf);
     hipLaunchKernelGGL(k_tp_expand_count, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf,
@@ -1877,12 +2091,20 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     PM_HIP_CHECK(hipGetLastError());
     ntok = nnext;
     res.tokens += ntok;
+    route_tokens(c, tu, ts, tp, ntok);  // to the owners of the next vertices
   }
-  if (ntok > 0) {
+  AckSink ak = ack_sink(c, std::max<uint64_t>(ntok, 1));
+  if (ntok > 0 && la.sv) {  // the terminal vertex is verified here (tokens were routed to its owner)
+    hipLaunchKernelGGL(k_tp_terminal_sv, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, ntok,
+                       la, tpub, c.d_perm, c.d_tsm, seen);
+    PM_HIP_CHECK(hipGetLastError());
+  } else if (ntok > 0) {
     hipLaunchKernelGGL(k_tp_terminal, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
-                       la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_perm, c.d_tsm);
+                       la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_perm, c.d_tsm, ak);
     PM_HIP_CHECK(hipGetLastError());
   }
+  route_acks(c, ak);
+  pseen_end(c, seen);
   unsigned long long trav = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&trav, d_trav, sizeof(trav), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -1900,12 +2122,13 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   walks_out.clear();
   if (line.enumeration.size() < static_cast<size_t>(stride))
     throw std::runtime_error("pattern_non_local_constraint enumeration shorter than the TDS walk");
-  auto* d_nsrc = arena_alloc<unsigned long long>(c, 2);
-  auto* d_trav = d_nsrc + 1;
-  PM_HIP_CHECK(hipMemsetAsync(d_nsrc, 0, 2 * sizeof(unsigned long long), c.stream));
-  ensure_sources(c, la, 1, d_nsrc);
+  auto* d_trav = arena_alloc<unsigned long long>(c, 1);
+  PM_HIP_CHECK(hipMemsetAsync(d_trav, 0, sizeof(unsigned long long), c.stream));
+  c.npseen = 0;  // token-source sets are dropped at the start of a non-selected line (beta.cpp:791-793)
+  ensure_sources(c, la, 1, line);
   res.sources = c.nsources;
-  if (c.nsources == 0) return res;
+  const bool sharded = c.comm != nullptr;
+  if (c.nsources == 0 && !sharded) return res;
   const uint16_t* tpub = c.d_tpub[c.cur];
   auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
   auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
@@ -1918,7 +2141,12 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
                      c.nsources, obase, c.d_offp, c.d_mcol, c.d_mlen, stride, walks);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += nw;
-  for (int k = 1; k <= C && nw > 0; ++k) {
+  if (sharded) walks = shard_route(c, walks, nw, stride, 1, nw);  // to the owners of the walks' last vertices
+  for (int k = 1; k <= C && (nw > 0 || sharded); ++k) {
+    if (nw == 0) {
+      walks = shard_route(c, walks, 0, stride, k + 1, nw);
+      continue;
+    }
     auto* wc = arena_alloc<uint32_t>(c, nw);
     hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
                        stride, la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, wc,
@@ -1934,11 +2162,13 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
     walks = wn;
     nw = nnext;
     res.tokens += nw;
+    if (sharded) walks = shard_route(c, walks, nw, stride, k + 1, nw);
   }
+  AckSink ak = ack_sink(c, std::max<uint64_t>(nw, 1));
   if (nw > 0) {
     auto* keep = arena_alloc<uint8_t>(c, nw);
     hipLaunchKernelGGL(k_tds_terminal, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, stride,
-                       la, tpub, c.d_tsm, keep);
+                       la, tpub, c.d_tsm, keep, ak);
     PM_HIP_CHECK(hipGetLastError());
     std::vector<uint32_t> all(nw * stride);
     std::vector<uint8_t> kp(nw);
@@ -1948,6 +2178,7 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
     for (uint64_t i = 0; i < nw; ++i)
       if (kp[i]) walks_out.insert(walks_out.end(), all.begin() + i * stride, all.begin() + (i + 1) * stride);
   }
+  route_acks(c, ak);
   res.walks = walks_out.size() / stride;
   unsigned long long trav = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&trav, d_trav, sizeof(trav), hipMemcpyDeviceToHost, c.stream));
@@ -1961,7 +2192,8 @@ uint32_t launch_post_tp(Ctx& c, const NlcLine& line) {
   auto* out = arena_alloc<unsigned long long>(c, 2);
   PM_HIP_CHECK(hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), c.stream));
   hipLaunchKernelGGL(k_tp_post, dim3(grid_for(c.nsources, kBlock, 1024)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, c.d_tsm, c.d_tpub[c.cur], static_cast<int>(line.indices[0]), out);
+                     c.nsources, c.d_tsm, c.d_tpub[c.cur],
+                     static_cast<int>(line.selected_vertices ? line.indices.back() : line.indices[0]), out);
   PM_HIP_CHECK(hipGetLastError());
   unsigned long long h[2] = {0, 0};
   PM_HIP_CHECK(hipMemcpyAsync(h, out, sizeof(h), hipMemcpyDeviceToHost, c.stream));

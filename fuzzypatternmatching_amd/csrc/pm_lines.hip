@@ -781,9 +781,8 @@ static void upload_lines(Ctx& c) {
 }
 
 size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
-                       size_t max_lines, bool sum_shards) {
-  sum_shards = sum_shards && c.comm;
-  if (sum_shards) max_lines = 1;
+                       size_t max_lines) {
+  if (c.comm) throw std::runtime_error("internal: fused lines run on one shard only");
   c.probe("lines entry");
   const size_t nl_all = c.pattern.lines.size();
   const size_t nl = pl0 < nl_all && max_lines < nl_all - pl0 ? pl0 + max_lines : nl_all;
@@ -863,26 +862,18 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(grid),
                                           dim3(kLineBlock), args, 0, c.stream));
   c.probe("lines launched");
-  // read-back through pinned memory: [done | kept slots | line stats | summed stats]
-  static_assert(sizeof(LineStats) % 8 == 0, "LineStats is summed as u64 words");
+  // read-back through pinned memory: [done | kept slots | line stats]
+  static_assert(sizeof(LineStats) % 8 == 0, "LineStats is read back as u64 words");
   const size_t sw = sizeof(LineStats) / 8;
-  uint64_t* pin = pinned(c, 2 + 2 * (nl - pl0) * sw);
+  uint64_t* pin = pinned(c, 2 + (nl - pl0) * sw);
   PM_HIP_CHECK(hipMemcpyAsync(pin, d_done, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1, d_kept_ctr, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipMemcpyAsync(pin + 2, c.d_lstats + pl0, (nl - pl0) * sizeof(LineStats), hipMemcpyDeviceToHost,
                               c.stream));
-  if (sum_shards) {  // the line's sums over the shards and every shard's post-processed T_pub, on the stream
-    c.comm->allreduce_sum_u64(reinterpret_cast<uint64_t*>(c.d_lstats + pl0), sw, c.stream);
-    PM_HIP_CHECK(hipMemcpyAsync(pin + 2 + sw, c.d_lstats + pl0, sizeof(LineStats), hipMemcpyDeviceToHost, c.stream));
-    shard_exchange_tpub_s(c);
-  }
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("lines synced");
   std::vector<LineStats> hs(nl - pl0);
   std::memcpy(hs.data(), pin + 2, hs.size() * sizeof(LineStats));
-  LineStats gs{};
-  if (sum_shards) std::memcpy(&gs, pin + 2 + sw, sizeof(LineStats));
-  c.any_overflow = sum_shards ? gs.overflow != 0 : false;
   const unsigned done = static_cast<unsigned>(pin[0] & 0xFFFFFFFFull);
   const unsigned long long kept_slots = pin[1];
   std::vector<uint32_t> kept;
@@ -921,29 +912,18 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
       break;
     }
     FusedLineOut out;
-    const LineStats& gl = sum_shards ? gs : st;
-    out.ltr.sources = st.nsrc;
-    out.ltr.acked = st.acked;
-    out.ltr.edges = st.trav;
-    out.ltr.tokens = st.tokens;
-    out.ltr.walks = st.walks;
-    out.ldeleted = st.deleted ? 1u : 0u;
-    out.tr.sources = gl.nsrc;
-    out.tr.acked = gl.acked;
-    out.tr.edges = gl.trav;
-    out.tr.tokens = gl.tokens;
-    out.tr.walks = gl.walks;
-    out.deleted = gl.deleted ? 1u : 0u;
+    out.tr.sources = st.nsrc;
+    out.tr.acked = st.acked;
+    out.tr.edges = st.trav;
+    out.tr.tokens = st.tokens;
+    out.tr.walks = st.walks;
+    out.deleted = st.deleted ? 1u : 0u;
     c.last_acked = st.acked;
     out.rm_v.assign(c.nranks, 0);
     out.rm_e.assign(c.nranks, 0);
-    out.grm_v.assign(c.nranks, 0);
-    out.grm_e.assign(c.nranks, 0);
     for (uint32_t r = 0; r < c.nranks; ++r) {
       out.rm_v[r] = st.removed[r];
       out.rm_e[r] = st.removed[P + r];
-      out.grm_v[r] = gl.removed[r];
-      out.grm_e[r] = gl.removed[P + r];
     }
     out.stride = static_cast<uint32_t>(c.pattern.lines[pl].cycle_length + 2);
     if (pl >= 4 && want_walks && st.walks) {

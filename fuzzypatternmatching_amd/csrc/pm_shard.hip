@@ -9,10 +9,11 @@
 //   * LCC: every row pulls its neighbours' T_pub, so after each superstep the
 //     shards all-gather the T_pub of their slist entries (the only vertices
 //     that can be in S) -- 2 B per entry, no per-edge messages;
-//   * NLCC: walks are independent per source (the (vertex, source) dedup of
-//     nem_1.hpp:131-139 and TDS walks never mix sources), so each shard runs
-//     the walks of its own sources over an all-gathered copy of the alive M
-//     rows of S (small after the first LCC call) and the replicated T_pub;
+//   * NLCC / TDS: after every walk position the tokens (vertex, source,
+//     parent) and walks move to the owner of their next vertex in one RCCL
+//     all-to-all (shard_route: ncclSend / ncclRecv pairs in a group), so the
+//     (vertex, source) dedup of nem_1.hpp:131-139, M[u] and the terminal
+//     checks stay local; acknowledgements travel to the source's owner;
 //   * counters and flags: one u64 sum all-reduce per LCC call / NLC line.
 // Results are identical for every shard count.
 
@@ -66,6 +67,23 @@ class RcclComm : public Comm {
     if (nranks_ == 1) return;
     PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm_, s));
   }
+  // grouped point-to-point sends / receives over xGMI (one pair per peer)
+  void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
+                 hipStream_t s) override {
+    if (nranks_ == 1) {
+      if (sbytes[0]) PM_HIP_CHECK(hipMemcpyAsync(recv, send, sbytes[0], hipMemcpyDeviceToDevice, s));
+      return;
+    }
+    uint64_t so = 0, ro = 0;
+    PM_NCCL_CHECK(ncclGroupStart());
+    for (int g = 0; g < nranks_; ++g) {
+      if (sbytes[g]) PM_NCCL_CHECK(ncclSend(static_cast<const char*>(send) + so, sbytes[g], ncclUint8, g, comm_, s));
+      if (rbytes[g]) PM_NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + ro, rbytes[g], ncclUint8, g, comm_, s));
+      so += sbytes[g];
+      ro += rbytes[g];
+    }
+    PM_NCCL_CHECK(ncclGroupEnd());
+  }
 
  private:
   ncclComm_t comm_ = nullptr;
@@ -73,6 +91,36 @@ class RcclComm : public Comm {
 };
 
 Comm* make_rccl_comm(const void* unique_id, int nranks, int rank) { return new RcclComm(unique_id, nranks, rank); }
+
+// Diagnostics: one-rank RCCL collective of `bytes` on `device` (op 0:
+// ncclAllGather, 1: ncclAllReduce u64 sum), result checked; the communicator
+// is created and destroyed here.  Returns 0 when the result is right.
+int rccl_selftest(int device, uint64_t bytes, int op) {
+  PM_HIP_CHECK(hipSetDevice(device));
+  ncclUniqueId id;
+  PM_NCCL_CHECK(ncclGetUniqueId(&id));
+  ncclComm_t comm = nullptr;
+  PM_NCCL_CHECK(ncclCommInitRank(&comm, 1, id, 0));
+  hipStream_t st;
+  PM_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const uint64_t words = std::max<uint64_t>(1, bytes / 8);
+  uint64_t *a = nullptr, *b = nullptr;
+  PM_HIP_CHECK(hipMalloc(&a, words * 8));
+  PM_HIP_CHECK(hipMalloc(&b, words * 8));
+  std::vector<uint64_t> h(words);
+  for (uint64_t i = 0; i < words; ++i) h[i] = i * 0x9E3779B97F4A7C15ull;
+  PM_HIP_CHECK(hipMemcpy(a, h.data(), words * 8, hipMemcpyHostToDevice));
+  if (op == 0) PM_NCCL_CHECK(ncclAllGather(a, b, words * 8, ncclUint8, comm, st));
+  else PM_NCCL_CHECK(ncclAllReduce(a, b, words, ncclUint64, ncclSum, comm, st));
+  PM_HIP_CHECK(hipStreamSynchronize(st));
+  std::vector<uint64_t> r(words);
+  PM_HIP_CHECK(hipMemcpy(r.data(), b, words * 8, hipMemcpyDeviceToHost));
+  (void)hipFree(a);
+  (void)hipFree(b);
+  (void)hipStreamDestroy(st);
+  (void)ncclCommDestroy(comm);
+  return r == h ? 0 : 1;
+}
 
 size_t rccl_unique_id(void* out, size_t len) {
   ncclUniqueId id;
@@ -85,9 +133,10 @@ size_t rccl_unique_id(void* out, size_t len) {
 // ---------------------------------------------------------------------------
 // Threads of one process, all shards on one device (parity tests on a
 // one-GPU box).  Shards compute one at a time (ThreadGroup::device is held
-// outside collectives), so their cooperative line kernels never share the
-// chip; a collective synchronises the caller's stream, releases the device,
-// meets the other shards at a barrier and copies with hipMemcpy.
+// outside collectives), so their kernels never share the chip; a collective
+// synchronises the caller's stream, releases the device, meets the other
+// shards at a barrier and copies with hipMemcpyAsync on the caller's stream
+// (synchronised before the closing barrier).
 void ThreadGroup::barrier() {
   std::unique_lock<std::mutex> lk(m);
   if (aborted) throw std::runtime_error("another shard failed");
@@ -148,6 +197,28 @@ class ThreadComm : public Comm {
     if (count) PM_HIP_CHECK(hipMemcpyAsync(buf, sum.data(), count * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     PM_HIP_CHECK(hipStreamSynchronize(s));
   }
+  void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
+                 hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));
+    DeviceReleased rel(g_);
+    const int G = g_->n;
+    g_->ptrs[rank_] = send;
+    g_->counts[rank_].assign(sbytes, sbytes + G);
+    g_->barrier();
+    uint64_t ro = 0;
+    for (int q = 0; q < G; ++q) {  // block for this rank inside shard q's send buffer
+      uint64_t off = 0;
+      for (int k = 0; k < rank_; ++k) off += g_->counts[q][k];
+      const uint64_t n = g_->counts[q][rank_];
+      if (n != rbytes[q]) throw std::runtime_error("alltoallv: receive size mismatch");
+      if (n)
+        PM_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + ro, static_cast<const char*>(g_->ptrs[q]) + off, n,
+                                    hipMemcpyDeviceToDevice, s));
+      ro += n;
+    }
+    PM_HIP_CHECK(hipStreamSynchronize(s));
+    g_->barrier();
+  }
 
  private:
   ThreadGroup* g_;
@@ -181,77 +252,25 @@ __global__ void k_unpack_tpub(const uint32_t* __restrict__ xslist, const uint32_
   }
 }
 
-// Alive-entry count of each own slist entry in S (0 outside S and past nS).
-__global__ void k_m_counts(const uint32_t* __restrict__ slist, uint32_t nS, uint32_t maxS,
-                           const uint16_t* __restrict__ tpub, const uint32_t* __restrict__ malive,
-                           uint32_t* __restrict__ cnt) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < maxS; i += uint64_t(gridDim.x) * blockDim.x) {
-    uint32_t x = 0;
-    if (i < nS) {
-      const uint32_t s = slist[i];
-      if (tpub[s]) x = malive[s];
-    }
-    cnt[i] = x;
+// Owner-bucketed routing of fixed-size records (the mailbox exchange of
+// new_mailbox.hpp:289-713 as one RCCL all-to-all per BSP step): record i is
+// `words` u32, its destination the owner of the position in word kw.
+__global__ void k_route_count(const uint32_t* __restrict__ items, uint64_t n, int words, int kw,
+                              const uint32_t* __restrict__ perm, uint32_t G, uint32_t* __restrict__ dest,
+                              unsigned long long* __restrict__ cnt) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t g = perm[items[i * words + kw]] % G;
+    dest[i] = g;
+    atomicAdd(&cnt[g], 1ull);
   }
 }
 
-// One wave per own slist entry: the alive entries of M[s], in row order, at
-// out + moff[i] (ballot compaction).
-__global__ __launch_bounds__(kXBlock) void k_m_pack(const uint32_t* __restrict__ slist, uint32_t nS,
-                                                    const uint16_t* __restrict__ tpub,
-                                                    const uint64_t* __restrict__ offp,
-                                                    const uint32_t* __restrict__ mlen,
-                                                    const uint32_t* __restrict__ mcol,
-                                                    const uint64_t* __restrict__ moff, uint32_t* __restrict__ out) {
-  const int lane = lane_id();
-  const uint64_t nw = uint64_t(gridDim.x) * (kXBlock / kWave);
-  for (uint64_t i = blockIdx.x * uint64_t(kXBlock / kWave) + threadIdx.x / kWave; i < nS; i += nw) {
-    const uint32_t s = slist[i];
-    if (!tpub[s]) continue;
-    const uint64_t b = offp[s];
-    const uint32_t L = mlen[s];
-    uint64_t o = moff[i];
-    for (uint32_t j0 = 0; j0 < L; j0 += kWave) {
-      const uint32_t j = j0 + lane;
-      const uint32_t x = j < L ? mcol[b + j] : 0u;
-      const bool alive = (x & kAlive) != 0;
-      const uint64_t bal = __ballot(alive);
-      if (alive) out[o + __builtin_popcountll(bal & ((1ull << lane) - 1))] = x;
-      o += __builtin_popcountll(bal);
-    }
-  }
-}
-
-// Start of each shard's block in the all-gathered counts' exclusive scan.
-__global__ void k_seg_starts(const uint64_t* __restrict__ xoff, uint32_t maxS, uint32_t G, uint64_t* __restrict__ out) {
-  const uint32_t g = threadIdx.x;
-  if (g <= G) out[g] = xoff[uint64_t(g) * maxS];
-}
-
-// Remote rows: offp / mlen / malive of the other shards' slist entries point
-// into the gathered region (block g at base + g * maxT).
-__global__ void k_m_unpack(const uint32_t* __restrict__ xslist, const uint32_t* __restrict__ xnS,
-                           const uint32_t* __restrict__ xcnt, const uint64_t* __restrict__ xoff,
-                           const uint64_t* __restrict__ seg, uint32_t maxS, uint32_t G, uint32_t me, uint64_t base,
-                           uint64_t maxT, uint64_t* __restrict__ offp, uint32_t* __restrict__ mlen,
-                           uint32_t* __restrict__ malive) {
-  const uint64_t total = uint64_t(G) * maxS;
-  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t g = static_cast<uint32_t>(j / maxS), i = static_cast<uint32_t>(j % maxS);
-    if (g == me || i >= xnS[g]) continue;
-    const uint32_t p = xslist[j];
-    offp[p] = base + uint64_t(g) * maxT + (xoff[j] - seg[g]);
-    mlen[p] = xcnt[j];
-    malive[p] = xcnt[j];
-  }
-}
-
-// This shard's S members (slist entries with T_pub != 0), unordered.
-__global__ void k_s_collect(const uint32_t* __restrict__ slist, uint32_t nS, const uint16_t* __restrict__ tpub,
-                            uint32_t* __restrict__ out, unsigned int* __restrict__ ctr) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t p = slist[i];
-    if (tpub[p]) out[atomicAdd(ctr, 1u)] = p;
+__global__ void k_route_scatter(const uint32_t* __restrict__ items, uint64_t n, int words,
+                                const uint32_t* __restrict__ dest, unsigned long long* __restrict__ cursor,
+                                uint32_t* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t o = atomicAdd(&cursor[dest[i]], 1ull);
+    for (int w = 0; w < words; ++w) out[o * words + w] = items[i * words + w];
   }
 }
 
@@ -306,6 +325,41 @@ std::vector<std::vector<uint32_t>> shard_allgatherv(Ctx& c, const std::vector<ui
   return out;
 }
 
+uint32_t* shard_route(Ctx& c, const uint32_t* items, uint64_t n, int words, int kw, uint64_t& nout) {
+  const uint32_t G = c.nshards;
+  auto* cnt = static_cast<unsigned long long*>(c.arena.get(2 * G * sizeof(unsigned long long)));
+  auto* cursor = cnt + G;
+  auto* allc = static_cast<uint64_t*>(c.arena.get(uint64_t(G) * G * sizeof(uint64_t)));
+  PM_HIP_CHECK(hipMemsetAsync(cnt, 0, G * sizeof(unsigned long long), c.stream));
+  auto* dest = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  if (n)
+    hipLaunchKernelGGL(k_route_count, dim3(xgrid(n)), dim3(kXBlock), 0, c.stream, items, n, words, kw, c.d_perm, G,
+                       dest, cnt);
+  c.comm->allgather(cnt, allc, G * sizeof(uint64_t), c.stream);  // allc[q * G + g]: shard q -> shard g
+  std::vector<uint64_t> m(uint64_t(G) * G);
+  PM_HIP_CHECK(hipMemcpyAsync(m.data(), allc, m.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  std::vector<uint64_t> sb(G), rb(G), soff(G, 0);
+  uint64_t nrecv = 0;
+  for (uint32_t g = 0; g < G; ++g) {
+    sb[g] = m[uint64_t(c.shard) * G + g] * words * sizeof(uint32_t);
+    rb[g] = m[uint64_t(g) * G + c.shard] * words * sizeof(uint32_t);
+    nrecv += m[uint64_t(g) * G + c.shard];
+    if (g) soff[g] = soff[g - 1] + m[uint64_t(c.shard) * G + g - 1];
+  }
+  auto* send = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(n, 1) * words * sizeof(uint32_t)));
+  auto* recv = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(nrecv, 1) * words * sizeof(uint32_t)));
+  if (n) {
+    PM_HIP_CHECK(hipMemcpyAsync(cursor, soff.data(), G * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+    hipLaunchKernelGGL(k_route_scatter, dim3(xgrid(n)), dim3(kXBlock), 0, c.stream, items, n, words, dest, cursor,
+                       send);
+  }
+  PM_HIP_CHECK(hipGetLastError());
+  c.comm->alltoallv(send, sb.data(), recv, rb.data(), c.stream);
+  nout = nrecv;
+  return recv;
+}
+
 void shard_exchange_tpub(Ctx& c) {
   if (!c.comm) return;
   const uint32_t G = c.nshards, maxS = c.xmaxS, nS = c.xnS[c.shard];
@@ -314,17 +368,6 @@ void shard_exchange_tpub(Ctx& c) {
   c.comm->allgather(c.d_xsend, c.d_xrecv, size_t(maxS) * sizeof(uint16_t), c.stream);
   hipLaunchKernelGGL(k_unpack_tpub, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream, c.d_xslist, c.d_xnS,
                      maxS, G, c.shard, c.d_xrecv, c.d_tpub[c.cur]);
-  PM_HIP_CHECK(hipGetLastError());
-}
-
-void shard_exchange_tpub_s(Ctx& c) {
-  if (!c.comm) return;
-  const uint32_t G = c.nshards, maxA = std::max<uint32_t>(c.amax, 1), nA = c.anum[c.shard];
-  if (nA) hipLaunchKernelGGL(k_pack_tpub, dim3(xgrid(nA)), dim3(kXBlock), 0, c.stream, c.d_aown, nA, c.d_tpub[c.cur],
-                             c.d_asend);
-  c.comm->allgather(c.d_asend, c.d_arecv, size_t(maxA) * sizeof(uint16_t), c.stream);
-  hipLaunchKernelGGL(k_unpack_tpub, dim3(xgrid(uint64_t(G) * maxA)), dim3(kXBlock), 0, c.stream, c.d_axl, c.d_anum,
-                     maxA, G, c.shard, c.d_arecv, c.d_tpub[c.cur]);
   PM_HIP_CHECK(hipGetLastError());
 }
 
@@ -358,108 +401,6 @@ void shard_after_first(Ctx& c) {
   // d_slist holds V entries >= maxS: the block past nS is padding
   c.comm->allgather(c.d_slist, c.d_xslist, size_t(maxS) * sizeof(uint32_t), c.stream);
   shard_exchange_tpub(c);
-  c.m_dirty = true;
-}
-
-void shard_replicate_m(Ctx& c) {
-  if (!c.comm || !c.m_dirty) return;
-  const uint32_t G = c.nshards, nS = c.xnS[c.shard];
-  const uint16_t* tpub = c.d_tpub[c.cur];
-  c.arena.reset();
-  // 1. this shard's S list (the only rows token passing reads from it), then every shard's
-  if (c.acap < std::max<uint32_t>(nS, 1)) {
-    if (c.d_aown) (void)hipFree(c.d_aown);
-    c.acap = std::max<uint32_t>(nS, 1);
-    PM_HIP_CHECK(hipMalloc(&c.d_aown, c.acap * sizeof(uint32_t)));
-  }
-  auto* actr = static_cast<unsigned int*>(c.arena.get(sizeof(unsigned int)));
-  PM_HIP_CHECK(hipMemsetAsync(actr, 0, sizeof(unsigned int), c.stream));
-  if (nS)
-    hipLaunchKernelGGL(k_s_collect, dim3(xgrid(nS)), dim3(kXBlock), 0, c.stream, c.d_slist, nS, tpub, c.d_aown, actr);
-  uint64_t* pin = pinned(c, 4);
-  PM_HIP_CHECK(hipMemcpyAsync(pin, actr, sizeof(unsigned int), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  const uint32_t na = static_cast<uint32_t>(pin[0] & 0xFFFFFFFFull);
-  std::vector<uint64_t> an(G, 0);
-  an[c.shard] = na;
-  an = shard_allreduce(c, an);
-  c.anum.assign(G, 0);
-  uint32_t amax = 1;
-  for (uint32_t g = 0; g < G; ++g) {
-    c.anum[g] = static_cast<uint32_t>(an[g]);
-    amax = std::max(amax, c.anum[g]);
-  }
-  if (amax > c.amax || !c.d_axl) {
-    void* ptrs[] = {c.d_axl, c.d_anum, c.d_asend, c.d_arecv};
-    for (void* p : ptrs)
-      if (p) (void)hipFree(p);
-    PM_HIP_CHECK(hipMalloc(&c.d_axl, size_t(G) * amax * sizeof(uint32_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_anum, G * sizeof(uint32_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_asend, size_t(amax) * sizeof(uint16_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_arecv, size_t(G) * amax * sizeof(uint16_t)));
-  }
-  if (c.acap < amax) {  // the send block is amax entries long
-    uint32_t* nb = nullptr;
-    PM_HIP_CHECK(hipMalloc(&nb, amax * sizeof(uint32_t)));
-    if (na) PM_HIP_CHECK(hipMemcpyAsync(nb, c.d_aown, na * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
-    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-    (void)hipFree(c.d_aown);
-    c.d_aown = nb;
-    c.acap = amax;
-  }
-  c.amax = amax;
-  PM_HIP_CHECK(hipMemcpyAsync(c.d_anum, c.anum.data(), G * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-  c.comm->allgather(c.d_aown, c.d_axl, size_t(amax) * sizeof(uint32_t), c.stream);
-  // 2. alive-entry counts per S entry, every shard's, and their exclusive scans
-  auto* cnt = static_cast<uint32_t*>(c.arena.get(size_t(amax) * sizeof(uint32_t)));
-  auto* xcnt = static_cast<uint32_t*>(c.arena.get(size_t(G) * amax * sizeof(uint32_t)));
-  auto* moff = static_cast<uint64_t*>(c.arena.get((size_t(amax) + 1) * sizeof(uint64_t)));
-  auto* xoff = static_cast<uint64_t*>(c.arena.get((size_t(G) * amax + 1) * sizeof(uint64_t)));
-  auto* seg = static_cast<uint64_t*>(c.arena.get((G + 1) * sizeof(uint64_t)));
-  hipLaunchKernelGGL(k_m_counts, dim3(xgrid(amax)), dim3(kXBlock), 0, c.stream, c.d_aown, na, amax, tpub, c.d_malive,
-                     cnt);
-  c.comm->allgather(cnt, xcnt, size_t(amax) * sizeof(uint32_t), c.stream);
-  PM_HIP_CHECK(hipMemsetAsync(moff, 0, sizeof(uint64_t), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(xoff, 0, sizeof(uint64_t), c.stream));
-  size_t t1 = 0, t2 = 0;
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, t1, cnt, moff + 1, static_cast<int>(amax), c.stream));
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, t2, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * amax),
-                                                c.stream));
-  size_t tb = std::max(t1, t2);
-  void* tmp = c.arena.get(tb);
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, cnt, moff + 1, static_cast<int>(amax), c.stream));
-  tb = std::max(t1, t2);
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tb, xcnt, xoff + 1, static_cast<int>(uint64_t(G) * amax),
-                                                c.stream));
-  hipLaunchKernelGGL(k_seg_starts, dim3(1), dim3(64 * ((G + 64) / 64)), 0, c.stream, xoff, amax, G, seg);
-  pin = pinned(c, G + 1);
-  PM_HIP_CHECK(hipMemcpyAsync(pin, seg, (G + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  uint64_t maxT = 1;
-  for (uint32_t g = 0; g < G; ++g) maxT = std::max(maxT, pin[g + 1] - pin[g]);
-  // 3. the alive rows of every shard's S into the remote region after this shard's own slots
-  const uint64_t need = c.nq + uint64_t(G) * maxT;
-  if (need > c.mcap) {
-    const uint64_t cap = std::max(need, c.mcap + c.mcap / 4);
-    uint32_t* nb = nullptr;
-    PM_HIP_CHECK(hipMalloc(&nb, (cap + kTileEntries) * sizeof(uint32_t)));  // + tail padding (k1_load)
-    if (c.nq) PM_HIP_CHECK(hipMemcpyAsync(nb, c.d_mcol, c.nq * sizeof(uint32_t), hipMemcpyDeviceToDevice, c.stream));
-    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-    (void)hipFree(c.d_mcol);
-    c.d_mcol = nb;
-    c.mcap = cap;
-  }
-  auto* send = static_cast<uint32_t*>(c.arena.get(maxT * sizeof(uint32_t)));
-  if (na)
-    hipLaunchKernelGGL(k_m_pack, dim3(xgrid(uint64_t(na) * kWave)), dim3(kXBlock), 0, c.stream, c.d_aown, na, tpub,
-                       c.d_offp, c.d_mlen, c.d_mcol, moff, send);
-  c.comm->allgather(send, c.d_mcol + c.nq, maxT * sizeof(uint32_t), c.stream);
-  hipLaunchKernelGGL(k_m_unpack, dim3(xgrid(uint64_t(G) * amax)), dim3(kXBlock), 0, c.stream, c.d_axl, c.d_anum, xcnt,
-                     xoff, seg, amax, G, c.shard, c.nq, maxT, c.d_offp, c.d_mlen, c.d_malive);
-  PM_HIP_CHECK(hipGetLastError());
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  c.arena.reset();
-  c.m_dirty = false;
 }
 
 }  // namespace pm

@@ -12,7 +12,7 @@ namespace pm {
 
 // Shards of one search driven by threads of one process on one device.
 struct ThreadGroup {
-  explicit ThreadGroup(int n_) : n(n_), ptrs(n_, nullptr), hvec(n_, nullptr) {}
+  explicit ThreadGroup(int n_) : n(n_), ptrs(n_, nullptr), hvec(n_, nullptr), counts(n_) {}
   int n;
   std::mutex m;
   std::condition_variable cv;
@@ -21,6 +21,7 @@ struct ThreadGroup {
   bool aborted = false;
   std::vector<const void*> ptrs;
   std::vector<std::vector<uint64_t>*> hvec;
+  std::vector<std::vector<uint64_t>> counts;  // alltoallv send sizes per shard
   std::mutex device;  // held by the shard that is computing (released inside collectives)
   void barrier();     // throws when another shard failed
   void abort();
@@ -28,6 +29,7 @@ struct ThreadGroup {
 
 Comm* make_rccl_comm(const void* unique_id, int nranks, int rank);
 size_t rccl_unique_id(void* out, size_t len);
+int rccl_selftest(int device, uint64_t bytes, int op);
 Comm* make_thread_comm(ThreadGroup* g, int rank);
 
 }  // namespace pm

@@ -182,6 +182,9 @@ int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen);
 /* Diagnostics: average time of `reps` launches of superstep-0 kernel variant
  * (0 = product kernel; others are ablation builds used by tools/ubench.py). */
 int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out);
+/* Diagnostics: a one-rank RCCL collective of `bytes` (op 0 ncclAllGather, 1 ncclAllReduce u64 sum),
+   result checked: 0 = right, 1 = wrong, -1 = error (pm_last_error). */
+int pm_debug_rccl_selftest(int device, uint64_t bytes, int op);
 /* Diagnostics: superstep-0 tiling statistics (real entries, loaded slots, rows, tiles, ranges, heavy rows). */
 int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n);
 

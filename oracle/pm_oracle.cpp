@@ -604,6 +604,12 @@ class Engine {
       if (!parent_ok) return;
       if (!l.VC) {
         if (t.vertex == t.target) return;
+        if (l.SV) {  // pattern_selected_vertices (:697-719): the source must be in Seen[vertex]
+          if (!seen_[t.vertex].count(t.target)) return;
+          auto f = tsm.find(t.vertex);
+          if (f != tsm.end()) f->second = 1;  // else "did not find the expected item"
+          return;
+        }
         Tok ack{t.target, t.vertex, t.target, t.itr, 0, true};
         if (tp_pre_visit(l, ack, msgcount)) q.push_back(ack);
       } else if (t.vertex == t.target) {
@@ -619,11 +625,19 @@ class Engine {
   void nlcc_path(const Nlc& l, std::unordered_map<uint64_t, uint8_t>& tsm, uint64_t& msgcount) {
     for (uint64_t v = 0; v < n_; ++v) {  // init visits (:387-528)
       if (!active_[v]) continue;
-      if (label_[v] != l.L[0]) continue;
+      if (l.SV) {  // pattern_selected_vertices (:409-436): last-label vertices are the ones verified
+        if (label_[v] != l.L[0] && label_[v] != l.L.back()) continue;
+        if (label_[v] == l.L.back()) {
+          if (!tsm.count(v)) tsm.insert({v, 0});
+          continue;
+        }
+      } else if (label_[v] != l.L[0]) {
+        continue;
+      }
       BitSet tv(tpub_[v]);
       if (tv.none() || !tv.test(l.I[0])) continue;
-      if (!l.VC && !tv.test(l.I.back())) continue;  // pattern_indices[size()-1] (nem_1.hpp:447-454)
-      if (!tsm.count(v)) tsm.insert({v, 0});
+      if (!l.VC && !l.SV && !tv.test(l.I.back())) continue;  // pattern_indices[size()-1] (nem_1.hpp:447-454)
+      if (!l.SV && !tsm.count(v)) tsm.insert({v, 0});
       std::deque<Tok> q;
       stats_.nlcc_edges += M_[v].size();
       for (auto& it : M_[v]) {
@@ -799,10 +813,16 @@ class Engine {
         nf = false;
         for (size_t pl = 0; pl < p_.nlc.size(); ++pl) {
           const Nlc& l = p_.nlc[pl];
-          if (l.SV) throw std::runtime_error("pattern_selected_vertices=1 is not supported");
+          if (l.SV && (pl >= 4 || l.VC))
+            throw std::runtime_error("pattern_selected_vertices=1 is supported on path lines (index < 4, valid_cycle 0)");
           for (auto& r : subgraphs[pl]) r.clear();  // file reopened with truncation (:713-717)
           std::unordered_map<uint64_t, uint8_t> tsm;
-          for (auto& s : seen_) s.clear();
+          if (!l.SV) {
+            for (auto& s : seen_) s.clear();  // beta.cpp:791-793
+          } else {  // keep the sets of active vertices with the line's last label (beta.cpp:823-850)
+            for (uint64_t v = 0; v < n_; ++v)
+              if (!(active_[v] && label_[v] == l.L.back())) seen_[v].clear();
+          }
           uint64_t msgcount = 0;
           auto tp0 = std::chrono::steady_clock::now();
           if (pl >= 4) {  // :762-767
@@ -812,12 +832,13 @@ class Engine {
           }
           // post-processing (:956-1071)
           bool deleted = false;
+          const uint64_t ibit = l.SV ? l.I.back() : l.I[0];  // token_source_pattern_ndices_tp_index (:959-962)
           for (auto& s : tsm) {
             if (s.second) continue;
             BitSet tv(tpub_[s.first]);
             if (tv.none()) continue;
-            if (tv.test(l.I[0])) {
-              tv.reset(l.I[0]);
+            if (tv.test(ibit)) {
+              tv.reset(ibit);
               tpub_[s.first] = (uint16_t)tv.to_ulong();
             }
             if (tv.none()) active_[s.first] = 0;

@@ -113,3 +113,44 @@ def test_oracle_partition_invariance(cycle_pattern, tmp_path):
         l.split(", ", 1)[1] for r in range(n) for l in open(d / "0" / sub / f"{stem}{r}").read().split("\n") if l)
     assert cat(a, "all_ranks_active_vertices", "active_vertices_", 1) == \
         cat(b, "all_ranks_active_vertices", "active_vertices_", 3)
+
+
+def test_oracle_selected_vertices_known_answer(tmp_path):
+    """patterns/selected_vertices_pattern on hand-built graphs (counts derived by hand, see
+    the pattern's README).  A 4-cycle c (label 5) - d (6) - a (3) - b (4) - c, plus
+    a2 (3) - b2 (4) - c2 (5) - d hanging off it.  a2 fails the LCC in superstep 0 (no
+    label-6 neighbour), b2 in superstep 1; c2 survives the LCC but line 0 never reaches it
+    from a through a B, so the selected-vertices line 1 leaves it unconfirmed: bit 2
+    cleared, c2 leaves S (its M and d's entry stay until the next LCC call).
+
+    The reference registers a selected vertex when its own init visit runs
+    (nem_1.hpp:409-436), and on one rank the init traversal drains every source's tokens
+    before the next vertex (visitor_queue.hpp:221-251): a C vertex is confirmed only if
+    its id precedes the source's.  With c = 0 < a = 3 the 4-cycle survives; with the ids
+    of the cycle reversed (a = 0 < c = 2) c is not yet registered when a's token arrives,
+    so it is dropped as well and the whole graph empties."""
+    pat = os.path.join(pmtest.ROOT, "patterns", "selected_vertices_pattern")
+    rd = lambda d, f: open(tmp_path / "0" / d / f).read().split("\n")[:-1]
+    # c=0, d=1, b=2, a=3, c2=4, b2=5, a2=6
+    pairs = [(3, 2), (2, 0), (0, 1), (1, 3), (6, 5), (5, 4), (4, 1)]
+    labels = np.array([5, 6, 4, 3, 5, 4, 3], np.uint64)
+    off, col = pmtest.symmetric_csr(pairs, 7)
+    so = oracle.run(off, col, pat, str(tmp_path), labels=labels)
+    assert so["iterations"] == 2 and so["terminated"] == 1
+    assert so["final_vertices"] == 4 and so["final_edges"] == 8
+    assert rd("all_ranks_active_vertices_count", "active_vertices_0") == [
+        "0, LP, 0, 6", "0, LP, 1, 5", "0, TP, 0, 5", "0, TP, 1, 4",
+        "1, LP, 0, 4", "1, LP, 1, 4"]  # no removal in iteration 1: no token passing
+    assert rd("all_ranks_active_edges_count", "active_edges_0") == [
+        "0, LP, 0, 13", "0, LP, 1, 11", "0, TP, 0, 11", "0, TP, 1, 9",
+        "1, LP, 0, 8", "1, LP, 1, 8"]
+    final = sorted(l.split(", ")[1] for l in rd("all_ranks_active_vertices", "active_vertices_0"))
+    assert final == ["0", "1", "2", "3"]
+    # a = 0, b = 1, c = 2, d = 3: c is registered after a's tokens have passed
+    pairs = [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 6), (6, 3)]
+    labels = np.array([3, 4, 5, 6, 3, 4, 5], np.uint64)
+    off, col = pmtest.symmetric_csr(pairs, 7)
+    so = oracle.run(off, col, pat, str(tmp_path / "b"), labels=labels)
+    assert so["final_vertices"] == 0
+    assert open(tmp_path / "b/0/all_ranks_active_vertices_count/active_vertices_0").read().split("\n")[3] == \
+        "0, TP, 1, 3"
