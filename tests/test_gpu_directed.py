@@ -117,3 +117,16 @@ def test_asymmetric_active_edge_map(k, extra, tmp_path, monkeypatch):
     if k == 1:  # hand-derived: iteration 1 keeps s with both (flagged) entries for one superstep
         lines = open(tmp_path / "gpu/0/all_ranks_active_edges_count/active_edges_0").read().split("\n")
         assert lines[4] == "1, LP, 0, 2" and sg["iterations"] == 2
+
+
+TDS_TAIL = os.path.join(pmtest.ROOT, "patterns", "triangle_tail_tds_pattern")
+
+
+@pytest.mark.parametrize("k,extra", [(4, [(1, 3), (7, 10)]), (6, [(1, 7), (4, 10), (2, 5), (9, 9), (12, 16), (13, 3)])])
+def test_subgraph_files_rewritten_per_iteration(k, extra, tmp_path):
+    """patterns/triangle_tail_tds_pattern: enumeration lines in two iterations, the second
+    one truncating subgraphs_4_0 (SURVEY A.6 hazard 6; hand-derived for k = 4 in the
+    pattern's README and tests/test_cpu_hazards.py)."""
+    off, col, labels = _triangles(k, extra)
+    sg = _check(off, col, TDS_TAIL, tmp_path, labels, symmetric=True)
+    assert sg["iterations"] == 2
