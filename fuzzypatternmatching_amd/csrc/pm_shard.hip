@@ -54,26 +54,20 @@ class RcclComm : public Comm {
   ~RcclComm() override {
     if (comm_) (void)ncclCommDestroy(comm_);
   }
-  // One rank: a copy / nothing (one-rank RCCL collectives of large buffers
-  // raise SIGFPE in this RCCL build; the communicator is still initialised).
+  // Every call goes through RCCL, one rank included (tests/test_gpu_shards.py
+  // ::test_rccl_shard_single_rank exercises the communicator); zero-sized calls
+  // are skipped on the host.
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-    if (nranks_ == 1) {
-      if (bytes && send != recv) PM_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
-      return;
-    }
+    if (!bytes) return;
     PM_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
-    if (nranks_ == 1) return;
+    if (!count) return;
     PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm_, s));
   }
   // grouped point-to-point sends / receives over xGMI (one pair per peer)
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                  hipStream_t s) override {
-    if (nranks_ == 1) {
-      if (sbytes[0]) PM_HIP_CHECK(hipMemcpyAsync(recv, send, sbytes[0], hipMemcpyDeviceToDevice, s));
-      return;
-    }
     uint64_t so = 0, ro = 0;
     PM_NCCL_CHECK(ncclGroupStart());
     for (int g = 0; g < nranks_; ++g) {
@@ -103,18 +97,18 @@ int rccl_selftest(int device, uint64_t bytes, int op) {
   PM_NCCL_CHECK(ncclCommInitRank(&comm, 1, id, 0));
   hipStream_t st;
   PM_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  const uint64_t words = std::max<uint64_t>(1, bytes / 8);
+  const uint64_t words = bytes / 8;  // 0: a zero-sized collective
   uint64_t *a = nullptr, *b = nullptr;
-  PM_HIP_CHECK(hipMalloc(&a, words * 8));
-  PM_HIP_CHECK(hipMalloc(&b, words * 8));
+  PM_HIP_CHECK(hipMalloc(&a, std::max<uint64_t>(words, 1) * 8));
+  PM_HIP_CHECK(hipMalloc(&b, std::max<uint64_t>(words, 1) * 8));
   std::vector<uint64_t> h(words);
   for (uint64_t i = 0; i < words; ++i) h[i] = i * 0x9E3779B97F4A7C15ull;
-  PM_HIP_CHECK(hipMemcpy(a, h.data(), words * 8, hipMemcpyHostToDevice));
+  if (words) PM_HIP_CHECK(hipMemcpy(a, h.data(), words * 8, hipMemcpyHostToDevice));
   if (op == 0) PM_NCCL_CHECK(ncclAllGather(a, b, words * 8, ncclUint8, comm, st));
   else PM_NCCL_CHECK(ncclAllReduce(a, b, words, ncclUint64, ncclSum, comm, st));
   PM_HIP_CHECK(hipStreamSynchronize(st));
   std::vector<uint64_t> r(words);
-  PM_HIP_CHECK(hipMemcpy(r.data(), b, words * 8, hipMemcpyDeviceToHost));
+  if (words) PM_HIP_CHECK(hipMemcpy(r.data(), b, words * 8, hipMemcpyDeviceToHost));
   (void)hipFree(a);
   (void)hipFree(b);
   (void)hipStreamDestroy(st);

@@ -21,7 +21,7 @@ if len(sys.argv) == 3:
 envs = [("default", {}), ("NCCL_ALGO=Ring", {"NCCL_ALGO": "Ring"}), ("NCCL_PROTO=Simple", {"NCCL_PROTO": "Simple"})]
 for name, extra in envs:
     for op in (0, 1):
-        for bytes_ in (1 << 10, 1 << 16, 1 << 20, 1 << 24, 1 << 26, 1 << 28):
+        for bytes_ in (0, 8, 1 << 10, 1 << 16, 1 << 20, 1 << 24, 1 << 26, 1 << 28):
             env = dict(os.environ, **extra)
             r = subprocess.run([sys.executable, __file__, str(bytes_), str(op)], env=env, capture_output=True,
                                text=True, timeout=120)
