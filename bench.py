@@ -264,9 +264,4 @@ if __name__ == "__main__":
         sys.stderr.write(open("/proc/self/maps").read())
     sys.stdout.flush()
     sys.stderr.flush()
-    if "rocprof" not in os.environ.get("LD_PRELOAD", ""):
-        # skip the interpreter teardown outside the profiler (nothing left to release);
-        # under rocprofv3 the normal exit writes the profile (it then segfaults in the
-        # HIP module teardown after "tool finalization": run it as a call's last GPU step)
-        os._exit(rc or 0)
     sys.exit(rc or 0)

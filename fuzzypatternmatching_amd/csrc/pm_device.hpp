@@ -158,6 +158,16 @@ __device__ __forceinline__ uint64_t wave_reserve(unsigned long long* ctr, uint32
   return base + incl - n;
 }
 
+// The same on a 32-bit counter.
+__device__ __forceinline__ uint32_t wave_reserve32(uint32_t* ctr, uint32_t n) {
+  const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(n));
+  const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+  uint32_t base = 0;
+  if (lane_id() == 0 && total) base = atomicAdd(ctr, total);
+  base = static_cast<uint32_t>(__shfl(static_cast<int>(base), 0, kWave));
+  return base + incl - n;
+}
+
 // Block-aggregated global add: one atomic per block (all threads must call).
 __device__ __forceinline__ void block_atomic_add(unsigned long long* dst, uint64_t v) {
   __shared__ unsigned long long s_b[kWpb];

@@ -105,6 +105,10 @@ struct KRange {
   uint32_t rlo[4], rlen[4];
   uint16_t rtu[4];
   uint32_t nrel;
+  // the same runs merged where they touch (membership only: superstep 0's
+  // first pass), up to four (len 0 = unused), nadm > 4: use the runs above
+  uint32_t alo[4], alen[4];
+  uint32_t nadm;
   // verify (keep_bits) of the label's template bits: bit kbit[i] survives iff
   // kneed[i] is a subset of TN (kneed = adj[t], or 1 << 16 when adj[t] = 0);
   // nkeep > 4 falls back to the LDS loop

@@ -164,6 +164,8 @@ struct K1Out {
 struct RelRuns {
   uint32_t lo[4], len[4], tu[4];
   uint32_t nrel;
+  uint32_t alo[4], alen[4];  // merged runs (admission test)
+  uint32_t nadm;
 };
 
 __device__ __forceinline__ RelRuns load_rel(const KRange& R) {
@@ -175,6 +177,12 @@ __device__ __forceinline__ RelRuns load_rel(const KRange& R) {
     x.tu[i] = __builtin_amdgcn_readfirstlane(R.rtu[i]);
   }
   x.nrel = __builtin_amdgcn_readfirstlane(R.nrel);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x.alo[i] = __builtin_amdgcn_readfirstlane(R.alo[i]);
+    x.alen[i] = __builtin_amdgcn_readfirstlane(R.alen[i]);
+  }
+  x.nadm = __builtin_amdgcn_readfirstlane(R.nadm);
   return x;
 }
 
@@ -245,6 +253,10 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
 // i-1; row_shl:s gives lane i the value of lane i+s inside its 16-lane row.
 __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t v) {
   return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(v), 0x138, 0xF, 0xF, false));
+}
+// wave_shr:1 with lane 0 reading 0 (no copy of an "old" value first)
+__device__ __forceinline__ uint32_t dpp_wave_shr1_z(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xF, 0xF, true));
 }
 template <int S>
 __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t v) {
@@ -320,9 +332,11 @@ __device__ __forceinline__ void k1_load(uint32_t (&v)[kSub], const K1Desc& d, co
   const uint32_t* tp = colp + (rem ? d.qbase + t0 : 0);
 #pragma unroll
   for (int q = 0; q < kSub; ++q) v[q] = __builtin_nontemporal_load(tp + q * kWave + lane);
+  if (rem < kTileEntries) {  // wave-uniform: only partial tiles pay the masking
 #pragma unroll
-  for (int q = 0; q < kSub; ++q)
-    if (static_cast<uint32_t>(q * kWave + lane) >= rem) v[q] = kNone;
+    for (int q = 0; q < kSub; ++q)
+      if (static_cast<uint32_t>(q * kWave + lane) >= rem) v[q] = kNone;
+  }
 }
 
 // Per-wave LDS staging of a light tile: per-row accumulators (TN | count << 16,
@@ -354,6 +368,54 @@ __device__ __forceinline__ uint64_t row_start_mask(uint32_t lg) {
   }
 }
 
+// Phase A of a light tile: appends the tile's contributing slots (neighbour
+// position in an admitted run, first occurrence in its row) to the wave's
+// staging list in slot order and returns their number (wave-uniform).  NR
+// merged-run compares (unused runs have length 0); NR = 0: the full label
+// test (more than four runs).  The compares land in 64-bit lane masks and
+// the row-start / first-occurrence logic stays on the scalar unit.
+template <int NR, bool WIDE>
+__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], bool big, uint32_t gm, uint64_t rs_light,
+                                               const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
+                                               uint16_t nm, K1Stage& st) {
+  const int lane = lane_id();
+  uint32_t nlist = 0;
+#pragma unroll
+  for (int q = 0; q < kSub; ++q) {
+    const uint32_t x = v[q];
+    uint64_t in_m = 0;  // one ballot per compare: each folds into its compare's mask
+    if (NR == 0) {
+      in_m = __builtin_amdgcn_ballot_w64((tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm) != 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) in_m |= __builtin_amdgcn_ballot_w64(x - rel_runs.alo[i] < rel_runs.alen[i]);
+    }
+    // first occurrence: differs from the left neighbour lane; lane 0 compares
+    // with the previous sub-tile's last slot, which matters only when a row
+    // continues across sub-tiles (G > 64; for G <= 64 lane 0 starts a row)
+    uint64_t ne_m = __builtin_amdgcn_ballot_w64(dpp_wave_shr1_z(x) != x);
+    if (q > 0) {  // (q = 0: lane 0 starts a row for every G)
+      const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[q - 1]), kWave - 1));
+      const uint32_t x0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 0));
+      // (c != x0) as integer carry arithmetic: a bool here would be widened on the VALU
+      ne_m = (ne_m & ~1ull) | ((uint64_t(c ^ x0) + 0xFFFFFFFFull) >> 32);
+    }
+    // row starts of this sub-tile (G <= 64: every G-th lane; larger G: lane 0
+    // when the sub-tile starts a row)
+    const uint64_t rsq = big ? (((q * kWave) & gm) == 0 ? 1ull : 0ull) : rs_light;
+    const uint64_t C = in_m & (rsq | ne_m);
+    if (C) {
+      if ((C >> lane) & 1ull) {
+        const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_amdgcn_mbcnt_hi(
+                                         static_cast<uint32_t>(C >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C), 0)));
+        st.list[idx] = make_uint2(x, static_cast<uint32_t>(q * kWave + lane));
+      }
+      nlist += static_cast<uint32_t>(__builtin_popcountll(C));
+    }
+  }
+  return nlist;
+}
+
 // Light tile (G = 1 << kind <= kTileEntries slots per row, 512 / G whole rows).
 // Phase A, per sub-tile, all in wave masks: a lane's neighbour can contribute
 // iff its position lies in one of the range's relevant label runs (one
@@ -369,39 +431,20 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
                                               const K1Out& o, BlockAcc& acc, unsigned long long* s_hist,
                                               unsigned long long* tm, K1Stage& st) {
   const int lane = lane_id();
-  const uint32_t lg = d.kind;
+  const uint32_t lg = __builtin_amdgcn_readfirstlane(d.kind);
   const uint32_t gm = (1u << lg) - 1;
+  const bool big = lg > 6;  // rows span sub-tiles
   const uint64_t rs_light = uniform64(row_start_mask(lg));
-  const uint32_t nrel = WIDE ? 0u : min(rel_runs.nrel, 4u);
-  uint32_t nlist = 0;  // wave-uniform
-#pragma unroll
-  for (int q = 0; q < kSub; ++q) {
-    const uint32_t x = v[q];
-    uint64_t cm = 0;
-    if (WIDE) {
-      cm = __ballot((tbits_rel<true>(x, rel_runs, s_runs, nruns) & nm) != 0);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (static_cast<uint32_t>(i) < nrel) cm |= __ballot(x - rel_runs.lo[i] < rel_runs.len[i]);
-    }
-    uint32_t pv = dpp_wave_shr1(x);
-    if (q > 0) {
-      const uint32_t carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[q - 1]), kWave - 1));
-      if (lane == 0) pv = carry;
-    }
-    uint64_t rs = rs_light;
-    if (lg > 6) rs = ((q * kWave) & gm) == 0 ? 1ull : 0ull;
-    const uint64_t C = cm & (rs | __ballot(pv != x));
-    if (C) {
-      if ((C >> lane) & 1ull) {
-        const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_amdgcn_mbcnt_hi(
-                                         static_cast<uint32_t>(C >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C), 0)));
-        st.list[idx] = make_uint2(x, static_cast<uint32_t>(q * kWave + lane));
-      }
-      nlist = __builtin_amdgcn_readfirstlane(nlist + static_cast<uint32_t>(__builtin_popcountll(C)));
-    }
-  }
+  // admission compares specialised on the number of merged runs (wave-uniform)
+  uint32_t nlist;
+  if (WIDE || rel_runs.nadm > 4)
+    nlist = k1_phase_a<0, WIDE>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
+  else if (rel_runs.nadm <= 1)
+    nlist = k1_phase_a<1, false>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
+  else if (rel_runs.nadm == 2)
+    nlist = k1_phase_a<2, false>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
+  else
+    nlist = k1_phase_a<4, false>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
   if (lane < kSub) st.sm[lane] = 0ull;
   if ((MODE & 16) || nlist == 0) {  // MODE 16 (diagnostic): phase A only
     if (lane < kSub && !(MODE & 64)) tm[lane] = 0ull;  // MODE 64: without this store
@@ -557,7 +600,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) 
   for (int i = threadIdx.x % kWave; i < static_cast<int>(kTileEntries); i += kWave) st.acc[i] = 0;
   __syncthreads();
   BlockAcc acc;
-  const int lane = lane_id();
   const uint32_t W = gridDim.x * kWpb;
   const int nruns = lr.n;
   uint32_t r = 0;
@@ -701,12 +743,8 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t nS = *nSp;
   const uint64_t nchunks = (uint64_t(nS) + kWave - 1) / kWave;
-  for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb) {
-    const uint64_t live = mask_in ? mask_in[chunk] : ~0ull;
-    if (!live) {  // wave-uniform: nothing left in this chunk
-      if (lane == 0) mask_out[chunk] = 0;
-      continue;
-    }
+  // one chunk of 64 slist entries (live: the chunk's live mask, non-zero)
+  auto chunk_body = [&](uint64_t chunk, uint64_t live) {
     const uint64_t i = chunk * kWave + lane;
     uint32_t u = kNone;
     uint16_t Tu = 0, nm = 0;
@@ -839,6 +877,31 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         acc.es += cnt;
       } else {
         acc_owner(s_hist, oa, u, cnt);
+      }
+    }
+  };
+  if (!mask_in) {
+    // first later superstep (every entry live): one chunk per wave at a time
+    for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb)
+      chunk_body(chunk, ~0ull);
+  } else {
+    // later: the wave's chunks stay strided over the grid (clustered live
+    // chunks spread over waves), but each lane loads the live mask of one of
+    // the wave's next 64 chunks, dead ones get their zero output mask in the
+    // same pass, and the wave then works through the live ones
+    const uint64_t W = uint64_t(gridDim.x) * kWpb;
+    for (uint64_t k0 = uint64_t(blockIdx.x) * kWpb + w; k0 < nchunks; k0 += W * kWave) {
+      const uint64_t ch = k0 + uint64_t(lane) * W;
+      const uint64_t lm = ch < nchunks ? mask_in[ch] : 0ull;
+      if (ch < nchunks && !lm) mask_out[ch] = 0;
+      uint64_t bal = __ballot(lm != 0);
+      while (bal) {
+        const int j = __ffsll(static_cast<long long>(bal)) - 1;
+        bal &= bal - 1;
+        const uint64_t live =
+            (uint64_t(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(lm >> 32), j))) << 32) |
+            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(lm), j));
+        chunk_body(k0 + uint64_t(j) * W, live);
       }
     }
   }
@@ -1203,6 +1266,7 @@ void build_tiling(Ctx& c) {
       R.kind = static_cast<uint32_t>(kind);
       R.qbase = dev_at(c.d_offp, a);
       R.nrel = 0;
+      R.nadm = 0;
       R.nkeep = 0;
       for (int t = 0; t < 16; ++t) {
         if (!((tu >> t) & 1u)) continue;
@@ -1220,6 +1284,15 @@ void build_tiling(Ctx& c) {
           R.rtu[R.nrel] = tus[m];
         }
         ++R.nrel;
+        if (R.nadm > 0 && R.nadm <= 4 && R.alo[R.nadm - 1] + R.alen[R.nadm - 1] == c.lr.lo[m]) {
+          R.alen[R.nadm - 1] += c.lr.len[m];  // touches the previous relevant run
+        } else {
+          if (R.nadm < 4) {
+            R.alo[R.nadm] = c.lr.lo[m];
+            R.alen[R.nadm] = c.lr.len[m];
+          }
+          ++R.nadm;
+        }
       }
       uint64_t nt;
       if (kind < kHeavyKind) {

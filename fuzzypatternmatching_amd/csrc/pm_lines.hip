@@ -1,4 +1,4 @@
-// Fused token passing: one cooperative kernel per NLC line.
+// Fused token passing: one persistent grid-synchronised kernel per run of NLC lines.
 //
 // The level-synchronous formulation of pm_kernels.hip ("Token passing")
 // executed as a single grid-wide kernel whose phases are separated by grid
@@ -28,8 +28,19 @@
 // Memory ordering: phases exchange data through global memory across CUs.
 // Reads of data written by another CU in an earlier phase whose cache line
 // this CU may already hold (frontier lists, hash slots, source list) go
-// through ld_acq (L1-bypassing atomic loads); TDS walk regions are fresh,
+// through ld_dev (L1-bypassing atomic loads); TDS walk regions are fresh,
 // 128-B aligned memory per position.
+//
+// Launch: an ordinary launch whose grid (at most one 1024-thread block per CU,
+// hipOccupancyMaxActiveBlocksPerMultiprocessor >= 1 checked) is co-resident:
+// the kernel runs alone on its stream after its stream-ordered predecessors,
+// and the only other work a shard's device may carry (RCCL, another in-process
+// shard's kernels; ThreadGroup holds the device during compute) runs to
+// completion without waiting on it, so every block is eventually scheduled.
+// hipLaunchCooperativeKernel is not used: the dedicated cooperative queue it
+// creates crashes libhsa-runtime's exit-time teardown under rocprofv3 (the
+// profile is written, the process then dies with SIGSEGV in
+// libamdhip64 -> libhsa-runtime64; tools/rp_exit.py beta vs beta_nocoop).
 
 #include <hip/hip_runtime.h>
 
@@ -48,8 +59,11 @@ static constexpr unsigned long long kEmpty = ~0ull;
 static constexpr uint32_t kMulti = 0xFFFFFFFEu;
 static constexpr int kMaxProbe = 128;
 
+// Relaxed device-scope atomic load: bypasses this CU's L1 so a value written by
+// another CU before the last grid barrier is seen; the ordering itself comes
+// from the barrier's release / acquire fences (tree_barrier).
 template <typename T>
-__device__ __forceinline__ T ld_acq(const T* p) {
+__device__ __forceinline__ T ld_dev(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -97,6 +111,7 @@ struct LineKernelArgs {
   unsigned* done;  // lines processed by the launch
   uint32_t* act;   // S members at launch start (slist entries with T_pub != 0), built by k_lines
   unsigned long long* nact;
+  uint64_t small_line;  // single-block threshold (kSmallLine)
 };
 
 __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
@@ -108,7 +123,7 @@ __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
 // `parent`; true for the first arrival (the slot joins the position's frontier).
 __device__ __forceinline__ bool ht_arrive(unsigned long long* hval, uint64_t h, uint32_t level, uint32_t parent) {
   const unsigned long long want = (static_cast<unsigned long long>(level) << 32) | parent;
-  unsigned long long old = ld_acq(&hval[h]);
+  unsigned long long old = ld_dev(&hval[h]);
   while (true) {
     if (old == kEmpty) {
       const unsigned long long prev = atomicCAS(&hval[h], kEmpty, want);
@@ -133,7 +148,7 @@ __device__ __forceinline__ uint64_t ht_insert(const LineKernelArgs& a, uint32_t 
   const unsigned long long key = (static_cast<unsigned long long>(s) << 32) | u;
   uint64_t h = mix64(key) & a.hmask;
   for (int probe = 0; probe < kMaxProbe; ++probe) {
-    unsigned long long k = ld_acq(&a.hkey[h]);
+    unsigned long long k = ld_dev(&a.hkey[h]);
     if (k == kEmpty) {
       const unsigned long long prev = atomicCAS(&a.hkey[h], kEmpty, key);
       k = prev == kEmpty ? key : prev;
@@ -250,7 +265,7 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
   return emitted;
 }
 
-// Grid barrier for co-resident blocks (cooperative launch): blocks arrive on
+// Grid barrier for co-resident blocks (see "Launch" above): blocks arrive on
 // per-group counters (16 blocks, own 128-B lines), the last of a group on the
 // top counter, the last group bumps the generation word everyone waits on.
 // Counters reset themselves; the generation only grows.
@@ -304,7 +319,7 @@ __device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t 
   bool ok = false;
   s = 0;
   if (i < nact) {
-    s = ld_acq(&a.act[i]);
+    s = ld_dev(&a.act[i]);
     const uint16_t T = a.tpub[s];
     ok = T && pos_ok(T, 0, *a.la);
     if (ok && !tds && !a.la->VC && !((T >> a.la->ilast) & 1u)) ok = false;
@@ -353,11 +368,11 @@ __device__ __forceinline__ void build_active(const LineKernelArgs& a) {
 __device__ __forceinline__ void line_post(const LineKernelArgs& a, const GridIdx& g, unsigned long long* s_hist) {
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   __syncthreads();
-  const uint64_t nsrc = ld_acq(&a.st->nsrc);
+  const uint64_t nsrc = ld_dev(&a.st->nsrc);
   uint64_t acked = 0, deleted = 0, rv = 0, re = 0;
   for (uint64_t i = g.tid; i < nsrc; i += g.nth) {
-    const uint32_t s = ld_acq(&a.sources[i]);
-    if (ld_acq(&a.tsm[s]) == 2) {
+    const uint32_t s = ld_dev(&a.sources[i]);
+    if (ld_dev(&a.tsm[s]) == 2) {
       ++acked;
       continue;
     }
@@ -463,7 +478,8 @@ __device__ __forceinline__ void phase_sync(const LineKernelArgs& a, bool single)
 }
 
 // A line whose sources and position-1 frontier are at most this large is
-// finished by block 0 alone (block barriers instead of grid barriers).
+// finished by block 0 alone (block barriers instead of grid barriers);
+// LineKernelArgs::small_line, PM_SMALL_LINE overrides.
 static constexpr uint64_t kSmallLine = 16384;
 
 // ---- path / cycle lines (nem_1) ----------------------------------------
@@ -473,16 +489,16 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
   LineStats* st = a.st;
   uint64_t trav = 0, tokens = 0, lo = 0;
   for (int k = 1; k <= a.la->C; ++k) {
-    if (ld_acq(&st->overflow)) break;  // same value in every wave after the barrier
-    const uint64_t hi = ld_acq(&st->ftotal);
+    if (ld_dev(&st->overflow)) break;  // same value in every wave after the barrier
+    const uint64_t hi = ld_dev(&st->ftotal);
     for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
       const uint64_t i = i0 + lane_id();
       const bool act = i < hi;
       uint32_t s = 0, u = 0, excl = kNone;
       if (act) {
-        const uint32_t h = ld_acq(&a.front[i]);
-        const unsigned long long key = ld_acq(&a.hkey[h]);
-        const uint32_t par = static_cast<uint32_t>(ld_acq(&a.hval[h]));
+        const uint32_t h = ld_dev(&a.front[i]);
+        const unsigned long long key = ld_dev(&a.hkey[h]);
+        const uint32_t par = static_cast<uint32_t>(ld_dev(&a.hval[h]));
         s = static_cast<uint32_t>(key >> 32);
         u = static_cast<uint32_t>(key);
         excl = par == kMulti ? kNone : par;
@@ -495,12 +511,12 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
   }
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
-  if (ld_acq(&st->overflow)) return;  // the host clears the table and reruns the line
+  if (ld_dev(&st->overflow)) return;  // the host clears the table and reruns the line
   line_post(a, g, s_hist);
   // hash cleanup: no insert happens after the last position
-  const uint64_t nf = ld_acq(&st->ftotal);
+  const uint64_t nf = ld_dev(&st->ftotal);
   for (uint64_t i = g.tid; i < nf; i += g.nth) {
-    const uint32_t h = ld_acq(&a.front[i]);
+    const uint32_t h = ld_dev(&a.front[i]);
     a.hkey[h] = kEmpty;
     a.hval[h] = kEmpty;
   }
@@ -511,7 +527,7 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
   LineStats* st = a.st;
   uint64_t trav = 0, tokens = 0;
   // P1 + position 1: (v, s, parent = s) for v in M[s]
-  const uint64_t nact = ld_acq(a.nact);
+  const uint64_t nact = ld_dev(a.nact);
   for (uint64_t i0 = g.gw * kWave; i0 < nact; i0 += g.nw * kWave) {
     uint32_t s;
     const bool ok = select_source(a, i0 + lane_id(), nact, false, s);
@@ -522,9 +538,9 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
   wave_add(&st->tokens, tokens);
   tree_barrier(a.gbar);
   if (blockIdx.x == 0 && threadIdx.x == 0) st->tstamp[1] = __builtin_amdgcn_s_memrealtime();
-  const uint64_t nsrc = ld_acq(&st->nsrc);
+  const uint64_t nsrc = ld_dev(&st->nsrc);
   if (nsrc == 0) return;  // no tokens, nothing to post-process (every block agrees)
-  const bool single = nsrc <= kSmallLine && ld_acq(&st->ftotal) <= kSmallLine;
+  const bool single = nsrc <= a.small_line && ld_dev(&st->ftotal) <= a.small_line;
   if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
   if (!single) path_rest(a, g, false, s_hist, wr);
   else if (blockIdx.x == 0) path_rest(a, block_idx(), true, s_hist, wr);
@@ -543,13 +559,13 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   // single block: the walk counters live in LDS (no global atomic per wave and round)
   const bool stage = stride <= kStage;
   if (single) {
-    if (threadIdx.x < 20) wr.wn[threadIdx.x] = threadIdx.x == 1 ? ld_acq(&st->wn[1]) : 0ull;
+    if (threadIdx.x < 20) wr.wn[threadIdx.x] = threadIdx.x == 1 ? ld_dev(&st->wn[1]) : 0ull;
     __syncthreads();
   }
   const int wv = threadIdx.x / kWave, lane = lane_id();
   for (int k = 1; k <= la.C; ++k) {
-    if (ld_acq(&st->overflow)) break;
-    const uint64_t nin = single ? wr.wn[k] : ld_acq(&st->wn[k]);
+    if (ld_dev(&st->overflow)) break;
+    const uint64_t nin = single ? wr.wn[k] : ld_dev(&st->wn[k]);
     const uint64_t out_base = (in_base + nin * stride + 31) & ~uint64_t(31);
     tokens += g.tid == 0 ? nin : 0;
     const uint32_t* win = a.wbuf + in_base;
@@ -589,11 +605,11 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
     phase_sync(a, single);
   }
   // every final walk may be kept: its room must exist before any terminal effect
-  const uint64_t nw = single ? wr.wn[la.C + 1] : ld_acq(&st->wn[la.C + 1]);
+  const uint64_t nw = single ? wr.wn[la.C + 1] : ld_dev(&st->wn[la.C + 1]);
   // kept slots used by the launch's earlier lines (read at line start: the
   // terminal loop below adds to the counter while slower blocks still enter it)
   const uint64_t kept0 = kept_base;
-  if (ld_acq(&st->overflow) || kept0 + nw * stride > a.kept_cap) {
+  if (ld_dev(&st->overflow) || kept0 + nw * stride > a.kept_cap) {
     if (g.tid == 0) atomicOr(&st->overflow, 1u);
     wave_add(&st->trav, trav);
     return;
@@ -643,8 +659,8 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   const int stride = a.la->C + 2;
   uint64_t trav = 0;
   // P1 + position 1 walks [s, w]; region 1 starts at slot 0
-  const uint64_t kept_base = ld_acq(a.kept_ctr);  // no kept walk of this line exists yet
-  const uint64_t nact = ld_acq(a.nact);
+  const uint64_t kept_base = ld_dev(a.kept_ctr);  // no kept walk of this line exists yet
+  const uint64_t nact = ld_dev(a.nact);
   for (uint64_t i0 = g.gw * kWave; i0 < nact; i0 += g.nw * kWave) {
     uint32_t s;
     const bool ok = select_source(a, i0 + lane_id(), nact, true, s);
@@ -689,9 +705,9 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   wave_add(&st->trav, trav);
   tree_barrier(a.gbar);
   if (blockIdx.x == 0 && threadIdx.x == 0) st->tstamp[1] = __builtin_amdgcn_s_memrealtime();
-  const uint64_t nsrc = ld_acq(&st->nsrc);
+  const uint64_t nsrc = ld_dev(&st->nsrc);
   if (nsrc == 0) return;  // no walks, nothing to post-process (every block agrees)
-  const bool single = nsrc <= kSmallLine && ld_acq(&st->wn[1]) <= kSmallLine;
+  const bool single = nsrc <= a.small_line && ld_dev(&st->wn[1]) <= a.small_line;
   if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
   if (!single) tds_rest(a, g, false, s_hist, wr, kept_base);
   else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist, wr, kept_base);
@@ -721,7 +737,7 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[2] = __builtin_amdgcn_s_memrealtime();
     tree_barrier(a.gbar);
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[3] = __builtin_amdgcn_s_memrealtime();
-    const bool stop = ld_acq(&b.st->overflow) || (d.il && ld_acq(&b.st->deleted));
+    const bool stop = ld_dev(&b.st->overflow) || (d.il && ld_dev(&b.st->deleted));
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.done = static_cast<unsigned>(pl + 1);
     if (stop) break;
   }
@@ -841,6 +857,8 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   a.fcap = c.hcap / 2;
   a.st = c.d_lstats;
   a.lines = c.d_ldesc;
+  a.small_line = kSmallLine;
+  if (const char* e = std::getenv("PM_SMALL_LINE")) a.small_line = std::strtoull(e, nullptr, 10);
   a.pl_begin = static_cast<int>(pl0);
   a.pl_end = static_cast<int>(nl);
   a.done = d_done;
@@ -859,8 +877,8 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   // before the first grid barrier completes)
   const unsigned grid = static_cast<unsigned>(
       std::max<uint64_t>(16, std::min<uint64_t>(c.line_grid, (c.live_hint + 255) / 256)));
-  PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(grid),
-                                          dim3(kLineBlock), args, 0, c.stream));
+  PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args, 0,
+                               c.stream));
   c.probe("lines launched");
   // read-back through pinned memory: [done | kept slots | line stats]
   static_assert(sizeof(LineStats) % 8 == 0, "LineStats is read back as u64 words");

@@ -15,6 +15,6 @@ for ctr in ${GROUPS_OVERRIDE:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_AN
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr --kernel-include-regex "k_lcc_first" --output-format csv \
     -d gpurun_out/${TAG}_$i -o run -- python3 tools/k1_harness.py $SCALE $PGEN 3 > gpurun_out/${TAG}_$i.log 2>&1
   rc=$?; echo "pass $i ($ctr) rc=$rc"; tail -2 gpurun_out/${TAG}_$i.log
-  [ $rc -eq 0 ] || [ $rc -eq 139 ] || exit $rc
+  [ $rc -eq 0 ] || exit $rc
 done
 exit 0
