@@ -267,6 +267,15 @@ class PatternMatcher:
         self._check(_lib().pm_token_passing(self._ctx, pl, ctypes.byref(st)))
         return {f[0]: getattr(st, f[0]) for f in st._fields_}
 
+    def tds(self, pl, sink=None):
+        """One TDS line through pm_tds: sink(rank, vertex_ids) is called for every kept walk
+        (the lines the reference writes to subgraphs_<pl>_<rank>); returns the line stats."""
+        st = _abi.TpStats()
+        cb = _abi.PathSink(lambda user, rank, v, n: sink(rank, [v[i] for i in range(n)])) if sink else None
+        self._check(_lib().pm_tds(self._ctx, pl, ctypes.cast(cb, ctypes.c_void_p) if cb else None, None,
+                                  ctypes.byref(st)))
+        return {f[0]: getattr(st, f[0]) for f in st._fields_}
+
     def post_token_passing(self, pl):
         d = ctypes.c_uint32()
         self._check(_lib().pm_post_token_passing(self._ctx, pl, ctypes.byref(d)))

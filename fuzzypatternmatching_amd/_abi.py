@@ -53,6 +53,10 @@ class LccStats(ctypes.Structure):
     ]
 
 
+# void (*)(void* user, uint32_t rank, const uint32_t* vertices, uint32_t length)
+PathSink = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32)
+
+
 class TpStats(ctypes.Structure):
     _fields_ = [
         ("sources", c_u64),
@@ -94,6 +98,7 @@ SIGNATURES = [
     ("pm_reset", ctypes.c_int, [c_vp]),
     ("pm_lcc_bsp", ctypes.c_int, [c_vp, ctypes.c_int, c_u64, ctypes.POINTER(LccStats)]),
     ("pm_token_passing", ctypes.c_int, [c_vp, c_u32, ctypes.POINTER(TpStats)]),
+    ("pm_tds", ctypes.c_int, [c_vp, c_u32, c_vp, c_vp, ctypes.POINTER(TpStats)]),
     ("pm_post_token_passing", ctypes.c_int, [c_vp, c_u32, ctypes.POINTER(c_u32)]),
     ("pm_run_beta", ctypes.c_int, [c_vp, c_char_p, c_u64, ctypes.POINTER(RunStats)]),
     ("pm_export_state", ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_u64)]),

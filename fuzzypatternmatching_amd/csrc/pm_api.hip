@@ -935,6 +935,31 @@ int pm_token_passing(pm_ctx* ctx, uint32_t pl, pm_tp_stats* out) {
   });
 }
 
+int pm_tds(pm_ctx* ctx, uint32_t pl, pm_path_sink sink, void* user, pm_tp_stats* out) {
+  PM_API_BODY(ctx, {
+    if (ctx->comm) throw std::runtime_error("pm_tds: sharded contexts run lines through pm_run_beta");
+    if (pl >= ctx->pattern.lines.size()) throw std::runtime_error("NLC line index out of range");
+    if (pl < 4) throw std::runtime_error("pm_tds: line index below 4 is a path / cycle line (pm_token_passing)");
+    std::vector<uint32_t> walks;
+    uint32_t stride = 0;
+    const pm::TpResult r = pm::run_tds_line(*ctx, ctx->pattern.lines[pl], walks, stride);
+    if (sink && stride) {
+      std::vector<uint32_t> ids(stride);
+      for (uint64_t i = 0; i < walks.size() / stride; ++i) {
+        for (uint32_t p = 0; p < stride; ++p) ids[p] = ctx->perm_host[walks[i * stride + p]];
+        sink(user, pm::owner_host(*ctx, ids[stride - 1]), ids.data(), stride);
+      }
+    }
+    if (out) {
+      out->sources = r.sources;
+      out->acked_sources = 0;
+      out->edges_traversed = r.edges;
+      out->tokens = r.tokens;
+      out->walks = r.walks;
+    }
+  });
+}
+
 int pm_post_token_passing(pm_ctx* ctx, uint32_t pl, uint32_t* deleted) {
   PM_API_BODY(ctx, {
     if (pl >= ctx->pattern.lines.size()) throw std::runtime_error("NLC line index out of range");

@@ -219,10 +219,11 @@ __device__ __forceinline__ KeepArgs load_keep(const KRange& R) {
 
 __device__ __forceinline__ uint16_t keep_fast(uint16_t tu, uint16_t TN, const KeepArgs& k, const uint16_t* adj) {
   if (k.n > 4) return keep_bits(tu, TN, adj);
+  // unused entries hold bit 0 (the KRange is zero-initialised): no test of n
   uint32_t out = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (i < static_cast<int>(k.n) && (TN & k.need[i]) == k.need[i]) out |= k.bit[i];
+    if ((TN & k.need[i]) == k.need[i]) out |= k.bit[i];
   return static_cast<uint16_t>(out);
 }
 
@@ -236,10 +237,12 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
     acc.removed = 1;
     return false;
   }
-  o.tst[u] = T;
-  o.tpub[u] = T;
-  o.mlen[u] = len;
-  o.malive[u] = cnt;
+  // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
+  const uint32_t b2 = u * 2u, b4 = u * 4u;
+  *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
+  *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+  *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = len;
+  *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
   if (oa.nranks <= 1) {
     acc.vs += 1;
     acc.es += cnt;
@@ -451,16 +454,25 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
     return;
   }
   __builtin_amdgcn_wave_barrier();
-  // phase B1: row TN (neighbour-mask bits of the contributors' template bits) and count
+  // phase B1: row TN (neighbour-mask bits of the contributors' template bits)
+  // and count; the list is in slot order, so a row's entries are consecutive
+  // and its first entry (head) resets the row's word before the others add
+  // (LDS operations of one wave complete in order)
+  uint32_t carry_row = kNone;
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
-    if (i < nlist) {
-      const uint2 e = st.list[i];
-      const uint32_t row = e.y >> lg;
+    const bool in = i < nlist;
+    const uint2 e = in ? st.list[i] : make_uint2(0u, 0u);
+    const uint32_t row = in ? (e.y >> lg) : kNone;
+    uint32_t prow = dpp_wave_shr1_z(row);
+    if (lane == 0) prow = carry_row;
+    if (in && row != prow) st.acc[row] = 0u;
+    if (in) {
       atomicOr(&st.acc[row], static_cast<uint32_t>(tbits_rel<WIDE>(e.x, rel_runs, s_runs, nruns) & nm));
       atomicAdd(&st.acc[row], 1u << 16);
     }
+    carry_row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), kWave - 1));
   }
   __builtin_amdgcn_wave_barrier();
   if (MODE & 32) {  // diagnostic: phase A + B1 only
@@ -469,42 +481,35 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
     for (uint32_t i = lane; i < nlist; i += kWave) st.acc[st.list[i].y >> lg] = 0;
     return;
   }
-  // phase B2: the list is in slot order, so each row's entries are
-  // consecutive; the first (head) verifies the row, and the row's entries
-  // learn the verdict from the head's ballot bit (survivors write M[u] in
-  // slot order at the start of u's padded row)
+  // phase B2: the head of each row verifies it and leaves (its list index,
+  // survived) in the row's word; every entry then reads its row's word and a
+  // survivor's entries write M[u] in slot order at the start of u's padded row
   const uint32_t row0 = d.rel * (kTileEntries >> lg);
-  uint32_t carry_head = 0, carry_row = kNone;
-  uint64_t carry_surv = 0;
+  // the tile's M slots from a uniform base: in-tile byte offsets are 32-bit
+  char* const mtile = reinterpret_cast<char*>(o.mcol + uniform64(d.qbase + (uint64_t(row0) << lg)));
+  carry_row = kNone;
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
     const bool in = i < nlist;
     const uint2 e = in ? st.list[i] : make_uint2(0u, 0u);
     const uint32_t row = in ? (e.y >> lg) : kNone;
-    uint32_t prow = dpp_wave_shr1(row);
+    uint32_t prow = dpp_wave_shr1_z(row);
     if (lane == 0) prow = carry_row;
-    const bool head = in && row != prow;
-    bool surv = false;
-    if (head) {
+    if (in && row != prow) {
       const uint32_t pk = st.acc[row];
-      st.acc[row] = 0;
+      bool surv = false;
       if (row0 + row < d.nrows)
         surv = k1_finish_row(d.start + row0 + row, tu, static_cast<uint16_t>(pk & 0xFFFFu), pk >> 16, pk >> 16, s_adj,
                              keep, oa, o, acc, s_hist);
+      st.acc[row] = i | (surv ? 0x80000000u : 0u);
       if (surv) atomicOr(&st.sm[row >> 6], 1ull << (row & 63));
     }
-    const uint64_t H = __ballot(head);
-    const uint64_t Sv = __ballot(surv);
-    const uint64_t hm = H & ((2ull << lane) - 1);  // heads at or below this lane
-    const uint32_t hl = hm ? 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(hm))) : 0u;
-    const uint32_t hidx = hm ? i0 + hl : carry_head;
-    const uint64_t mys = hm ? ((Sv >> hl) & 1ull) : carry_surv;
-    if (!(MODE & 1) && in && mys) o.mcol[d.qbase + (uint64_t(row0 + row) << lg) + (i - hidx)] = e.x | kAlive;
-    if (H) {
-      const uint32_t hlast = 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(H)));
-      carry_head = i0 + hlast;
-      carry_surv = (Sv >> hlast) & 1ull;
+    __builtin_amdgcn_wave_barrier();
+    if (in) {
+      const uint32_t w = st.acc[row];
+      if (!(MODE & 1) && (w >> 31))
+        *reinterpret_cast<uint32_t*>(mtile + (((row << lg) + (i - (w & 0x7FFFFFFFu))) << 2)) = e.x | kAlive;
     }
     carry_row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), kWave - 1));
   }
@@ -575,7 +580,7 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t 
 // after phase B1.  WIDE: some range has more than four
 // relevant label runs (tbits_rel scans them all).
 template <int MODE, bool WIDE = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_lcc_first(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, uint32_t nhseg, unsigned long long* __restrict__ tmask,

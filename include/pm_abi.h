@@ -130,6 +130,15 @@ int pm_lcc_bsp(pm_ctx* ctx, int init_step, uint64_t itr, pm_lcc_stats* out);
 /* One NLC line (index pl): path/cycle walk for pl < 4, TDS for pl >= 4. */
 int pm_token_passing(pm_ctx* ctx, uint32_t pl, pm_tp_stats* out);
 
+/* One TDS line (pl >= 4) with its kept walks handed to `sink` instead of a subgraph
+ * file: the reference writes each walk as "[rank], v0, ..., vk, [vk]" into its open
+ * stream (token_passing_pattern_matching_nonunique_tds_batch_1.hpp:739-743, the
+ * stream opened by run_pattern_matching_beta.cpp:713-717); here the sink gets that
+ * rank (owner of the last vertex), the vertex ids v0..vk and k + 1.  The walk array
+ * is valid during the call only.  Single-GPU contexts. */
+typedef void (*pm_path_sink)(void* user, uint32_t rank, const uint32_t* vertices, uint32_t length);
+int pm_tds(pm_ctx* ctx, uint32_t pl, pm_path_sink sink, void* user, pm_tp_stats* out);
+
 /* Post-processing of the last pm_token_passing call; *deleted = any source invalidated. */
 int pm_post_token_passing(pm_ctx* ctx, uint32_t pl, uint32_t* deleted);
 

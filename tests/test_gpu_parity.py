@@ -150,6 +150,28 @@ def test_step_api_matches_driver():
     m.close()
 
 
+def test_tds_walk_sink_matches_subgraph_file(tmp_path):
+    """pm_tds hands each kept walk to a callback: iteration 0 of the hand-derived
+    patterns/triangle_tail_tds_pattern input (four triangles) through the step API gives the
+    lines of the oracle's subgraphs_4_0 after one iteration (tests/test_cpu_hazards.py)."""
+    pat = os.path.join(pmtest.ROOT, "patterns", "triangle_tail_tds_pattern")
+    pairs = [(3 * t + a, 3 * t + b) for t in range(4) for a, b in ((0, 1), (1, 2), (0, 2))] + [(1, 3), (7, 10)]
+    off, col = pmtest.symmetric_csr(pairs, 12)
+    labels = np.array([3, 4, 5] * 4, np.uint64)
+    oracle.run(off, col, pat, str(tmp_path), labels=labels, max_iterations=1)
+    want = sorted(l for l in open(tmp_path / "0" / "all_ranks_subgraphs" / "subgraphs_4_0").read().split("\n") if l)
+    m = pm.PatternMatcher(pm.Graph(off, col, True), pat, labels=labels)
+    m.reset()
+    m.lcc_bsp(True)
+    for pl in range(4):
+        m.token_passing(pl)
+        m.post_token_passing(pl)
+    got = []
+    st = m.tds(4, lambda rank, v: got.append(f"[{rank}], " + ", ".join(map(str, v)) + f", [{v[-1]}]"))
+    m.close()
+    assert sorted(got) == want and len(want) == 4 and st["walks"] == 4
+
+
 def test_iteration_cap_reports_non_termination(tmp_path):
     g = pm.rmat_graph(12, 4)
     labels = pmtest.hash_labels(g.n, 8)
