@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpm.so")
+LIB_PATH = os.environ.get("PM_LIB") or os.path.join(_HERE, "lib", "libpm.so")  # PM_LIB: diagnostic builds
 
 c_u64 = ctypes.c_uint64
 c_u32 = ctypes.c_uint32

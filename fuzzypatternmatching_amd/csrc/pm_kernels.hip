@@ -295,6 +295,14 @@ __device__ __forceinline__ void k1_slice(uint32_t v, uint16_t tv, uint32_t j, ui
   if (cm) tnacc |= tv;
 }
 
+// A wave-uniform 64-bit value held in scalar registers.  readfirstlane returns
+// int: each half goes through uint32_t, or the low half would sign-extend.
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32)));
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x)));
+  return (uint64_t(hi) << 32) | lo;
+}
+
 // Uniform description of one superstep-0 tile, resolved from the KRange table.
 struct K1Desc {
   uint64_t qbase;  // first slot of the run
@@ -315,8 +323,7 @@ __device__ __forceinline__ K1Desc k1_desc(const KRange* s_tab, uint32_t& r, uint
   d.start = __builtin_amdgcn_readfirstlane(s_tab[r].start);
   d.nrows = __builtin_amdgcn_readfirstlane(s_tab[r].end) - d.start;
   d.rel = t - __builtin_amdgcn_readfirstlane(s_tab[r].tile0);
-  d.qbase = (uint64_t(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase >> 32))) << 32) |
-            __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s_tab[r].qbase));
+  d.qbase = uniform64(s_tab[r].qbase);
   return d;
 }
 
@@ -352,11 +359,7 @@ struct K1Stage {
   unsigned long long sm[kSub];  // survivor bits of the tile's rows
 };
 
-// A wave-uniform 64-bit value held in scalar registers.
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-  return (uint64_t(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32))) << 32) |
-         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
-}
+
 
 // Lanes whose slot starts a row, for G = 1 << lg <= 64 slots per row.
 __device__ __forceinline__ uint64_t row_start_mask(uint32_t lg) {
