@@ -87,9 +87,9 @@ struct Arena {
 
 // Superstep-0 tiling of the padded label-major CSR (DESIGN.md "Data
 // layout"): one entry per (pattern label, degree class) run of rows.  kind
-// 0..kHeavyKind-1: rows of degree in (G/2, G], G = 1 << kind <= kHeavyDeg,
-// stored in G padded slots, so the run is a dense rows x G array and a tile
-// is kTileEntries consecutive slots holding 512 / G whole rows; kind
+// 0..kHeavyKind-1: rows of one light degree class, stored in G = kind_slots
+// padded slots, so the run is a dense rows x G array and a tile is rpt =
+// kTileEntries / G whole rows (rpt * G consecutive slots); kind
 // kHeavyKind: rows above kHeavyDeg (stored unpadded), one kHeavyDeg-entry
 // segment per tile (HSeg list).
 struct KRange {
@@ -98,7 +98,10 @@ struct KRange {
   uint32_t start, end;  // row positions [start, end)
   uint32_t aux;         // heavy kind: first HSeg index
   uint16_t tu, nm;      // template bits of the label and their neighbour mask
-  uint32_t kind;
+  uint32_t kind;         // light degree class (kind_slots) or kHeavyKind
+  uint32_t g, rpt;       // light: slots per row, whole rows per tile (rpt * g <= kTileEntries)
+  uint32_t rdiv;         // light: slot / g == (slot * rdiv) >> 19 for slot < kTileEntries
+  uint64_t rs[8];        // light: row-start lanes of each 64-slot sub-tile of a tile
   // label runs whose template bits meet nm (the only neighbours that can
   // contribute), first four inline (len 0 = unused); nrel > 4 adds a scan of
   // all LabelRuns
@@ -127,7 +130,7 @@ struct HSeg {
 static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
 static constexpr uint32_t kTileEntries = 64 * kSub; // 512
 static constexpr uint32_t kHeavyDeg = kTileEntries; // light rows fit in one tile
-static constexpr int kHeavyKind = 10;               // log2(kHeavyDeg) + 1
+static constexpr int kHeavyKind = 48;              // light kinds 0..47 (light_kind), heavy above
 static constexpr int kMaxRanges = 16 * (kHeavyKind + 1) + 1;
 // Active-edge map entries: neighbour position | kAlive | kFlag (cycle mark,
 // nem_1.hpp:764-770).  Positions use 30 bits (V < 2^30).
@@ -135,13 +138,27 @@ static constexpr uint32_t kAlive = 1u << 31;
 static constexpr uint32_t kFlag = 1u << 30;
 static constexpr uint32_t kPosMask = kFlag - 1;
 
-// Padded row length: nextpow2(degree) up to kHeavyDeg, the degree above.
+// Light degree classes (degree 1..kHeavyDeg): the padded row length G of a
+// class is the degree itself up to 16, then rounded up to a multiple of 4 (to
+// 64), of 8 (to 128) and of 32 (to 512): at most a few percent of padding on
+// R-MAT degree mixes (power-of-two classes padded ~24 %).
+__host__ __device__ inline uint32_t light_kind(uint64_t d) {  // 1 <= d <= kHeavyDeg
+  if (d <= 16) return static_cast<uint32_t>(d - 1);
+  if (d <= 64) return 16 + static_cast<uint32_t>(d - 17) / 4;
+  if (d <= 128) return 28 + static_cast<uint32_t>(d - 65) / 8;
+  return 36 + static_cast<uint32_t>(d - 129) / 32;
+}
+__host__ __device__ inline uint32_t kind_slots(uint32_t k) {
+  if (k < 16) return k + 1;
+  if (k < 28) return 20 + 4 * (k - 16);
+  if (k < 36) return 72 + 8 * (k - 28);
+  return 160 + 32 * (k - 36);
+}
+
+// Padded row length: the class length up to kHeavyDeg, the degree above.
 __host__ __device__ inline uint64_t padded_degree(uint64_t d) {
-  if (d <= 1) return d;
-  if (d > kHeavyDeg) return d;
-  uint64_t g = 1;
-  while (g < d) g <<= 1;
-  return g;
+  if (d == 0 || d > kHeavyDeg) return d;
+  return kind_slots(light_kind(d));
 }
 
 // Outputs of one fused NLC-line kernel (pm_lines.hip), device resident.

@@ -168,21 +168,26 @@ struct RelRuns {
   uint32_t nadm;
 };
 
-__device__ __forceinline__ RelRuns load_rel(const KRange& R) {
+// The range table is read through the constant address space: every index
+// into it is wave-uniform, so the fields arrive by scalar loads (SGPRs, no LDS
+// copy, no readfirstlane).
+typedef __attribute__((address_space(4))) const KRange* KTab;
+
+__device__ __forceinline__ RelRuns load_rel(KTab R) {
   RelRuns x;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    x.lo[i] = __builtin_amdgcn_readfirstlane(R.rlo[i]);
-    x.len[i] = __builtin_amdgcn_readfirstlane(R.rlen[i]);
-    x.tu[i] = __builtin_amdgcn_readfirstlane(R.rtu[i]);
+    x.lo[i] = __builtin_amdgcn_readfirstlane(R->rlo[i]);
+    x.len[i] = __builtin_amdgcn_readfirstlane(R->rlen[i]);
+    x.tu[i] = __builtin_amdgcn_readfirstlane(R->rtu[i]);
   }
-  x.nrel = __builtin_amdgcn_readfirstlane(R.nrel);
+  x.nrel = __builtin_amdgcn_readfirstlane(R->nrel);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    x.alo[i] = __builtin_amdgcn_readfirstlane(R.alo[i]);
-    x.alen[i] = __builtin_amdgcn_readfirstlane(R.alen[i]);
+    x.alo[i] = __builtin_amdgcn_readfirstlane(R->alo[i]);
+    x.alen[i] = __builtin_amdgcn_readfirstlane(R->alen[i]);
   }
-  x.nadm = __builtin_amdgcn_readfirstlane(R.nadm);
+  x.nadm = __builtin_amdgcn_readfirstlane(R->nadm);
   return x;
 }
 
@@ -206,14 +211,14 @@ struct KeepArgs {
   uint32_t n;
 };
 
-__device__ __forceinline__ KeepArgs load_keep(const KRange& R) {
+__device__ __forceinline__ KeepArgs load_keep(KTab R) {
   KeepArgs k;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    k.bit[i] = __builtin_amdgcn_readfirstlane(R.kbit[i]);
-    k.need[i] = __builtin_amdgcn_readfirstlane(R.kneed[i]);
+    k.bit[i] = __builtin_amdgcn_readfirstlane(R->kbit[i]);
+    k.need[i] = __builtin_amdgcn_readfirstlane(R->kneed[i]);
   }
-  k.n = __builtin_amdgcn_readfirstlane(R.nkeep);
+  k.n = __builtin_amdgcn_readfirstlane(R->nkeep);
   return k;
 }
 
@@ -309,70 +314,74 @@ struct K1Desc {
   uint32_t start;  // first row position of the run
   uint32_t nrows;  // rows of the run
   uint32_t rel;    // tile index inside the run
-  uint32_t kind;   // log2 G (light) or kHeavyKind
+  uint32_t kind;   // light degree class or kHeavyKind
+  uint32_t g;      // light: slots per row
+  uint32_t rpt;    // light: rows per tile
+  uint32_t rdiv;   // light: row of a slot = (slot * rdiv) >> 19
   uint32_t r;      // KRange index
 };
 
 // Advances the wave's range cursor r to the range holding tile t (tiles are
 // visited in increasing order by each wave) and returns the tile's description.
-__device__ __forceinline__ K1Desc k1_desc(const KRange* s_tab, uint32_t& r, uint32_t t) {
-  while (__builtin_amdgcn_readfirstlane(s_tab[r + 1].tile0) <= t) ++r;
+__device__ __forceinline__ K1Desc k1_desc(KTab kt, uint32_t& r, uint32_t t) {
+  while (kt[r + 1].tile0 <= t) ++r;
   K1Desc d;
   d.r = r;
-  d.kind = __builtin_amdgcn_readfirstlane(s_tab[r].kind);
-  d.start = __builtin_amdgcn_readfirstlane(s_tab[r].start);
-  d.nrows = __builtin_amdgcn_readfirstlane(s_tab[r].end) - d.start;
-  d.rel = t - __builtin_amdgcn_readfirstlane(s_tab[r].tile0);
-  d.qbase = uniform64(s_tab[r].qbase);
+  d.kind = kt[r].kind;
+  d.g = kt[r].g;
+  d.rpt = kt[r].rpt;
+  d.rdiv = kt[r].rdiv;
+  d.start = kt[r].start;
+  d.nrows = kt[r].end - d.start;
+  d.rel = t - kt[r].tile0;
+  d.qbase = kt[r].qbase;
   return d;
 }
 
-// The kSub x 64 slots of a light tile (kNone past the run): one load per
-// lane and sub-tile, all issued before any use.  The loads are unconditional
-// and use one uniform base + the lane offset (the slot buffers carry
-// kTileEntries entries of tail padding, so a partial tile, a heavy tile or a
-// tile past the end reads in bounds; such slots are replaced by kNone).
+// Pins a loop-carried descriptor to scalar registers (the compiler otherwise
+// keeps it in VGPRs and turns every range-table read into a vector load).
+__device__ __forceinline__ void k1_uniform(K1Desc& d) {
+  d.r = __builtin_amdgcn_readfirstlane(d.r);
+  d.kind = __builtin_amdgcn_readfirstlane(d.kind);
+  d.g = __builtin_amdgcn_readfirstlane(d.g);
+  d.rpt = __builtin_amdgcn_readfirstlane(d.rpt);
+  d.rdiv = __builtin_amdgcn_readfirstlane(d.rdiv);
+  d.start = __builtin_amdgcn_readfirstlane(d.start);
+  d.nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+  d.rel = __builtin_amdgcn_readfirstlane(d.rel);
+  d.qbase = uniform64(d.qbase);
+}
+
+// The rpt * g slots of a light tile (kNone past them): one load per lane and
+// sub-tile, all issued before any use, from one uniform base + the lane
+// offset.  Lanes past the tile's slots load nothing (a heavy tile or a tile
+// past the end loads nothing at all).
 __device__ __forceinline__ void k1_load(uint32_t (&v)[kSub], const K1Desc& d, const uint32_t* __restrict__ colp,
                                         bool valid) {
   const int lane = lane_id();
-  const uint64_t t0 = uint64_t(d.rel) * kTileEntries;
   const bool light = valid && d.kind < static_cast<uint32_t>(kHeavyKind);
-  const uint64_t tend = light ? uint64_t(d.nrows) << d.kind : 0;
-  const uint32_t rem = tend > t0 ? static_cast<uint32_t>(min<uint64_t>(tend - t0, kTileEntries)) : 0u;
-  const uint32_t* tp = colp + (rem ? d.qbase + t0 : 0);
+  // slots of the tile inside the run, in 32-bit row arithmetic (rows < 2^30)
+  const uint32_t r0 = d.rel * d.rpt;
+  const uint32_t rows = light && d.nrows > r0 ? min(d.nrows - r0, d.rpt) : 0u;
+  const uint32_t rem = rows * d.g;
+  const uint32_t* tp = colp + (rem ? d.qbase + uint64_t(r0) * d.g : 0);
 #pragma unroll
-  for (int q = 0; q < kSub; ++q) v[q] = __builtin_nontemporal_load(tp + q * kWave + lane);
-  if (rem < kTileEntries) {  // wave-uniform: only partial tiles pay the masking
-#pragma unroll
-    for (int q = 0; q < kSub; ++q)
-      if (static_cast<uint32_t>(q * kWave + lane) >= rem) v[q] = kNone;
-  }
+  for (int q = 0; q < kSub; ++q)
+    v[q] = static_cast<uint32_t>(q * kWave + lane) < rem ? __builtin_nontemporal_load(tp + q * kWave + lane) : kNone;
 }
 
-// Per-wave LDS staging of a light tile: per-row accumulators (TN | count << 16,
-// one word per row of the tile) and the tile's contributing entries in slot
-// order (neighbour position, slot), which become M rows once the verify has
-// decided which rows survive.
+// Per-wave LDS staging of a light tile: the tile's contributing entries in
+// slot order (neighbour position, row inside the tile), which become M rows
+// once the verify has decided which rows survive, and per-row accumulators:
+// TN (two rows per word, zero between tiles) and the row's first / last + 1
+// list index (valid while its TN is non-zero).
 struct K1Stage {
-  uint32_t acc[kTileEntries];
-  uint2 list[kTileEntries];     // (neighbour position, slot inside the tile)
+  uint32_t lx[kTileEntries];
+  uint16_t lrow[kTileEntries];
+  uint16_t hd[kTileEntries], tl[kTileEntries];
+  uint32_t tn[kTileEntries / 2];
   unsigned long long sm[kSub];  // survivor bits of the tile's rows
 };
-
-
-
-// Lanes whose slot starts a row, for G = 1 << lg <= 64 slots per row.
-__device__ __forceinline__ uint64_t row_start_mask(uint32_t lg) {
-  switch (lg) {
-    case 0: return ~0ull;
-    case 1: return 0x5555555555555555ull;
-    case 2: return 0x1111111111111111ull;
-    case 3: return 0x0101010101010101ull;
-    case 4: return 0x0001000100010001ull;
-    case 5: return 0x0000000100000001ull;
-    default: return 1ull;
-  }
-}
 
 // Phase A of a light tile: appends the tile's contributing slots (neighbour
 // position in an admitted run, first occurrence in its row) to the wave's
@@ -381,7 +390,7 @@ __device__ __forceinline__ uint64_t row_start_mask(uint32_t lg) {
 // test (more than four runs).  The compares land in 64-bit lane masks and
 // the row-start / first-occurrence logic stays on the scalar unit.
 template <int NR, bool WIDE>
-__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], bool big, uint32_t gm, uint64_t rs_light,
+__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R, uint32_t rdiv,
                                                const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
                                                uint16_t nm, K1Stage& st) {
   const int lane = lane_id();
@@ -398,23 +407,22 @@ __device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], bool b
     }
     // first occurrence: differs from the left neighbour lane; lane 0 compares
     // with the previous sub-tile's last slot, which matters only when a row
-    // continues across sub-tiles (G > 64; for G <= 64 lane 0 starts a row)
+    // continues across sub-tiles (else lane 0 starts a row)
     uint64_t ne_m = __builtin_amdgcn_ballot_w64(dpp_wave_shr1_z(x) != x);
-    if (q > 0) {  // (q = 0: lane 0 starts a row for every G)
+    if (q > 0) {  // (q = 0: the tile starts with a row)
       const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[q - 1]), kWave - 1));
       const uint32_t x0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 0));
       // (c != x0) as integer carry arithmetic: a bool here would be widened on the VALU
       ne_m = (ne_m & ~1ull) | ((uint64_t(c ^ x0) + 0xFFFFFFFFull) >> 32);
     }
-    // row starts of this sub-tile (G <= 64: every G-th lane; larger G: lane 0
-    // when the sub-tile starts a row)
-    const uint64_t rsq = big ? (((q * kWave) & gm) == 0 ? 1ull : 0ull) : rs_light;
-    const uint64_t C = in_m & (rsq | ne_m);
+    // row starts of this sub-tile: the same in every tile of the range
+    const uint64_t C = in_m & (R->rs[q] | ne_m);
     if (C) {
       if ((C >> lane) & 1ull) {
         const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_amdgcn_mbcnt_hi(
                                          static_cast<uint32_t>(C >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C), 0)));
-        st.list[idx] = make_uint2(x, static_cast<uint32_t>(q * kWave + lane));
+        st.lx[idx] = x;
+        st.lrow[idx] = static_cast<uint16_t>((static_cast<uint32_t>(q * kWave + lane) * rdiv) >> 19);
       }
       nlist += static_cast<uint32_t>(__builtin_popcountll(C));
     }
@@ -422,109 +430,105 @@ __device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], bool b
   return nlist;
 }
 
-// Light tile (G = 1 << kind <= kTileEntries slots per row, 512 / G whole rows).
+// Light tile (G = d.g slots per row, d.rpt = kTileEntries / G whole rows).
 // Phase A, per sub-tile, all in wave masks: a lane's neighbour can contribute
 // iff its position lies in one of the range's relevant label runs (one
 // compare per run, the masks OR-ed on the scalar unit) and it is the first
 // occurrence in its row (row start, or differs from the left neighbour lane);
 // only the contributing lanes (a few percent of the slots) are appended to
-// the LDS staging list.  Phase B over the list only: row TN / count
-// accumulated in LDS, heads verify their row, survivors' entries write M[u].
+// the LDS staging list.  Phase B: row TN / first and last list index from the
+// list (B1), one lane per row verifies (B2), survivors' entries write M[u] (B3).
 template <int MODE, bool WIDE>
-__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K1Desc& d, uint16_t tu, uint16_t nm,
+__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K1Desc& d, KTab R, uint16_t tu,
+                                              uint16_t nm,
                                               const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
                                               const KeepArgs& keep, const uint16_t* s_adj, const OwnerArgs& oa,
                                               const K1Out& o, BlockAcc& acc, unsigned long long* s_hist,
                                               unsigned long long* tm, K1Stage& st) {
   const int lane = lane_id();
-  const uint32_t lg = __builtin_amdgcn_readfirstlane(d.kind);
-  const uint32_t gm = (1u << lg) - 1;
-  const bool big = lg > 6;  // rows span sub-tiles
-  const uint64_t rs_light = uniform64(row_start_mask(lg));
+  const uint32_t g = d.g, rpt = d.rpt;
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
   if (WIDE || rel_runs.nadm > 4)
-    nlist = k1_phase_a<0, WIDE>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<0, WIDE>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else if (rel_runs.nadm <= 1)
-    nlist = k1_phase_a<1, false>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<1, false>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else if (rel_runs.nadm == 2)
-    nlist = k1_phase_a<2, false>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<2, false>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else
-    nlist = k1_phase_a<4, false>(v, big, gm, rs_light, rel_runs, s_runs, nruns, nm, st);
-  if (lane < kSub) st.sm[lane] = 0ull;
+    nlist = k1_phase_a<4, false>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   if ((MODE & 16) || nlist == 0) {  // MODE 16 (diagnostic): phase A only
     if (lane < kSub && !(MODE & 64)) tm[lane] = 0ull;  // MODE 64: without this store
     return;
   }
   __builtin_amdgcn_wave_barrier();
-  // phase B1: row TN (neighbour-mask bits of the contributors' template bits)
-  // and count; the list is in slot order, so a row's entries are consecutive
-  // and its first entry (head) resets the row's word before the others add
-  // (LDS operations of one wave complete in order)
-  uint32_t carry_row = kNone;
+  // phase B1 over the list: a row's entries are consecutive (slot order), so
+  // its first entry records the row's first list index and its last entry the
+  // end; TN is OR-ed into the row's half word
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
-    const bool in = i < nlist;
-    const uint2 e = in ? st.list[i] : make_uint2(0u, 0u);
-    const uint32_t row = in ? (e.y >> lg) : kNone;
-    uint32_t prow = dpp_wave_shr1_z(row);
-    if (lane == 0) prow = carry_row;
-    if (in && row != prow) st.acc[row] = 0u;
-    if (in) {
-      atomicOr(&st.acc[row], static_cast<uint32_t>(tbits_rel<WIDE>(e.x, rel_runs, s_runs, nruns) & nm));
-      atomicAdd(&st.acc[row], 1u << 16);
+    if (i < nlist) {
+      const uint32_t x = st.lx[i];
+      const uint32_t row = st.lrow[i];
+      const uint32_t prow = i ? st.lrow[i - 1] : 0xFFFFu;
+      const uint32_t nrow = i + 1 < nlist ? st.lrow[i + 1] : 0xFFFFu;
+      if (row != prow) st.hd[row] = static_cast<uint16_t>(i);
+      if (row != nrow) st.tl[row] = static_cast<uint16_t>(i + 1);
+      atomicOr(&st.tn[row >> 1], static_cast<uint32_t>(tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm)
+                                     << ((row & 1u) << 4));
     }
-    carry_row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), kWave - 1));
   }
   __builtin_amdgcn_wave_barrier();
   if (MODE & 32) {  // diagnostic: phase A + B1 only
     if (lane < kSub) tm[lane] = 0ull;
-#pragma unroll 1
-    for (uint32_t i = lane; i < nlist; i += kWave) st.acc[st.list[i].y >> lg] = 0;
+    for (uint32_t r = lane; r < rpt; r += 2 * kWave) st.tn[r >> 1] = 0;
     return;
   }
-  // phase B2: the head of each row verifies it and leaves (its list index,
-  // survived) in the row's word; every entry then reads its row's word and a
-  // survivor's entries write M[u] in slot order at the start of u's padded row
-  const uint32_t row0 = d.rel * (kTileEntries >> lg);
-  // the tile's M slots from a uniform base: in-tile byte offsets are 32-bit
-  char* const mtile = reinterpret_cast<char*>(o.mcol + uniform64(d.qbase + (uint64_t(row0) << lg)));
-  carry_row = kNone;
+  // phase B2, one lane per row of the tile (consecutive positions, so the
+  // state stores coalesce): verify the rows with contributors, reset TN
+  const uint32_t row0 = d.rel * rpt;
+  uint64_t any = 0;
+#pragma unroll 1
+  for (uint32_t r0 = 0; r0 < rpt; r0 += kWave) {
+    const uint32_t row = r0 + lane;
+    bool surv = false;
+    if (row < rpt) {
+      const uint16_t TN = static_cast<uint16_t>(st.tn[row >> 1] >> ((row & 1u) << 4));
+      if (TN && row0 + row < d.nrows) {
+        const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
+        surv = k1_finish_row(d.start + row0 + row, tu, TN, cnt, cnt, s_adj, keep, oa, o, acc, s_hist);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (row < rpt && !(row & 1u)) st.tn[row >> 1] = 0u;
+    const uint64_t b = __builtin_amdgcn_ballot_w64(surv);
+    if (lane == 0) st.sm[r0 / kWave] = b;
+    any |= b;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t ngroups = (rpt + kWave - 1) / kWave;
+  if (lane < kSub) tm[lane] = static_cast<uint32_t>(lane) < ngroups ? st.sm[lane] : 0ull;  // bit r = row r
+  if ((MODE & 1) || !any) return;
+  // phase B3: survivors' entries write M[u] in slot order at the start of u's
+  // padded row (the tile's M slots from a uniform base: 32-bit offsets)
+  char* const mtile = reinterpret_cast<char*>(o.mcol + (d.qbase + uint64_t(row0) * g));
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
-    const bool in = i < nlist;
-    const uint2 e = in ? st.list[i] : make_uint2(0u, 0u);
-    const uint32_t row = in ? (e.y >> lg) : kNone;
-    uint32_t prow = dpp_wave_shr1_z(row);
-    if (lane == 0) prow = carry_row;
-    if (in && row != prow) {
-      const uint32_t pk = st.acc[row];
-      bool surv = false;
-      if (row0 + row < d.nrows)
-        surv = k1_finish_row(d.start + row0 + row, tu, static_cast<uint16_t>(pk & 0xFFFFu), pk >> 16, pk >> 16, s_adj,
-                             keep, oa, o, acc, s_hist);
-      st.acc[row] = i | (surv ? 0x80000000u : 0u);
-      if (surv) atomicOr(&st.sm[row >> 6], 1ull << (row & 63));
+    if (i < nlist) {
+      const uint32_t row = st.lrow[i];
+      if ((st.sm[row / kWave] >> (row % kWave)) & 1ull)
+        *reinterpret_cast<uint32_t*>(mtile + ((row * g + (i - st.hd[row])) << 2)) = st.lx[i] | kAlive;
     }
-    __builtin_amdgcn_wave_barrier();
-    if (in) {
-      const uint32_t w = st.acc[row];
-      if (!(MODE & 1) && (w >> 31))
-        *reinterpret_cast<uint32_t*>(mtile + (((row << lg) + (i - (w & 0x7FFFFFFFu))) << 2)) = e.x | kAlive;
-    }
-    carry_row = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), kWave - 1));
   }
-  __builtin_amdgcn_wave_barrier();
-  if (lane < kSub) tm[lane] = st.sm[lane];  // survivor bit r = row r of the tile
 }
 
 // Heavy rows (above kHeavyDeg): one kHeavyDeg segment per tile, uncompacted M;
 // the segments' TN / counts meet in the hscr scratch and the last segment to
 // finish (ticket) runs the verify.  Rare: kept out of line.
 template <int MODE, bool WIDE>
-__device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t hi,
+__device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
                                                             const HSeg* __restrict__ hseg,
                                                             const uint64_t* __restrict__ offp,
                                                             const uint32_t* __restrict__ colp, const uint32_t* s_runs,
@@ -534,9 +538,9 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(const KRange* s_tab, uint32_t 
   BlockAcc acc;
   const int lane = lane_id();
   const HSeg hs = hseg[hi];
-  const KRange& R = s_tab[__builtin_amdgcn_readfirstlane(hs.range)];
-  const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.tu));
-  const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.nm));
+  const KTab R = kt + __builtin_amdgcn_readfirstlane(hs.range);
+  const uint16_t tu = R->tu;
+  const uint16_t nm = R->nm;
   const RelRuns rel_runs = load_rel(R);
   const KeepArgs keep = load_keep(R);
   const uint64_t b0 = offp[hs.row];
@@ -588,13 +592,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, uint32_t nhseg, unsigned long long* __restrict__ tmask,
     Partials pp) {
-  extern __shared__ KRange s_tab[];  // nr + 1 entries (dynamic LDS)
+  const KTab kt = (KTab)ktab;  // nr + 1 entries, read by scalar loads
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
   __shared__ uint32_t s_runs[3 * 16];
   __shared__ K1Stage s_stage[kWpb];
-  for (uint32_t i = threadIdx.x; i <= nr; i += blockDim.x) s_tab[i] = ktab[i];
   load_adj(s_adj, pa);
   if (threadIdx.x < 16) {
     const int l = threadIdx.x;
@@ -605,7 +608,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform
   K1Stage& st = s_stage[wid];
-  for (int i = threadIdx.x % kWave; i < static_cast<int>(kTileEntries); i += kWave) st.acc[i] = 0;
+  for (int i = threadIdx.x % kWave; i < static_cast<int>(kTileEntries / 2); i += kWave) st.tn[i] = 0;
   __syncthreads();
   BlockAcc acc;
   const uint32_t W = gridDim.x * kWpb;
@@ -615,25 +618,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   // the next tile's slots are in flight while the current one is processed
   uint32_t vc[kSub], vn[kSub];
   K1Desc cur{};
-  if (t < ntiles) cur = k1_desc(s_tab, r, t);
+  if (t < ntiles) cur = k1_desc(kt, r, t);
   k1_load(vc, cur, colp, t < ntiles);
   while (t < ntiles) {
     const uint32_t tn = t + W;
     K1Desc nxt{};
-    if (tn < ntiles) nxt = k1_desc(s_tab, r, tn);
+    if (tn < ntiles) nxt = k1_desc(kt, r, tn);
     k1_load(vn, nxt, colp, tn < ntiles);
-    const KRange& R = s_tab[cur.r];
+    k1_uniform(cur);
+    const KTab R = kt + cur.r;
     unsigned long long* tm = tmask + uint64_t(t) * kSub;
     if (cur.kind < static_cast<uint32_t>(kHeavyKind)) {
-      const uint16_t tu = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.tu));
-      const uint16_t nm = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(R.nm));
+      const uint16_t tu = R->tu;
+      const uint16_t nm = R->nm;
       const RelRuns rel_runs = load_rel(R);
       if (MODE & 8) {
 #pragma unroll
         for (int q = 0; q < kSub; ++q) acc.vs += vc[q] ^ tbits_rel<WIDE>(vc[q], rel_runs, s_runs, nruns);
       } else if (!(MODE & 2)) {
         const KeepArgs keep = load_keep(R);
-        k1_light_tile<MODE, WIDE>(vc, cur, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
+        k1_light_tile<MODE, WIDE>(vc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
       }
     }  // heavy tiles: the loop below
     t = tn;
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   // buffers live, so the light loop's register budget is its own)
   if (!(MODE & 4))
     for (uint32_t hi = blockIdx.x * kWpb + wid; hi < nhseg; hi += W) {
-      const BlockAcc h = k1_heavy_tile<MODE, WIDE>(s_tab, hi, hseg, offp, colp, s_runs, nruns, s_adj, oa, o, hscr,
+      const BlockAcc h = k1_heavy_tile<MODE, WIDE>(kt, hi, hseg, offp, colp, s_runs, nruns, s_adj, oa, o, hscr,
                                                    nheavy, s_hist, tmask + uint64_t(hseg[hi].tile) * kSub);
       acc.vs += h.vs;
       acc.es += h.es;
@@ -677,7 +681,7 @@ __global__ void k_slist_write(const KRange* __restrict__ ktab, uint32_t nr, cons
       m &= m - 1;
       uint32_t row;
       if (R.kind < static_cast<uint32_t>(kHeavyKind)) {  // bit r of the tile = row r of the tile
-        row = R.start + rel * (kTileEntries >> R.kind) + q * kWave + b;
+        row = R.start + rel * R.rpt + q * kWave + b;
       } else {
         row = hseg[R.aux + rel].row;
       }
@@ -1096,14 +1100,12 @@ __global__ void k_owner_keys(const uint32_t* __restrict__ ids, uint64_t n, uint3
     key[i] = ids[i] % nshards;
 }
 
-// degree class: 0 for degree 0, 1 + k for padded degree 1 << k (k < kHeavyKind),
-// kHeavyKind + 1 above kHeavyDeg
+// degree class: 0 for degree 0, 1 + light_kind for degree <= kHeavyDeg,
+// kHeavyKind + 1 above (monotone in the degree)
 __host__ __device__ inline uint32_t degree_class(uint64_t d) {
   if (d == 0) return 0;
   if (d > kHeavyDeg) return kHeavyKind + 1;
-  uint32_t k = 0;
-  while ((1ull << k) < d) ++k;
-  return 1 + k;
+  return 1 + light_kind(d);
 }
 
 __global__ void k_class_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ ids, uint64_t n,
@@ -1149,7 +1151,7 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
       PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids2, ids, static_cast<int>(n), 0,
                                                       obits, c.stream));
       hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, ids, n, dkey);
-      PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 4,
+      PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 6,
                                                       c.stream));
     }
     hipLaunchKernelGGL(k_gather_labels, dim3(g), dim3(kBlock), 0, c.stream, c.d_labels, ids2, n, lkey);
@@ -1197,7 +1199,7 @@ void build_tiling(Ctx& c) {
   const int nl = static_cast<int>(labs.size());
   // Run boundaries in the label-major order (host binary searches over
   // perm_host): B[0] = first position with the label, B[1 + k] = first with
-  // padded degree >= 1 << k (k < kHeavyKind), B[1 + kHeavyKind] = first with
+  // light kind >= k (k < kHeavyKind), B[1 + kHeavyKind] = first with
   // degree > kHeavyDeg, B[kLB - 1] = one past the label's last position.
   static constexpr int kLB = kHeavyKind + 3;
   const uint64_t n = c.n;
@@ -1258,7 +1260,7 @@ void build_tiling(Ctx& c) {
       for (uint64_t i = B[0]; i < hi; ++i) c.ss0_trav += c.deg_host[c.perm_host[i]];
     if (hi <= first_nz) continue;
     if (c.symmetric) c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
-    // kind k = [B[1+k], B[2+k]) for k < kHeavyKind (padded degree 1 << k); kHeavyKind = [B[1+kHeavyKind], hi)
+    // kind k = [B[1+k], B[2+k]) for k < kHeavyKind (light class k); kHeavyKind = [B[1+kHeavyKind], hi)
     for (int kind = 0; kind <= kHeavyKind; ++kind) {
       const auto ab = owned(B[1 + kind], kind == kHeavyKind ? hi : B[2 + kind]);
       const uint64_t a = ab.first, b = ab.second;
@@ -1272,6 +1274,12 @@ void build_tiling(Ctx& c) {
       R.tu = tu;
       R.nm = nm;
       R.kind = static_cast<uint32_t>(kind);
+      if (kind < kHeavyKind) {
+        R.g = kind_slots(static_cast<uint32_t>(kind));
+        R.rpt = kTileEntries / R.g;
+        R.rdiv = ((1u << 19) + R.g - 1) / R.g;
+        for (uint32_t sl = 0; sl < R.rpt * R.g; sl += R.g) R.rs[sl / 64] |= 1ull << (sl % 64);
+      }
       R.qbase = dev_at(c.d_offp, a);
       R.nrel = 0;
       R.nadm = 0;
@@ -1304,8 +1312,7 @@ void build_tiling(Ctx& c) {
       }
       uint64_t nt;
       if (kind < kHeavyKind) {
-        const uint64_t te = std::max<uint64_t>(kTileEntries, 1ull << kind);
-        nt = ((b - a) * (1ull << kind) + te - 1) / te;
+        nt = (b - a + R.rpt - 1) / R.rpt;
       } else {
         R.aux = static_cast<uint32_t>(hs.size());
         std::vector<uint64_t> o(b - a + 1);
@@ -1374,7 +1381,7 @@ static K1Out k1_out(Ctx& c) {
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
   if (c.ntiles == 0) return;
 #define PM_K1_ARGS                                                                                                    \
-  dim3(grid), dim3(kBlock), c.ktab.size() * sizeof(KRange), c.stream, c.d_ktab,                                    \
+  dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab,                                    \
       static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,                                                  \
       c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c), c.d_hscr, c.nheavy, c.nhseg,                         \
       reinterpret_cast<unsigned long long*>(c.d_tmask), partials(c, d_slot)
@@ -1403,7 +1410,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
 unsigned lcc_first_grid(const Ctx& c) {
   int per_cu = 0;
   PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lcc_first<0>, kBlock,
-                                                           c.ktab.size() * sizeof(KRange)));
+                                                           0));
   hipDeviceProp_t prop;
   PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
   const uint64_t cap = std::min<uint64_t>(kPartGridMax, uint64_t(std::max(per_cu, 1)) * prop.multiProcessorCount);
