@@ -89,7 +89,7 @@ struct Arena {
 // layout"): one entry per (pattern label, degree class) run of rows.  kind
 // 0..kHeavyKind-1: rows of one light degree class, stored in G = kind_slots
 // padded slots, so the run is a dense rows x G array and a tile is rpt =
-// kTileEntries / G whole rows (rpt * G consecutive slots); kind
+// (kTileEntries - 4) / G whole rows (rpt * G consecutive slots); kind
 // kHeavyKind: rows above kHeavyDeg (stored unpadded), one kHeavyDeg-entry
 // segment per tile (HSeg list).
 struct KRange {
@@ -101,7 +101,9 @@ struct KRange {
   uint32_t kind;         // light degree class (kind_slots) or kHeavyKind
   uint32_t g, rpt;       // light: slots per row, whole rows per tile (rpt * g <= kTileEntries)
   uint32_t rdiv;         // light: slot / g == (slot * rdiv) >> 19 for slot < kTileEntries
-  uint64_t rs[8];        // light: row-start lanes of each 64-slot sub-tile of a tile
+  // light: row-start lanes of the 8 load groups (load k, component c: tile
+  // slot 256 k + 4 lane + c - s) for each alignment shift s of the tile base
+  uint64_t rs[4][8];
   // label runs whose template bits meet nm (the only neighbours that can
   // contribute), first four inline (len 0 = unused); nrel > 4 adds a scan of
   // all LabelRuns
@@ -129,8 +131,11 @@ struct HSeg {
 };
 static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
 static constexpr uint32_t kTileEntries = 64 * kSub; // 512
-static constexpr uint32_t kHeavyDeg = kTileEntries; // light rows fit in one tile
-static constexpr int kHeavyKind = 48;              // light kinds 0..47 (light_kind), heavy above
+static constexpr uint32_t kHeavyDeg = kTileEntries; // heavy rows: segments of this many entries
+// Light rows fit in one tile with room for the 16-B alignment shift of its
+// loads (a light tile holds at most kTileEntries - 4 slots).
+static constexpr uint32_t kLightMax = 480;
+static constexpr int kHeavyKind = 47;              // light kinds 0..46 (light_kind), heavy above
 static constexpr int kMaxRanges = 16 * (kHeavyKind + 1) + 1;
 // Active-edge map entries: neighbour position | kAlive | kFlag (cycle mark,
 // nem_1.hpp:764-770).  Positions use 30 bits (V < 2^30).
@@ -138,11 +143,11 @@ static constexpr uint32_t kAlive = 1u << 31;
 static constexpr uint32_t kFlag = 1u << 30;
 static constexpr uint32_t kPosMask = kFlag - 1;
 
-// Light degree classes (degree 1..kHeavyDeg): the padded row length G of a
+// Light degree classes (degree 1..kLightMax): the padded row length G of a
 // class is the degree itself up to 16, then rounded up to a multiple of 4 (to
-// 64), of 8 (to 128) and of 32 (to 512): at most a few percent of padding on
+// 64), of 8 (to 128) and of 32 (to 480): at most a few percent of padding on
 // R-MAT degree mixes (power-of-two classes padded ~24 %).
-__host__ __device__ inline uint32_t light_kind(uint64_t d) {  // 1 <= d <= kHeavyDeg
+__host__ __device__ inline uint32_t light_kind(uint64_t d) {  // 1 <= d <= kLightMax
   if (d <= 16) return static_cast<uint32_t>(d - 1);
   if (d <= 64) return 16 + static_cast<uint32_t>(d - 17) / 4;
   if (d <= 128) return 28 + static_cast<uint32_t>(d - 65) / 8;
@@ -155,9 +160,9 @@ __host__ __device__ inline uint32_t kind_slots(uint32_t k) {
   return 160 + 32 * (k - 36);
 }
 
-// Padded row length: the class length up to kHeavyDeg, the degree above.
+// Padded row length: the class length up to kLightMax, the degree above.
 __host__ __device__ inline uint64_t padded_degree(uint64_t d) {
-  if (d == 0 || d > kHeavyDeg) return d;
+  if (d == 0 || d > kLightMax) return d;
   return kind_slots(light_kind(d));
 }
 

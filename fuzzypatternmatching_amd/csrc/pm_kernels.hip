@@ -352,22 +352,33 @@ __device__ __forceinline__ void k1_uniform(K1Desc& d) {
   d.qbase = uniform64(d.qbase);
 }
 
-// The rpt * g slots of a light tile (kNone past them): one load per lane and
-// sub-tile, all issued before any use, from one uniform base + the lane
-// offset.  Lanes past the tile's slots load nothing (a heavy tile or a tile
-// past the end loads nothing at all).
-__device__ __forceinline__ void k1_load(uint32_t (&v)[kSub], const K1Desc& d, const uint32_t* __restrict__ colp,
-                                        bool valid) {
+// The rpt * g slots of a light tile (kNone outside them) in two 16-B loads per
+// lane, issued before any use: load k, component c of lane l holds the slot
+// at 256 k + 4 l + c of the 16-B aligned window that starts s = base & 3
+// slots before the tile (rpt * g <= kTileEntries - 4, so the window covers
+// the tile).  Lanes whose four slots all lie outside the tile load nothing;
+// a heavy tile or a tile past the end loads nothing at all.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t k1_load(uint32_t (&v)[kSub], const K1Desc& d, const uint32_t* __restrict__ colp,
+                                            bool valid) {
   const int lane = lane_id();
   const bool light = valid && d.kind < static_cast<uint32_t>(kHeavyKind);
   // slots of the tile inside the run, in 32-bit row arithmetic (rows < 2^30)
   const uint32_t r0 = d.rel * d.rpt;
   const uint32_t rows = light && d.nrows > r0 ? min(d.nrows - r0, d.rpt) : 0u;
   const uint32_t rem = rows * d.g;
-  const uint32_t* tp = colp + (rem ? d.qbase + uint64_t(r0) * d.g : 0);
+  const uint64_t b = rem ? d.qbase + uint64_t(r0) * d.g : 0;
+  const uint32_t s = static_cast<uint32_t>(b) & 3u;
+  const u32x4* tp = reinterpret_cast<const u32x4*>(colp + (b - s));
 #pragma unroll
-  for (int q = 0; q < kSub; ++q)
-    v[q] = static_cast<uint32_t>(q * kWave + lane) < rem ? __builtin_nontemporal_load(tp + q * kWave + lane) : kNone;
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t o = static_cast<uint32_t>(k * 256 + 4 * lane);  // window offset of component 0
+    u32x4 w = {kNone, kNone, kNone, kNone};
+    if (o + 3 >= s && o < rem + s) w = __builtin_nontemporal_load(tp + k * kWave + lane);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[4 * k + c] = (o + c >= s && o + c < rem + s) ? w[c] : kNone;
+  }
+  return s;
 }
 
 // Per-wave LDS staging of a light tile: the tile's contributing entries in
@@ -387,44 +398,64 @@ struct K1Stage {
 // position in an admitted run, first occurrence in its row) to the wave's
 // staging list in slot order and returns their number (wave-uniform).  NR
 // merged-run compares (unused runs have length 0); NR = 0: the full label
-// test (more than four runs).  The compares land in 64-bit lane masks and
-// the row-start / first-occurrence logic stays on the scalar unit.
+// test (more than four runs).  Per 16-B load: the compares of its four
+// components land in 64-bit lane masks; a component's left neighbour is the
+// previous component of the same lane (component 0: lane - 1's component 3),
+// the row starts come from the range's masks for the tile's shift s, and a
+// lane's contributors are written in component order after those of the lower
+// lanes (prefix = sum of four masked popcounts), which keeps slot order.
 template <int NR, bool WIDE>
-__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R, uint32_t rdiv,
+__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R, uint32_t s, uint32_t rdiv,
                                                const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
                                                uint16_t nm, K1Stage& st) {
   const int lane = lane_id();
   uint32_t nlist = 0;
 #pragma unroll
-  for (int q = 0; q < kSub; ++q) {
-    const uint32_t x = v[q];
-    uint64_t in_m = 0;  // one ballot per compare: each folds into its compare's mask
-    if (NR == 0) {
-      in_m = __builtin_amdgcn_ballot_w64((tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm) != 0);
-    } else {
+  for (int k = 0; k < 2; ++k) {
+    uint64_t C[4];
 #pragma unroll
-      for (int i = 0; i < NR; ++i) in_m |= __builtin_amdgcn_ballot_w64(x - rel_runs.alo[i] < rel_runs.alen[i]);
-    }
-    // first occurrence: differs from the left neighbour lane; lane 0 compares
-    // with the previous sub-tile's last slot, which matters only when a row
-    // continues across sub-tiles (else lane 0 starts a row)
-    uint64_t ne_m = __builtin_amdgcn_ballot_w64(dpp_wave_shr1_z(x) != x);
-    if (q > 0) {  // (q = 0: the tile starts with a row)
-      const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[q - 1]), kWave - 1));
-      const uint32_t x0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 0));
-      // (c != x0) as integer carry arithmetic: a bool here would be widened on the VALU
-      ne_m = (ne_m & ~1ull) | ((uint64_t(c ^ x0) + 0xFFFFFFFFull) >> 32);
-    }
-    // row starts of this sub-tile: the same in every tile of the range
-    const uint64_t C = in_m & (R->rs[q] | ne_m);
-    if (C) {
-      if ((C >> lane) & 1ull) {
-        const uint32_t idx = nlist + static_cast<uint32_t>(__builtin_amdgcn_mbcnt_hi(
-                                         static_cast<uint32_t>(C >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C), 0)));
-        st.lx[idx] = x;
-        st.lrow[idx] = static_cast<uint16_t>((static_cast<uint32_t>(q * kWave + lane) * rdiv) >> 19);
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t x = v[4 * k + c];
+      uint64_t in_m = 0;  // one ballot per compare: each folds into its compare's mask
+      if (NR == 0) {
+        in_m = __builtin_amdgcn_ballot_w64((tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm) != 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) in_m |= __builtin_amdgcn_ballot_w64(x - rel_runs.alo[i] < rel_runs.alen[i]);
       }
-      nlist += static_cast<uint32_t>(__builtin_popcountll(C));
+      uint64_t ne_m;
+      if (c > 0) {
+        ne_m = __builtin_amdgcn_ballot_w64(v[4 * k + c - 1] != x);
+      } else {
+        ne_m = __builtin_amdgcn_ballot_w64(dpp_wave_shr1_z(v[4 * k + 3]) != x);
+        if (k > 0) {  // lane 0 continues from lane 63's last component of the previous load
+          const uint32_t p = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v[3]), kWave - 1));
+          const uint32_t x0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 0));
+          // (p != x0) as integer carry arithmetic: a bool here would be widened on the VALU
+          ne_m = (ne_m & ~1ull) | ((uint64_t(p ^ x0) + 0xFFFFFFFFull) >> 32);
+        }
+        // k = 0: lane 0's component 0 is either outside the tile or its first slot (a row start)
+      }
+      C[c] = in_m & (R->rs[s][4 * k + c] | ne_m);
+    }
+    const uint64_t any = C[0] | C[1] | C[2] | C[3];
+    if (any) {
+      if ((any >> lane) & 1ull) {
+        uint32_t idx = nlist;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          idx += __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(C[c] >> 32),
+                                           __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C[c]), 0));
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if ((C[c] >> lane) & 1ull) {
+            st.lx[idx] = v[4 * k + c];
+            st.lrow[idx] = static_cast<uint16_t>(((static_cast<uint32_t>(k * 256 + 4 * lane + c) - s) * rdiv) >> 19);
+            ++idx;
+          }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) nlist += static_cast<uint32_t>(__builtin_popcountll(C[c]));
     }
   }
   return nlist;
@@ -439,8 +470,8 @@ __device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R
 // the LDS staging list.  Phase B: row TN / first and last list index from the
 // list (B1), one lane per row verifies (B2), survivors' entries write M[u] (B3).
 template <int MODE, bool WIDE>
-__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K1Desc& d, KTab R, uint16_t tu,
-                                              uint16_t nm,
+__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, const K1Desc& d, KTab R,
+                                              uint16_t tu, uint16_t nm,
                                               const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
                                               const KeepArgs& keep, const uint16_t* s_adj, const OwnerArgs& oa,
                                               const K1Out& o, BlockAcc& acc, unsigned long long* s_hist,
@@ -450,13 +481,13 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], const K
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
   if (WIDE || rel_runs.nadm > 4)
-    nlist = k1_phase_a<0, WIDE>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<0, WIDE>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else if (rel_runs.nadm <= 1)
-    nlist = k1_phase_a<1, false>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<1, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else if (rel_runs.nadm == 2)
-    nlist = k1_phase_a<2, false>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<2, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else
-    nlist = k1_phase_a<4, false>(v, R, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<4, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   if ((MODE & 16) || nlist == 0) {  // MODE 16 (diagnostic): phase A only
     if (lane < kSub && !(MODE & 64)) tm[lane] = 0ull;  // MODE 64: without this store
     return;
@@ -619,13 +650,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   uint32_t vc[kSub], vn[kSub];
   K1Desc cur{};
   if (t < ntiles) cur = k1_desc(kt, r, t);
-  k1_load(vc, cur, colp, t < ntiles);
+  uint32_t sc = k1_load(vc, cur, colp, t < ntiles);
   while (t < ntiles) {
     const uint32_t tn = t + W;
     K1Desc nxt{};
     if (tn < ntiles) nxt = k1_desc(kt, r, tn);
-    k1_load(vn, nxt, colp, tn < ntiles);
+    const uint32_t sn = k1_load(vn, nxt, colp, tn < ntiles);
     k1_uniform(cur);
+    sc = __builtin_amdgcn_readfirstlane(sc);
     const KTab R = kt + cur.r;
     unsigned long long* tm = tmask + uint64_t(t) * kSub;
     if (cur.kind < static_cast<uint32_t>(kHeavyKind)) {
@@ -637,11 +669,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         for (int q = 0; q < kSub; ++q) acc.vs += vc[q] ^ tbits_rel<WIDE>(vc[q], rel_runs, s_runs, nruns);
       } else if (!(MODE & 2)) {
         const KeepArgs keep = load_keep(R);
-        k1_light_tile<MODE, WIDE>(vc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
+        k1_light_tile<MODE, WIDE>(vc, sc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
       }
     }  // heavy tiles: the loop below
     t = tn;
     cur = nxt;
+    sc = sn;
 #pragma unroll
     for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
   }
@@ -1100,11 +1133,11 @@ __global__ void k_owner_keys(const uint32_t* __restrict__ ids, uint64_t n, uint3
     key[i] = ids[i] % nshards;
 }
 
-// degree class: 0 for degree 0, 1 + light_kind for degree <= kHeavyDeg,
+// degree class: 0 for degree 0, 1 + light_kind for degree <= kLightMax,
 // kHeavyKind + 1 above (monotone in the degree)
 __host__ __device__ inline uint32_t degree_class(uint64_t d) {
   if (d == 0) return 0;
-  if (d > kHeavyDeg) return kHeavyKind + 1;
+  if (d > kLightMax) return kHeavyKind + 1;
   return 1 + light_kind(d);
 }
 
@@ -1200,7 +1233,7 @@ void build_tiling(Ctx& c) {
   // Run boundaries in the label-major order (host binary searches over
   // perm_host): B[0] = first position with the label, B[1 + k] = first with
   // light kind >= k (k < kHeavyKind), B[1 + kHeavyKind] = first with
-  // degree > kHeavyDeg, B[kLB - 1] = one past the label's last position.
+  // degree > kLightMax, B[kLB - 1] = one past the label's last position.
   static constexpr int kLB = kHeavyKind + 3;
   const uint64_t n = c.n;
   auto lab_at = [&](uint64_t i) { return c.labels_host[c.perm_host[i]]; };
@@ -1276,9 +1309,13 @@ void build_tiling(Ctx& c) {
       R.kind = static_cast<uint32_t>(kind);
       if (kind < kHeavyKind) {
         R.g = kind_slots(static_cast<uint32_t>(kind));
-        R.rpt = kTileEntries / R.g;
+        R.rpt = (kTileEntries - 4) / R.g;
         R.rdiv = ((1u << 19) + R.g - 1) / R.g;
-        for (uint32_t sl = 0; sl < R.rpt * R.g; sl += R.g) R.rs[sl / 64] |= 1ull << (sl % 64);
+        for (uint32_t sh = 0; sh < 4; ++sh)
+          for (uint32_t sl = 0; sl < R.rpt * R.g; sl += R.g) {  // tile slot sl sits at load offset sl + sh
+            const uint32_t o = sl + sh, k = o / 256, ln = (o % 256) / 4, cc = o % 4;
+            R.rs[sh][4 * k + cc] |= 1ull << ln;
+          }
       }
       R.qbase = dev_at(c.d_offp, a);
       R.nrel = 0;
