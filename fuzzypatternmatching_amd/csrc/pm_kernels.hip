@@ -324,7 +324,10 @@ struct K1Desc {
 // Advances the wave's range cursor r to the range holding tile t (tiles are
 // visited in increasing order by each wave) and returns the tile's description.
 __device__ __forceinline__ K1Desc k1_desc(KTab kt, uint32_t& r, uint32_t t) {
-  while (kt[r + 1].tile0 <= t) ++r;
+  // (r and t are wave-uniform: pinned to SGPRs, or the search runs on vector loads)
+  r = __builtin_amdgcn_readfirstlane(r);
+  t = __builtin_amdgcn_readfirstlane(t);
+  while (kt[r + 1].tile0 <= t) r = __builtin_amdgcn_readfirstlane(r + 1);
   K1Desc d;
   d.r = r;
   d.kind = kt[r].kind;
@@ -461,23 +464,48 @@ __device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R
   return nlist;
 }
 
-// Light tile (G = d.g slots per row, d.rpt = kTileEntries / G whole rows).
-// Phase A, per sub-tile, all in wave masks: a lane's neighbour can contribute
+// A light tile's global stores, issued at the top of the next iteration (no
+// store is issued between a tile's prefetch loads and their first use, so the
+// wait for those loads never waits for a store as well).
+struct K1Pend {
+  unsigned long long* tm;  // the tile's survivor mask words (null: nothing pending)
+  uint64_t mbase;          // first M slot of the tile
+  uint32_t ustart;         // position of the tile's first row
+  uint32_t g;              // slots per row
+  uint32_t nlist;          // staged contributors
+  uint32_t ngroups;        // 64-row groups with verified rows (0: none)
+  uint32_t any;            // some row survived
+};
+
+__device__ __forceinline__ void k1_pend_uniform(K1Pend& p) {
+  p.tm = reinterpret_cast<unsigned long long*>(uniform64(reinterpret_cast<uint64_t>(p.tm)));
+  p.mbase = uniform64(p.mbase);
+  p.ustart = __builtin_amdgcn_readfirstlane(p.ustart);
+  p.g = __builtin_amdgcn_readfirstlane(p.g);
+  p.nlist = __builtin_amdgcn_readfirstlane(p.nlist);
+  p.ngroups = __builtin_amdgcn_readfirstlane(p.ngroups);
+  p.any = __builtin_amdgcn_readfirstlane(p.any);
+}
+
+// Light tile (G = d.g slots per row, d.rpt = (kTileEntries - 4) / G whole rows).
+// Phase A, per 16-B load, all in wave masks: a lane's neighbour can contribute
 // iff its position lies in one of the range's relevant label runs (one
 // compare per run, the masks OR-ed on the scalar unit) and it is the first
-// occurrence in its row (row start, or differs from the left neighbour lane);
+// occurrence in its row (row start, or differs from its left neighbour);
 // only the contributing lanes (a few percent of the slots) are appended to
 // the LDS staging list.  Phase B: row TN / first and last list index from the
-// list (B1), one lane per row verifies (B2), survivors' entries write M[u] (B3).
+// list (B1), one lane per row verifies and leaves T_state in the row's half
+// word (B2); the stores (state, survivor mask, M) wait in LDS for k1_flush.
 template <int MODE, bool WIDE>
-__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, const K1Desc& d, KTab R,
-                                              uint16_t tu, uint16_t nm,
-                                              const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
-                                              const KeepArgs& keep, const uint16_t* s_adj, const OwnerArgs& oa,
-                                              const K1Out& o, BlockAcc& acc, unsigned long long* s_hist,
-                                              unsigned long long* tm, K1Stage& st) {
+__device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, const K1Desc& d, KTab R,
+                                                uint16_t tu, uint16_t nm, const RelRuns& rel_runs,
+                                                const uint32_t* s_runs, int nruns, const KeepArgs& keep,
+                                                const uint16_t* s_adj, const OwnerArgs& oa, BlockAcc& acc,
+                                                unsigned long long* s_hist, unsigned long long* tm, K1Stage& st) {
   const int lane = lane_id();
   const uint32_t g = d.g, rpt = d.rpt;
+  const uint32_t row0 = d.rel * rpt;
+  K1Pend p{tm, d.qbase + uint64_t(row0) * g, d.start + row0, g, 0u, 0u, 0u};
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
   if (WIDE || rel_runs.nadm > 4)
@@ -488,10 +516,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
     nlist = k1_phase_a<2, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
   else
     nlist = k1_phase_a<4, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
-  if ((MODE & 16) || nlist == 0) {  // MODE 16 (diagnostic): phase A only
-    if (lane < kSub && !(MODE & 64)) tm[lane] = 0ull;  // MODE 64: without this store
-    return;
-  }
+  if ((MODE & 16) || nlist == 0) return p;  // MODE 16 (diagnostic): phase A only
   __builtin_amdgcn_wave_barrier();
   // phase B1 over the list: a row's entries are consecutive (slot order), so
   // its first entry records the row's first list index and its last entry the
@@ -512,45 +537,88 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
   }
   __builtin_amdgcn_wave_barrier();
   if (MODE & 32) {  // diagnostic: phase A + B1 only
-    if (lane < kSub) tm[lane] = 0ull;
     for (uint32_t r = lane; r < rpt; r += 2 * kWave) st.tn[r >> 1] = 0;
-    return;
+    return p;
   }
-  // phase B2, one lane per row of the tile (consecutive positions, so the
-  // state stores coalesce): verify the rows with contributors, reset TN
-  const uint32_t row0 = d.rel * rpt;
+  // phase B2, one lane per row of the tile: verify the rows with contributors;
+  // a row's half word then holds its T_state (0: not in S)
+  uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
   uint64_t any = 0;
 #pragma unroll 1
   for (uint32_t r0 = 0; r0 < rpt; r0 += kWave) {
     const uint32_t row = r0 + lane;
-    bool surv = false;
+    uint16_t T = 0;
     if (row < rpt) {
-      const uint16_t TN = static_cast<uint16_t>(st.tn[row >> 1] >> ((row & 1u) << 4));
-      if (TN && row0 + row < d.nrows) {
-        const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
-        surv = k1_finish_row(d.start + row0 + row, tu, TN, cnt, cnt, s_adj, keep, oa, o, acc, s_hist);
+      const uint16_t TN = tn16[row];
+      if (TN) {
+        if (row0 + row < d.nrows) {
+          const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
+          T = keep_fast(tu, TN, keep, s_adj);
+          if (!T) {
+            acc.removed = 1;
+          } else if (oa.nranks <= 1) {
+            acc.vs += 1;
+            acc.es += cnt;
+          } else {
+            acc_owner(s_hist, oa, d.start + row0 + row, cnt);
+          }
+        }
+        tn16[row] = T;
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    if (row < rpt && !(row & 1u)) st.tn[row >> 1] = 0u;
-    const uint64_t b = __builtin_amdgcn_ballot_w64(surv);
+    const uint64_t b = __builtin_amdgcn_ballot_w64(T != 0);
     if (lane == 0) st.sm[r0 / kWave] = b;
     any |= b;
   }
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t ngroups = (rpt + kWave - 1) / kWave;
-  if (lane < kSub) tm[lane] = static_cast<uint32_t>(lane) < ngroups ? st.sm[lane] : 0ull;  // bit r = row r
-  if ((MODE & 1) || !any) return;
-  // phase B3: survivors' entries write M[u] in slot order at the start of u's
-  // padded row (the tile's M slots from a uniform base: 32-bit offsets)
-  char* const mtile = reinterpret_cast<char*>(o.mcol + (d.qbase + uint64_t(row0) * g));
+  p.nlist = nlist;
+  p.ngroups = (rpt + kWave - 1) / kWave;
+  p.any = any ? 1u : 0u;
+  return p;
+}
+
+// The pending stores of a light tile: survivor mask words, T_state / T_pub /
+// |M| of the survivors (consecutive positions: coalesced), M[u] of the
+// survivors in slot order at the start of u's padded row; leaves the tile's
+// TN words zero.
+template <int MODE>
+__device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stage& st) {
+  const int lane = lane_id();
+  if (!p.tm) return;
+  if (!(MODE & 64) && lane < kSub)
+    p.tm[lane] = static_cast<uint32_t>(lane) < p.ngroups ? st.sm[lane] : 0ull;  // bit r = row r
+  if (!p.any) {
+    // no survivor: the half words of verified rows are already 0
+    return;
+  }
+  uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
 #pragma unroll 1
-  for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
+  for (uint32_t gi = 0; gi < p.ngroups; ++gi) {
+    const uint64_t m = uniform64(st.sm[gi]);
+    if (!m) continue;
+    if ((m >> lane) & 1ull) {
+      const uint32_t row = gi * kWave + lane;
+      const uint16_t T = tn16[row];
+      const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
+      tn16[row] = 0;
+      if (!(MODE & 128)) {
+        // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
+        const uint32_t u = p.ustart + row, b2 = u * 2u, b4 = u * 4u;
+        *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
+        *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+      }
+    }
+  }
+  if (MODE & 129) return;  // diagnostics: without the M stores
+  char* const mtile = reinterpret_cast<char*>(o.mcol + p.mbase);  // 32-bit in-tile offsets
+#pragma unroll 1
+  for (uint32_t i0 = 0; i0 < p.nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
-    if (i < nlist) {
+    if (i < p.nlist) {
       const uint32_t row = st.lrow[i];
       if ((st.sm[row / kWave] >> (row % kWave)) & 1ull)
-        *reinterpret_cast<uint32_t*>(mtile + ((row * g + (i - st.hd[row])) << 2)) = st.lx[i] | kAlive;
+        *reinterpret_cast<uint32_t*>(mtile + ((row * p.g + (i - st.hd[row])) << 2)) = st.lx[i] | kAlive;
     }
   }
 }
@@ -651,8 +719,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   K1Desc cur{};
   if (t < ntiles) cur = k1_desc(kt, r, t);
   uint32_t sc = k1_load(vc, cur, colp, t < ntiles);
+  K1Pend pend{};  // the previous light tile's stores
   while (t < ntiles) {
+    t = __builtin_amdgcn_readfirstlane(t);
     const uint32_t tn = t + W;
+    // the previous tile's stores go out ahead of the next tile's loads
+    k1_pend_uniform(pend);
+    k1_flush<MODE>(pend, o, st);
+    pend.tm = nullptr;
     K1Desc nxt{};
     if (tn < ntiles) nxt = k1_desc(kt, r, tn);
     const uint32_t sn = k1_load(vn, nxt, colp, tn < ntiles);
@@ -669,7 +743,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         for (int q = 0; q < kSub; ++q) acc.vs += vc[q] ^ tbits_rel<WIDE>(vc[q], rel_runs, s_runs, nruns);
       } else if (!(MODE & 2)) {
         const KeepArgs keep = load_keep(R);
-        k1_light_tile<MODE, WIDE>(vc, sc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, o, acc, s_hist, tm, st);
+        pend = k1_light_tile<MODE, WIDE>(vc, sc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist,
+                                         tm, st);
       }
     }  // heavy tiles: the loop below
     t = tn;
@@ -678,6 +753,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
 #pragma unroll
     for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
   }
+  k1_pend_uniform(pend);
+  k1_flush<MODE>(pend, o, st);
   // heavy rows, one segment per wave at a time (a separate loop: no slot
   // buffers live, so the light loop's register budget is its own)
   if (!(MODE & 4))
@@ -1436,6 +1513,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 16: hipLaunchKernelGGL(k_lcc_first<16>, PM_K1_ARGS); break;
     case 32: hipLaunchKernelGGL(k_lcc_first<32>, PM_K1_ARGS); break;
     case 80: hipLaunchKernelGGL(k_lcc_first<80>, PM_K1_ARGS); break;
+    case 128: hipLaunchKernelGGL(k_lcc_first<128>, PM_K1_ARGS); break;
     default: throw std::runtime_error("unknown superstep-0 kernel variant");
   }
 #undef PM_K1_ARGS
