@@ -211,6 +211,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_nS = dalloc<uint32_t>(1);
   c->d_flags = dalloc<uint32_t>(4);
   c->d_tsm = dalloc<uint8_t>(c->n);
+  c->d_tcode = dalloc<uint32_t>((c->n + 15) / 16 + 1);
   if (c->nranks > 64) throw std::runtime_error("more than 64 ranks for result-file attribution");
   c->d_part = dalloc<uint64_t>(uint64_t(kPartGridMax) * slot_words(*c));
   size_t free_b = 0, total_b = 0;
@@ -222,6 +223,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
+  if (const char* e = std::getenv("PM_DIAG_STEP")) c->diag_step = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
   // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
   // asymmetric M then aborts the search: tests use it to find such inputs)
@@ -259,7 +261,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -366,7 +368,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       // pull form while M is known symmetric (the first call on a symmetric
       // graph: no cycle flag set yet); push form otherwise (one shard only)
       if (!c.comm && !c.force_pull && (!c.symmetric || !init_step)) launch_lcc_push(c, slot);
-      else launch_lcc_step(c, slot);
+      else launch_lcc_step(c, slot, init_step && ss == 1);
       shard_exchange_tpub(c);
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));

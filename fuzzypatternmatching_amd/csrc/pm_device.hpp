@@ -23,6 +23,11 @@ struct PopcOp {
   }
 };
 
+// u32 -> u64 scan input (64-bit accumulation of 32-bit counts)
+struct Widen {
+  __host__ __device__ uint64_t operator()(uint32_t x) const { return static_cast<uint64_t>(x); }
+};
+
 // ---------------------------------------------------------------------------
 // helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }

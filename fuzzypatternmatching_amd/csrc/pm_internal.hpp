@@ -283,7 +283,11 @@ struct Ctx {
   uint64_t* d_counts = nullptr;   // per-slot per-rank counts (vertices, edges) + traversed
   uint64_t* d_part = nullptr;     // per-block counter partials (kPartGridMax x slot_words)
   uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile
-  uint64_t* d_tbase = nullptr;    // exclusive scan of the mask popcounts
+  uint64_t* d_tbase = nullptr;    // exclusive scan of the per-tile survivor counts
+  uint32_t* d_tcode = nullptr;   // superstep-0 T_pub in 2 bits per position (k_lcc_first -> first later superstep)
+  uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
+  uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile
+  uint32_t* d_tstart = nullptr;   // position of a tile's row 0 (heavy tile: its row)
   void* d_scan_tmp = nullptr;     // hipcub scan workspace for the slist build
   size_t scan_tmp_bytes = 0;
   uint64_t tmask_words = 0;
@@ -349,7 +353,9 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0 = nullptr, hipEve
 void lcc_first_prepare(Ctx& c);  // zeroes the heavy-row scratch before a launch
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot);  // variant != 0: diagnostics
 unsigned lcc_first_grid(const Ctx& c);
-void launch_lcc_step(Ctx& c, uint64_t* d_slot);
+// first_after_ss0: the superstep right after superstep 0 of the first call
+// (T_pub is still superstep 0's output: neighbours' T_pub from the 2-bit codes)
+void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false);
 // Push form of a later superstep (send + verify launches): directed inputs and
 // LCC calls after the first (M may be asymmetric there).
 void launch_lcc_push(Ctx& c, uint64_t* d_slot);

@@ -157,7 +157,20 @@ struct K1Out {
   uint32_t* mcol;
   uint32_t* mlen;
   uint32_t* malive;
+  uint32_t* tcnt;    // per tile: survivors
+  uint32_t* tstart;  // per tile: position of row 0 (light) or the heavy row
+  uint32_t* tcode;   // T_pub in 2 bits per position (tpub_code), OR-ed in
 };
+
+// 2-bit code of a vertex's T_pub for the gathers of the next superstep: the
+// label's template bits t0 < t1 (bit 0: T has t0, bit 1: T has t1); a label
+// with more than two template vertices codes any non-empty T as 3 (gather
+// T_pub).  0 <=> T_pub = 0.
+__host__ __device__ __forceinline__ uint32_t tpub_code(uint32_t T, uint32_t tu) {
+  const uint32_t rest = tu & (tu - 1);
+  if (rest & (rest - 1)) return T ? 3u : 0u;
+  return ((T & tu & (0u - tu)) ? 1u : 0u) | ((T & rest) ? 2u : 0u);
+}
 
 // Template bits of neighbour position p that can meet the range's nm: four
 // runs held in registers (wave-uniform), the rest (rare) scanned from LDS.
@@ -248,6 +261,7 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
   *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = len;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+  atomicOr(&o.tcode[u >> 4], tpub_code(T, tu) << ((u & 15u) << 1));
   if (oa.nranks <= 1) {
     acc.vs += 1;
     acc.es += cnt;
@@ -474,7 +488,9 @@ struct K1Pend {
   uint32_t g;              // slots per row
   uint32_t nlist;          // staged contributors
   uint32_t ngroups;        // 64-row groups with verified rows (0: none)
-  uint32_t any;            // some row survived
+  uint32_t any;            // survivors of the tile
+  uint32_t tile;           // tile index
+  uint32_t tu;             // template bits of the tile's label
 };
 
 __device__ __forceinline__ void k1_pend_uniform(K1Pend& p) {
@@ -485,6 +501,8 @@ __device__ __forceinline__ void k1_pend_uniform(K1Pend& p) {
   p.nlist = __builtin_amdgcn_readfirstlane(p.nlist);
   p.ngroups = __builtin_amdgcn_readfirstlane(p.ngroups);
   p.any = __builtin_amdgcn_readfirstlane(p.any);
+  p.tile = __builtin_amdgcn_readfirstlane(p.tile);
+  p.tu = __builtin_amdgcn_readfirstlane(p.tu);
 }
 
 // Light tile (G = d.g slots per row, d.rpt = (kTileEntries - 4) / G whole rows).
@@ -501,11 +519,12 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
                                                 uint16_t tu, uint16_t nm, const RelRuns& rel_runs,
                                                 const uint32_t* s_runs, int nruns, const KeepArgs& keep,
                                                 const uint16_t* s_adj, const OwnerArgs& oa, BlockAcc& acc,
-                                                unsigned long long* s_hist, unsigned long long* tm, K1Stage& st) {
+                                                unsigned long long* s_hist, unsigned long long* tm, uint32_t tile,
+                                                K1Stage& st) {
   const int lane = lane_id();
   const uint32_t g = d.g, rpt = d.rpt;
   const uint32_t row0 = d.rel * rpt;
-  K1Pend p{tm, d.qbase + uint64_t(row0) * g, d.start + row0, g, 0u, 0u, 0u};
+  K1Pend p{tm, d.qbase + uint64_t(row0) * g, d.start + row0, g, 0u, 0u, 0u, tile, tu};
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
   if (WIDE || rel_runs.nadm > 4)
@@ -543,7 +562,7 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
   // phase B2, one lane per row of the tile: verify the rows with contributors;
   // a row's half word then holds its T_state (0: not in S)
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
-  uint64_t any = 0;
+  uint32_t any = 0;
 #pragma unroll 1
   for (uint32_t r0 = 0; r0 < rpt; r0 += kWave) {
     const uint32_t row = r0 + lane;
@@ -568,11 +587,11 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
     }
     const uint64_t b = __builtin_amdgcn_ballot_w64(T != 0);
     if (lane == 0) st.sm[r0 / kWave] = b;
-    any |= b;
+    any += static_cast<uint32_t>(__builtin_popcountll(b));
   }
   p.nlist = nlist;
   p.ngroups = (rpt + kWave - 1) / kWave;
-  p.any = any ? 1u : 0u;
+  p.any = any;
   return p;
 }
 
@@ -586,6 +605,10 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
   if (!p.tm) return;
   if (!(MODE & 64) && lane < kSub)
     p.tm[lane] = static_cast<uint32_t>(lane) < p.ngroups ? st.sm[lane] : 0ull;  // bit r = row r
+  if (lane == 0) {
+    o.tcnt[p.tile] = p.any;
+    o.tstart[p.tile] = p.ustart;
+  }
   if (!p.any) {
     // no survivor: the half words of verified rows are already 0
     return;
@@ -607,6 +630,7 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
         *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
         *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
         *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+        atomicOr(&o.tcode[u >> 4], tpub_code(T, p.tu) << ((u & 15u) << 1));
       }
     }
   }
@@ -677,6 +701,10 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
     }
   }
   if (lane < kSub && !(MODE & 8)) tm[lane] = (lane == 0 && surv) ? 1ull : 0ull;
+  if (lane == 0 && !(MODE & 8)) {
+    o.tcnt[hs.tile] = surv ? 1u : 0u;
+    o.tstart[hs.tile] = hs.row;
+  }
   return acc;
 }
 
@@ -744,7 +772,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
       } else if (!(MODE & 2)) {
         const KeepArgs keep = load_keep(R);
         pend = k1_light_tile<MODE, WIDE>(vc, sc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist,
-                                         tm, st);
+                                         tm, t, st);
       }
     }  // heavy tiles: the loop below
     t = tn;
@@ -767,35 +795,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     }
   flush_block(acc, oa, s_hist, s_red, pp);
 }
-// slist from the superstep-0 survivor masks: an exclusive scan of the mask
-// popcounts (hipcub) gives each word's base; bits decode to row positions
-// through the tiling.
-__global__ void k_slist_write(const KRange* __restrict__ ktab, uint32_t nr, const HSeg* __restrict__ hseg,
+// slist from the superstep-0 survivor masks: an exclusive scan of the
+// per-tile survivor counts (hipcub) gives each tile's base; a tile's mask bit
+// r is row r of the tile, at position tstart + r (a heavy tile: bit 0, its row).
+__global__ void k_slist_write(const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ tstart,
                               const unsigned long long* __restrict__ tmask, const uint64_t* __restrict__ base,
-                              uint64_t nwords, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
-  for (uint64_t wi = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; wi < nwords; wi += uint64_t(gridDim.x) * blockDim.x) {
-    unsigned long long m = tmask[wi];
-    uint64_t o = base[wi];
-    if (wi == nwords - 1) *nS = static_cast<uint32_t>(o + __builtin_popcountll(m));
-    if (!m) continue;
-    const uint32_t t = static_cast<uint32_t>(wi / kSub), q = static_cast<uint32_t>(wi % kSub);
-    uint32_t lo = 0, hi = nr;  // last range with tile0 <= t
-    while (lo + 1 < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (ktab[mid].tile0 <= t) lo = mid; else hi = mid;
-    }
-    const KRange R = ktab[lo];
-    const uint32_t rel = t - R.tile0;
-    while (m) {
-      const int b = __ffsll(static_cast<long long>(m)) - 1;
-      m &= m - 1;
-      uint32_t row;
-      if (R.kind < static_cast<uint32_t>(kHeavyKind)) {  // bit r of the tile = row r of the tile
-        row = R.start + rel * R.rpt + q * kWave + b;
-      } else {
-        row = hseg[R.aux + rel].row;
+                              uint32_t ntiles, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
+    uint32_t c = tcnt[t];
+    uint64_t o = base[t];
+    if (t == ntiles - 1) *nS = static_cast<uint32_t>(o + c);
+    if (!c) continue;
+    const uint32_t p0 = tstart[t];
+    const unsigned long long* w = tmask + uint64_t(t) * kSub;
+    for (uint32_t q = 0; c && q < kSub; ++q) {
+      unsigned long long m = w[q];
+      c -= static_cast<uint32_t>(__builtin_popcountll(m));
+      while (m) {
+        const int b = __ffsll(static_cast<long long>(m)) - 1;
+        m &= m - 1;
+        slist[o++] = p0 + q * kWave + static_cast<uint32_t>(b);
       }
-      slist[o++] = row;
     }
   }
 }
@@ -850,16 +870,37 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
     const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
-    uint32_t* __restrict__ malive, Partials pp) {
+    uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
   __shared__ uint64_t s_beg[kWpb][kWave];  // flattened short rows (per wave)
   __shared__ uint32_t s_end[kWpb][kWave], s_tn[kWpb][kWave], s_cnt[kWpb][kWave];
   __shared__ uint16_t s_nm[kWpb][kWave];
+  __shared__ uint32_t s_rlo[16], s_rlen[16], s_rtu[16];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   load_adj(s_adj, pa);
+  if (threadIdx.x < 16) {
+    const int l = threadIdx.x;
+    s_rlo[l] = lr.lo[l];
+    s_rlen[l] = l < lr.n ? lr.len[l] : 0u;
+    s_rtu[l] = lr.tu[l];
+  }
   __syncthreads();
+  const int nruns = lr.n;
+  // T_pub of neighbour position p: from the 2-bit codes when present (the
+  // label's template bits from its run), the T_pub array otherwise
+  auto tpub_of = [&](uint32_t p) -> uint16_t {
+    if (!tcode) return tcur[p];
+    const uint32_t code = (tcode[p >> 4] >> ((p & 15u) << 1)) & 3u;
+    if (!code) return 0;
+    uint32_t tu = 0;
+    for (int l = 0; l < nruns; ++l)
+      if (p - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
+    const uint32_t rest = tu & (tu - 1);
+    if (rest & (rest - 1)) return tcur[p];
+    return static_cast<uint16_t>(((code & 1u) ? (tu & (0u - tu)) : 0u) | ((code & 2u) ? rest : 0u));
+  };
   BlockAcc acc;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -924,7 +965,8 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
           }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
+        for (int q = 0; q < 4; ++q)
+          tv[q] = (m[q] & kAlive) ? ((diag & 1) ? uint16_t(m[q] & 0x7Fu) : tpub_of(m[q] & kPosMask)) : uint16_t(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (m[q] & kAlive) {
@@ -958,7 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
           m[q] = j < lr ? mcol[br + j] : 0u;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tcur[m[q] & kPosMask] : uint16_t(0);
+        for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tpub_of(m[q] & kPosMask) : uint16_t(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (m[q] & kAlive) k2_entry(mcol, br + j0 + q * kWave + lane, m[q], tv[q], nmr, tnr, cntr, asym);
@@ -1469,6 +1511,9 @@ void build_tiling(Ctx& c) {
   if (c.d_hscr) (void)hipFree(c.d_hscr);
   if (c.d_tmask) (void)hipFree(c.d_tmask);
   if (c.d_tbase) (void)hipFree(c.d_tbase);
+  if (c.d_tcnt) (void)hipFree(c.d_tcnt);
+  if (c.d_tstart) (void)hipFree(c.d_tstart);
+  c.d_tcnt = c.d_tstart = nullptr;
   if (c.d_scan_tmp) (void)hipFree(c.d_scan_tmp);
   c.d_ktab = nullptr;
   c.d_hseg = nullptr;
@@ -1483,13 +1528,15 @@ void build_tiling(Ctx& c) {
   c.tmask_words = std::max<uint64_t>(1, uint64_t(tiles) * kSub);
   PM_HIP_CHECK(hipMalloc(&c.d_tmask, c.tmask_words * sizeof(uint64_t)));
   PM_HIP_CHECK(hipMalloc(&c.d_tbase, c.tmask_words * sizeof(uint64_t)));
-  c.scan_tmp_bytes = slist_scan_tmp_bytes(c.tmask_words);
+  PM_HIP_CHECK(hipMalloc(&c.d_tcnt, std::max<size_t>(1, tiles) * sizeof(uint32_t)));
+  PM_HIP_CHECK(hipMalloc(&c.d_tstart, std::max<size_t>(1, tiles) * sizeof(uint32_t)));
+  c.scan_tmp_bytes = slist_scan_tmp_bytes(std::max<uint64_t>(1, tiles));
   PM_HIP_CHECK(hipMalloc(&c.d_scan_tmp, std::max<size_t>(1, c.scan_tmp_bytes)));
   c.k1_grid = lcc_first_grid(c);
 }
 
 static K1Out k1_out(Ctx& c) {
-  return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mlen, c.d_malive};
+  return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mlen, c.d_malive, c.d_tcnt, c.d_tstart, c.d_tcode};
 }
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
@@ -1547,26 +1594,25 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
   }
   const unsigned grid = c.k1_grid;
   lcc_first_prepare(c);
+  PM_HIP_CHECK(hipMemsetAsync(c.d_tcode, 0, ((c.n + 15) / 16 + 1) * sizeof(uint32_t), c.stream));
   if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
   launch_lcc_first_kernel(c, 0, grid, d_slot);
   if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
   reduce_into(c, grid, d_slot);
-  // slist = survivors in label-major row order
-  hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(
-      reinterpret_cast<const unsigned long long*>(c.d_tmask), PopcOp());
+  // slist = survivors in label-major row order (tiles are in position order)
+  hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> it(c.d_tcnt, Widen());
   size_t tmp = c.scan_tmp_bytes;
-  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_tbase, static_cast<int>(c.tmask_words),
+  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_tbase, static_cast<int>(c.ntiles),
                                                 c.stream));
   c.smask_valid = false;
-  hipLaunchKernelGGL(k_slist_write, dim3(grid_for(c.tmask_words, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_ktab,
-                     static_cast<uint32_t>(c.ktab.size() - 1), c.d_hseg,
-                     reinterpret_cast<const unsigned long long*>(c.d_tmask), c.d_tbase, c.tmask_words, c.d_slist,
+  hipLaunchKernelGGL(k_slist_write, dim3(grid_for(c.ntiles, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_tcnt,
+                     c.d_tstart, reinterpret_cast<const unsigned long long*>(c.d_tmask), c.d_tbase, c.ntiles, c.d_slist,
                      c.d_nS);
   PM_HIP_CHECK(hipGetLastError());
 }
 
 size_t slist_scan_tmp_bytes(uint64_t words) {
-  hipcub::TransformInputIterator<uint64_t, PopcOp, const unsigned long long*> it(nullptr, PopcOp());
+  hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> it(nullptr, Widen());
   size_t tmp = 0;
   PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, static_cast<uint64_t*>(nullptr),
                                                 static_cast<int>(std::max<uint64_t>(words, 1)), hipStream_t(0)));
@@ -1591,7 +1637,7 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
   c.smask_valid = false;  // the pull kernel's live masks are not maintained here
 }
 
-void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
+void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   // first later superstep (every slist entry live): one chunk per wave, the
   // latency-bound rows need waves in flight; afterwards few chunks are live
@@ -1602,7 +1648,8 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot) {
   auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
-                     c.d_malive, partials(c, d_slot));
+                     c.d_malive, partials(c, d_slot), first_after_ss0 && !c.comm ? c.d_tcode : nullptr, c.lr,
+                     c.diag_step);
   PM_HIP_CHECK(hipGetLastError());
   reduce_into(c, grid, d_slot);
   c.cur ^= 1;
