@@ -24,7 +24,12 @@
 #include <cstdio>
 #include <cstring>
 #include <dirent.h>
+#include <fcntl.h>
 #include <fstream>
+#include <memory>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <regex>
 #include <sstream>
 #include <stdexcept>
@@ -248,7 +253,61 @@ inline void transfer_graph_files(const std::string& from, const std::string& to)
   throw std::runtime_error("no backup graph files found for base " + from);
 }
 
-// Reads every <base>_<r>_of_<P> file and assembles the global CSR.
+// A graph file mapped read-only (the reference maps its per-rank segments,
+// distributed_db.hpp:191-272): header, row ids, degrees and the rows' entries
+// are read in place, with no staging copy of the file.
+class MappedGraphFile {
+ public:
+  explicit MappedGraphFile(const std::string& path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("missing graph file " + path);
+    struct stat st{};
+    if (::fstat(fd_, &st) != 0 || st.st_size < static_cast<off_t>(sizeof(GraphFileHeader))) {
+      ::close(fd_);
+      throw std::runtime_error("not a graph file: " + path);
+    }
+    size_ = static_cast<size_t>(st.st_size);
+    void* p = ::mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (p == MAP_FAILED) {
+      ::close(fd_);
+      throw std::runtime_error("cannot map graph file " + path);
+    }
+    ::madvise(p, size_, MADV_SEQUENTIAL);
+    base_ = static_cast<const char*>(p);
+    std::memcpy(&h_, base_, sizeof(h_));
+    const uint64_t need = sizeof(h_) + 16 * h_.nrows + 4 * h_.nnz;
+    if (std::memcmp(h_.magic, kGraphMagic, 8) != 0) {
+      unmap();
+      throw std::runtime_error("not a graph file: " + path);
+    }
+    if (size_ < need) {
+      unmap();
+      throw std::runtime_error("truncated graph file " + path);
+    }
+  }
+  ~MappedGraphFile() { unmap(); }
+  MappedGraphFile(const MappedGraphFile&) = delete;
+  MappedGraphFile& operator=(const MappedGraphFile&) = delete;
+  const GraphFileHeader& header() const { return h_; }
+  // unaligned-safe element reads (the sections follow a 64-B header: aligned in practice)
+  const uint64_t* rows() const { return reinterpret_cast<const uint64_t*>(base_ + sizeof(h_)); }
+  const uint64_t* degrees() const { return rows() + h_.nrows; }
+  const uint32_t* cols() const { return reinterpret_cast<const uint32_t*>(degrees() + h_.nrows); }
+
+ private:
+  void unmap() {
+    if (base_) ::munmap(const_cast<char*>(base_), size_);
+    if (fd_ >= 0) ::close(fd_);
+    base_ = nullptr;
+    fd_ = -1;
+  }
+  int fd_ = -1;
+  size_t size_ = 0;
+  const char* base_ = nullptr;
+  GraphFileHeader h_{};
+};
+
+// Reads every <base>_<r>_of_<P> file (mapped) and assembles the global CSR.
 inline Csr read_graph_files(const std::string& base, uint32_t* nranks_out = nullptr,
                             uint64_t* hub_threshold_out = nullptr) {
   uint64_t nranks = 0;
@@ -259,43 +318,42 @@ inline Csr read_graph_files(const std::string& base, uint32_t* nranks_out = null
     }
   if (nranks == 0) throw std::runtime_error("no graph files found for base " + base);
   Csr g;
-  std::vector<uint64_t> deg;
-  std::vector<std::vector<uint64_t>> rows_per_file(nranks);
-  std::vector<std::vector<uint32_t>> cols_per_file(nranks);
-  std::vector<std::vector<uint64_t>> deg_per_file(nranks);
+  std::vector<std::unique_ptr<MappedGraphFile>> files;
   uint64_t hub_threshold = 0;
   for (uint64_t r = 0; r < nranks; ++r) {
-    const std::string path = graph_file_name(base, r, nranks);
-    FILE* f = std::fopen(path.c_str(), "rb");
-    if (!f) throw std::runtime_error("missing graph file " + path);
-    GraphFileHeader h{};
-    if (std::fread(&h, sizeof(h), 1, f) != 1 || std::memcmp(h.magic, kGraphMagic, 8) != 0)
-      throw std::runtime_error("not a graph file: " + path);
+    files.emplace_back(new MappedGraphFile(graph_file_name(base, r, nranks)));
+    const GraphFileHeader& h = files.back()->header();
     if (r == 0) {
       g.n = h.n;
       g.symmetric = h.symmetric != 0;
       hub_threshold = h.hub_threshold;
-      deg.assign(g.n, 0);
+    } else if (h.n != g.n || h.nranks != nranks) {
+      throw std::runtime_error("graph file " + graph_file_name(base, r, nranks) + " belongs to another graph");
     }
-    rows_per_file[r].resize(h.nrows);
-    deg_per_file[r].resize(h.nrows);
-    cols_per_file[r].resize(h.nnz);
-    bool ok = std::fread(rows_per_file[r].data(), sizeof(uint64_t), h.nrows, f) == h.nrows;
-    ok = ok && std::fread(deg_per_file[r].data(), sizeof(uint64_t), h.nrows, f) == h.nrows;
-    ok = ok && std::fread(cols_per_file[r].data(), sizeof(uint32_t), h.nnz, f) == h.nnz;
-    std::fclose(f);
-    if (!ok) throw std::runtime_error("truncated graph file " + path);
-    for (uint64_t i = 0; i < h.nrows; ++i) deg[rows_per_file[r][i]] = deg_per_file[r][i];
+  }
+  std::vector<uint64_t> deg(g.n, 0);
+  for (const auto& f : files) {
+    const GraphFileHeader& h = f->header();
+    const uint64_t* rows = f->rows();
+    const uint64_t* d = f->degrees();
+    for (uint64_t i = 0; i < h.nrows; ++i) {
+      if (rows[i] >= g.n) throw std::runtime_error("graph file row id out of range");
+      deg[rows[i]] = d[i];
+    }
   }
   g.off.assign(g.n + 1, 0);
   for (uint64_t v = 0; v < g.n; ++v) g.off[v + 1] = g.off[v] + deg[v];
   g.col.resize(g.off[g.n]);
-  for (uint64_t r = 0; r < nranks; ++r) {
+  for (const auto& f : files) {  // each row straight from the mapping to its CSR slot
+    const GraphFileHeader& h = f->header();
+    const uint64_t* rows = f->rows();
+    const uint64_t* d = f->degrees();
+    const uint32_t* c = f->cols();
     uint64_t pos = 0;
-    for (uint64_t i = 0; i < rows_per_file[r].size(); ++i) {
-      const uint64_t v = rows_per_file[r][i], d = deg_per_file[r][i];
-      std::copy(cols_per_file[r].begin() + pos, cols_per_file[r].begin() + pos + d, g.col.begin() + g.off[v]);
-      pos += d;
+    for (uint64_t i = 0; i < h.nrows; ++i) {
+      if (pos + d[i] > h.nnz) throw std::runtime_error("truncated graph file");
+      std::memcpy(g.col.data() + g.off[rows[i]], c + pos, d[i] * sizeof(uint32_t));
+      pos += d[i];
     }
   }
   if (nranks_out) *nranks_out = static_cast<uint32_t>(nranks);

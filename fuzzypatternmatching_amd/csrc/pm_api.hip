@@ -114,6 +114,28 @@ static void set_degree_labels(Ctx& c) {
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
 }
 
+// Host pages registered with the runtime for the lifetime of the object (large
+// uploads only; a range the runtime refuses, e.g. memory that is already
+// pinned, is copied as pageable memory).
+struct PinnedRange {
+  void* base = nullptr;
+  PinnedRange(const void* p, size_t bytes) {
+    if (!p || bytes < (size_t(16) << 20)) return;
+    const size_t page = 4096;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
+    const size_t len = ((reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1)) - a;
+    if (hipHostRegister(reinterpret_cast<void*>(a), len, hipHostRegisterDefault) == hipSuccess)
+      base = reinterpret_cast<void*>(a);
+    else
+      (void)hipGetLastError();
+  }
+  ~PinnedRange() {
+    if (base) (void)hipHostUnregister(base);
+  }
+  PinnedRange(const PinnedRange&) = delete;
+  PinnedRange& operator=(const PinnedRange&) = delete;
+};
+
 static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int device) {
   std::unique_ptr<Comm> comm(in.comm);
   if (!in.off || !in.col) throw std::runtime_error("pm_create: null graph");
@@ -191,7 +213,10 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_perm = dalloc<uint32_t>(c->n);
   c->d_pos = dalloc<uint32_t>(c->n);
   c->d_labs = dalloc<uint64_t>(c->n);
-  PM_HIP_CHECK(hipMemcpy(c->d_off, off_all, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  {
+    PinnedRange pin(off_all, (c->n + 1) * sizeof(uint64_t));
+    PM_HIP_CHECK(hipMemcpy(c->d_off, off_all, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+  }
   if (in.gdeg) PM_HIP_CHECK(hipMemcpy(c->d_offl, soff, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   if (!c->hubs_host.empty()) {
     c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
@@ -230,9 +255,16 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (const char* e = std::getenv("PM_FORCE_PULL")) c->force_pull = std::string(e) == "1" && c->symmetric;
   // default labels = degree labels; the id-major adjacency is staged in the
   // M column buffer and permuted into the label-major d_colp
-  if (c->nnz)
-    PM_HIP_CHECK(hipMemcpy(c->d_mcol, scol, c->nnz * sizeof(uint32_t),
-                           in.col_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+  if (c->nnz) {
+    if (in.col_on_device) {
+      PM_HIP_CHECK(hipMemcpy(c->d_mcol, scol, c->nnz * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+    } else {
+      // pinned staging: the caller's pages are registered for the copy, so the
+      // adjacency moves by DMA without a bounce through driver staging buffers
+      PinnedRange pin(scol, c->nnz * sizeof(uint32_t));
+      PM_HIP_CHECK(hipMemcpy(c->d_mcol, scol, c->nnz * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+  }
   set_degree_labels(*c);
   const auto t_lay = std::chrono::steady_clock::now();
   build_label_layout(*c, c->d_mcol, false, c->d_colp);
