@@ -160,6 +160,16 @@ __host__ __device__ inline uint32_t kind_slots(uint32_t k) {
   return 160 + 32 * (k - 36);
 }
 
+// 2-bit code of a vertex's T_pub for the gathers of the next superstep: the
+// label's template bits t0 < t1 (bit 0: T has t0, bit 1: T has t1); a label
+// with more than two template vertices codes any non-empty T as 3 (gather
+// T_pub).  0 <=> T_pub = 0.
+__host__ __device__ inline uint32_t tpub_code(uint32_t T, uint32_t tu) {
+  const uint32_t rest = tu & (tu - 1);
+  if (rest & (rest - 1)) return T ? 3u : 0u;
+  return ((T & tu & (0u - tu)) ? 1u : 0u) | ((T & rest) ? 2u : 0u);
+}
+
 // Padded row length: the class length up to kLightMax, the degree above.
 __host__ __device__ inline uint64_t padded_degree(uint64_t d) {
   if (d == 0 || d > kLightMax) return d;

@@ -162,15 +162,6 @@ struct K1Out {
   uint32_t* tcode;   // T_pub in 2 bits per position (tpub_code), OR-ed in
 };
 
-// 2-bit code of a vertex's T_pub for the gathers of the next superstep: the
-// label's template bits t0 < t1 (bit 0: T has t0, bit 1: T has t1); a label
-// with more than two template vertices codes any non-empty T as 3 (gather
-// T_pub).  0 <=> T_pub = 0.
-__host__ __device__ __forceinline__ uint32_t tpub_code(uint32_t T, uint32_t tu) {
-  const uint32_t rest = tu & (tu - 1);
-  if (rest & (rest - 1)) return T ? 3u : 0u;
-  return ((T & tu & (0u - tu)) ? 1u : 0u) | ((T & rest) ? 2u : 0u);
-}
 
 // Template bits of neighbour position p that can meet the range's nm: four
 // runs held in registers (wave-uniform), the rest (rare) scanned from LDS.
@@ -910,16 +901,21 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
   auto chunk_body = [&](uint64_t chunk, uint64_t live) {
     const uint64_t i = chunk * kWave + lane;
     uint32_t u = kNone;
-    uint16_t Tu = 0, nm = 0;
+    uint16_t Tu = 0, nm = 0, Ts = 0;
     uint64_t beg = 0;
     uint32_t len = 0, alive0 = 0;
     if (i < nS && ((live >> lane) & 1ull)) {
       u = slist[i];
+      // the row's state is loaded with T_pub in one round trip (a removed
+      // row, T_pub = 0, ignores it)
       Tu = tcur[u];
+      const uint64_t b = offp[u];
+      const uint32_t l = mlen[u], a0 = malive[u];
+      Ts = tst[u];
       if (Tu) {
-        beg = offp[u];
-        len = mlen[u];
-        alive0 = malive[u];
+        beg = b;
+        len = l;
+        alive0 = a0;
         nm = nbr_mask(Tu, s_adj);
       } else {
         tnxt[u] = 0;
@@ -1014,7 +1010,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     }
     bool survivor = false, removed = false;
     if (Tu) {
-      const uint16_t T = keep_bits(tst[u], static_cast<uint16_t>(tn), s_adj);
+      const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
         survivor = true;
         tst[u] = T;
