@@ -100,6 +100,25 @@ def rmat_graph(scale, p_gen=1, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD, de
     return Graph(off, col, True, nranks, hub_threshold)
 
 
+def _file_array(files):
+    files = [os.fspath(f).encode() for f in files]
+    arr = (ctypes.c_char_p * max(len(files), 1))(*files)
+    return arr, len(files)
+
+
+def ingest_edge_list_gpu(files, undirected=False, device=0, nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """ingest_edge_list's text parse and graph construction on the GPU (pm_ingest.hip):
+    "src dst [weight]" lines, undirected=True adds (dst, src).  Returns a host Graph."""
+    lib = _lib()
+    arr, nf = _file_array(files)
+    off_p, col_p, n, sym = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int()
+    if lib.pm_ingest_edge_list_gpu(arr, nf, int(bool(undirected)), device, ctypes.byref(off_p), ctypes.byref(col_p),
+                                   ctypes.byref(n), ctypes.byref(sym)) != 0:
+        raise _err()
+    off, col = _take_host_csr(off_p, col_p, n.value)
+    return Graph(off, col, bool(sym.value), nranks, hub_threshold)
+
+
 def mt19937_jump_outputs(seed, skip, count):
     """Outputs skip .. skip+count-1 of std::mt19937(seed) by one GF(2) jump (host check)."""
     out = np.zeros(max(count, 1), np.uint32)
@@ -251,6 +270,10 @@ class PatternMatcher:
             raise ValueError("labels must have one entry per vertex id")
         self._check(_lib().pm_vertex_data_set(self._ctx, lab.ctypes.data))
 
+    def labels_from_files(self, prefix):
+        """-v <prefix>: label files parsed on the device (pm_vertex_data_files)."""
+        self._check(_lib().pm_vertex_data_files(self._ctx, os.fspath(prefix).encode()))
+
     def degree_labels(self):
         self._check(_lib().pm_vertex_data_degree(self._ctx))
 
@@ -323,6 +346,25 @@ def rmat_matcher(scale, p_gen, pattern_dir, device=0, nranks=1, hub_threshold=DE
     m = PatternMatcher.__new__(PatternMatcher)
     m._ctx = ctx
     m.graph = _DeviceGraph(1 << scale, (1 << scale) * 32, nranks, hub_threshold)
+    return m, secs.value
+
+
+def edge_list_matcher(files, pattern_dir, undirected=False, device=0, nranks=1,
+                      hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """PatternMatcher over text edge-list files ingested on the device (the adjacency never
+    visits the host).  Returns (matcher, ingest seconds)."""
+    arr, nf = _file_array(files)
+    secs = ctypes.c_double()
+    ctx = _lib().pm_create_edge_list(arr, nf, int(bool(undirected)), os.fspath(pattern_dir).encode(), device, nranks,
+                                     hub_threshold, ctypes.byref(secs))
+    if not ctx:
+        raise _err()
+    n, nnz, sym = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    _lib().pm_graph_size(ctx, ctypes.byref(n), ctypes.byref(nnz), ctypes.byref(sym))
+    m = PatternMatcher.__new__(PatternMatcher)
+    m._ctx = ctx
+    m.graph = _DeviceGraph(n.value, nnz.value, nranks, hub_threshold)
+    m.graph.symmetric = bool(sym.value)
     return m, secs.value
 
 

@@ -122,6 +122,13 @@ SIGNATURES = [
                                        ctypes.POINTER(c_u64)]),
     ("pm_create_rmat", c_vp, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u64, ctypes.POINTER(ctypes.c_double)]),
     ("pm_mt19937_jump_outputs", ctypes.c_int, [c_u32, c_u64, c_vp, c_u64]),
+    ("pm_vertex_data_files", ctypes.c_int, [c_vp, c_char_p]),
+    ("pm_graph_size", ctypes.c_int, [c_vp, ctypes.POINTER(c_u64), ctypes.POINTER(c_u64), ctypes.POINTER(ctypes.c_int)]),
+    ("pm_ingest_edge_list_gpu", ctypes.c_int, [c_vp, c_u32, ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_vp),
+                                               ctypes.POINTER(c_vp), ctypes.POINTER(c_u64),
+                                               ctypes.POINTER(ctypes.c_int)]),
+    ("pm_create_edge_list", c_vp, [c_vp, c_u32, ctypes.c_int, c_char_p, ctypes.c_int, c_u32, c_u64,
+                                   ctypes.POINTER(ctypes.c_double)]),
 ]
 
 _lib = None

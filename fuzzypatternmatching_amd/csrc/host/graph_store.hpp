@@ -379,7 +379,7 @@ inline uint64_t degree_label(uint64_t degree) {
 // vertices not listed keep 0.  A line that fails to parse yields the entry
 // (0, 0), exactly like the reference's `iss >> v >> d` on zero-initialised
 // values (vertex_data_db.hpp:176-185).  Files are applied in sorted name order.
-inline std::vector<uint64_t> load_vertex_labels(const std::string& prefix, uint64_t n) {
+inline std::vector<std::string> vertex_label_files(const std::string& prefix) {
   std::string dir = ".", wildcard = prefix;
   const size_t slash = prefix.find_last_of('/');
   if (slash != std::string::npos) {
@@ -403,6 +403,13 @@ inline std::vector<uint64_t> load_vertex_labels(const std::string& prefix, uint6
   }
   if (files.empty()) throw std::runtime_error("no vertex label files match " + prefix);
   std::sort(files.begin(), files.end());
+  return files;
+}
+
+// Host loader (tests and host-only tools; the product CLI parses on the GPU,
+// pm_vertex_data_files / pm_ingest.hip).
+inline std::vector<uint64_t> load_vertex_labels(const std::string& prefix, uint64_t n) {
+  const std::vector<std::string> files = vertex_label_files(prefix);
   std::vector<uint64_t> labels(n, 0);
   for (const auto& path : files) {
     std::ifstream f(path);

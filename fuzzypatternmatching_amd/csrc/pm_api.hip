@@ -27,6 +27,7 @@
 #include "host/graph_store.hpp"
 #include "host/mt_jump.hpp"
 #include "pm_internal.hpp"
+#include "pm_ingest.hpp"
 #include "pm_rmat.hpp"
 #include "pm_shard.hpp"
 #include <thread>
@@ -82,6 +83,8 @@ struct CtxInput {
   Comm* comm = nullptr;            // ownership passes to the context
   bool col_on_device = false;      // col is device memory (GPU-built graph); off stays host
   uint32_t inprocess_shards = 1;   // shards of this process on the same device (ThreadComm groups)
+  const uint64_t* in_off = nullptr;  // directed graphs: in-rows built by the caller (host offsets,
+  const uint32_t* in_col = nullptr;  // columns where col lives), e.g. by the GPU ingest
 };
 
 // In-rows of a directed CSR (rows sorted by source id, duplicates adjacent):
@@ -163,10 +166,15 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   const uint32_t* scol = in.col;
   if (!c->symmetric) {
     if (in.nshards > 1) throw std::runtime_error("directed input graphs are supported on one shard only");
-    if (in.col_on_device) throw std::runtime_error("directed input graphs must be host resident");
-    transpose_csr(c->n, in.off, in.col, tin_off, tin_col);
-    soff = tin_off.data();
-    scol = tin_col.data();
+    if (in.in_off && in.in_col) {
+      soff = in.in_off;
+      scol = in.in_col;
+    } else {
+      if (in.col_on_device) throw std::runtime_error("directed device-resident graphs need their in-rows");
+      transpose_csr(c->n, in.off, in.col, tin_off, tin_col);
+      soff = tin_off.data();
+      scol = tin_col.data();
+    }
     c->rdeg_host.resize(c->n);
     for (uint64_t v = 0; v < c->n; ++v) c->rdeg_host[v] = static_cast<uint32_t>(soff[v + 1] - soff[v]);
   }
@@ -925,6 +933,19 @@ int pm_vertex_data_set(pm_ctx* ctx, const uint64_t* labels) {
   });
 }
 
+int pm_vertex_data_files(pm_ctx* ctx, const char* prefix) {
+  PM_API_BODY(ctx, {
+    if (!prefix) throw std::runtime_error("null label prefix");
+    const std::vector<std::string> files = pm::vertex_label_files(prefix);
+    pm::labels_from_files_device(files, ctx->n, ctx->d_labels, ctx->stream);
+    ctx->labels_host.resize(ctx->n);
+    PM_HIP_CHECK(hipMemcpyAsync(ctx->labels_host.data(), ctx->d_labels, ctx->n * sizeof(uint64_t),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    pm::relayout(*ctx);
+  });
+}
+
 int pm_reset(pm_ctx* ctx) {
   PM_API_BODY(ctx, {
     pm::reset_state(*ctx);
@@ -1261,6 +1282,114 @@ pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, 
     pm::g_last_error = e.what();
     return nullptr;
   }
+}
+
+static std::vector<std::string> file_list(const char* const* files, uint32_t nfiles) {
+  if (nfiles && !files) throw std::runtime_error("null file list");
+  std::vector<std::string> v;
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    if (!files[i]) throw std::runtime_error("null file name");
+    v.emplace_back(files[i]);
+  }
+  return v;
+}
+
+static void free_dev_csr(pm::DevCsr& g) {
+  if (g.d_off) (void)hipFree(g.d_off);
+  if (g.d_col) (void)hipFree(g.d_col);
+  g.d_off = nullptr;
+  g.d_col = nullptr;
+}
+
+// GPU text ingest (pm_ingest.hip): the CSR ingest_edge_list builds, returned to the host.
+int pm_ingest_edge_list_gpu(const char* const* files, uint32_t nfiles, int undirected, int device, uint64_t** off,
+                            uint32_t** col, uint64_t* n, int* symmetric) {
+  hipStream_t s = nullptr;
+  pm::IngestCsr g;
+  try {
+    if (!off || !col || !n) throw std::runtime_error("null output");
+    const std::vector<std::string> fl = file_list(files, nfiles);
+    pm::require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g = pm::ingest_edges_device(fl, undirected != 0, false, s);
+    uint64_t* o = static_cast<uint64_t*>(std::malloc((g.fwd.n + 1) * sizeof(uint64_t)));
+    uint32_t* c = static_cast<uint32_t*>(std::malloc(std::max<uint64_t>(1, g.fwd.nnz) * sizeof(uint32_t)));
+    if (!o || !c) {
+      std::free(o);
+      std::free(c);
+      throw std::runtime_error("pm_ingest_edge_list_gpu: out of host memory");
+    }
+    PM_HIP_CHECK(hipMemcpy(o, g.fwd.d_off, (g.fwd.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (g.fwd.nnz) PM_HIP_CHECK(hipMemcpy(c, g.fwd.d_col, g.fwd.nnz * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *off = o;
+    *col = c;
+    *n = g.fwd.n;
+    if (symmetric) *symmetric = g.symmetric ? 1 : 0;
+    free_dev_csr(g.fwd);
+    free_dev_csr(g.rev);
+    (void)hipStreamDestroy(s);
+    return 0;
+  } catch (const std::exception& e) {
+    free_dev_csr(g.fwd);
+    free_dev_csr(g.rev);
+    if (s) (void)hipStreamDestroy(s);
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+// Context over a graph ingested from text on the device (the adjacency never
+// leaves HBM; a directed graph's in-rows come from the same sort).
+pm_ctx* pm_create_edge_list(const char* const* files, uint32_t nfiles, int undirected, const char* pattern_dir,
+                            int device, uint32_t nranks, uint64_t hub_threshold, double* ingest_seconds) {
+  hipStream_t s = nullptr;
+  pm::IngestCsr g;
+  try {
+    const std::vector<std::string> fl = file_list(files, nfiles);
+    pm::require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const auto t0 = std::chrono::steady_clock::now();
+    g = pm::ingest_edges_device(fl, undirected != 0, true, s);
+    if (ingest_seconds)
+      *ingest_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<uint64_t> off(g.fwd.n + 1), roff;
+    PM_HIP_CHECK(hipMemcpy(off.data(), g.fwd.d_off, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    pm::CtxInput in;
+    in.n = g.fwd.n;
+    in.off = off.data();
+    in.col = g.fwd.d_col;
+    in.col_on_device = true;
+    in.symmetric = g.symmetric;
+    in.nranks = nranks;
+    in.hub_threshold = hub_threshold;
+    if (!g.symmetric) {
+      roff.resize(g.rev.n + 1);
+      PM_HIP_CHECK(hipMemcpy(roff.data(), g.rev.d_off, roff.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      in.in_off = roff.data();
+      in.in_col = g.rev.d_col;
+    }
+    pm_ctx* c = pm::create_ctx(in, pattern_dir, device);
+    free_dev_csr(g.fwd);
+    free_dev_csr(g.rev);
+    (void)hipStreamDestroy(s);
+    return c;
+  } catch (const std::exception& e) {
+    free_dev_csr(g.fwd);
+    free_dev_csr(g.rev);
+    if (s) (void)hipStreamDestroy(s);
+    pm::g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+int pm_graph_size(const pm_ctx* ctx, uint64_t* n, uint64_t* nnz, int* symmetric) {
+  if (!ctx) return -1;
+  if (n) *n = ctx->n;
+  if (nnz) *nnz = ctx->nnz;
+  if (symmetric) *symmetric = ctx->symmetric ? 1 : 0;
+  return 0;
 }
 
 // Host check of the MT19937 jump-ahead machinery (host/mt_jump.hpp): the

@@ -102,8 +102,13 @@ int main(int argc, char** argv) {
       return 1;
     }
     if (!vertex_metadata.empty()) {
-      std::vector<uint64_t> labels = pm::load_vertex_labels(vertex_metadata, n);
-      if (pm_vertex_data_set(ctx, labels.data()) != 0) throw std::runtime_error(pm_last_error(ctx));
+      // parsed on the GPU (pm_ingest.hip); PM_HOST_LABELS=1 takes the host loader instead
+      if (std::getenv("PM_HOST_LABELS")) {
+        std::vector<uint64_t> labels = pm::load_vertex_labels(vertex_metadata, n);
+        if (pm_vertex_data_set(ctx, labels.data()) != 0) throw std::runtime_error(pm_last_error(ctx));
+      } else if (pm_vertex_data_files(ctx, vertex_metadata.c_str()) != 0) {
+        throw std::runtime_error(pm_last_error(ctx));
+      }
     }
     const char* mi = std::getenv("PM_MAX_ITERATIONS");
     pm_run_stats st{};

@@ -38,6 +38,13 @@
  *                                 built on the GPU: MT19937 jump-ahead substreams + radix-sorted CSR
  *   pm_create_rmat                generate_rmat + graph open (beta.cpp:209-223) in one step with the
  *                                 adjacency never leaving HBM (north_star scale-28 configuration)
+ *   pm_ingest_edge_list_gpu       ingest_edge_list's text parse + graph construction
+ *                                 (src/ingest_edge_list.cpp:164-240, parallel_edge_list_reader.hpp:242-266,
+ *                                 delegate_partitioned_graph ctor ipp:70-167) parsed and sorted on the GPU
+ *   pm_create_edge_list           ingest_edge_list + graph open (beta.cpp:209-223) with the adjacency
+ *                                 never leaving HBM (config C5)
+ *   pm_vertex_data_files          vertex_data_db(graph, labels, prefix, 10000) (-v) parsed on the GPU:
+ *                                 include/havoqgt/vertex_data_db.hpp:137-257
  *
  * Conventions: plain C types; int status (0 = OK, negative = error with
  * pm_last_error()); device memory is owned by the context; host buffers are
@@ -121,6 +128,10 @@ const char* pm_last_error(const pm_ctx* ctx);
 int pm_vertex_data_degree(pm_ctx* ctx);
 int pm_vertex_data_set(pm_ctx* ctx, const uint64_t* labels /* n entries, host */);
 
+/* -v <prefix>: every file basename(prefix).* in dirname(prefix), in name order, lines "vid label"
+ * parsed on the device (last line wins, unlisted vertices keep 0; vertex_data_db.hpp:176-257). */
+int pm_vertex_data_files(pm_ctx* ctx, const char* prefix);
+
 /* Per-pattern reset: every vertex active, empty state map (beta.cpp:484-492). */
 int pm_reset(pm_ctx* ctx);
 
@@ -178,6 +189,17 @@ int pm_rmat_csr_gpu(uint64_t scale, uint64_t p_gen, int device, uint64_t** off, 
  * gen_seconds (may be NULL) receives the generation + CSR build wall time. */
 pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nranks,
                        uint64_t hub_threshold, double* gen_seconds);
+/* GPU text ingest: files of "src dst [weight]" lines (lines that do not start with two numbers are
+ * skipped; ids above 2^32 - 2 are an error), undirected != 0 adds (dst, src) for every edge.  Returns
+ * the row-sorted CSR with multiplicity (malloc'ed, pm_free_host) and whether it is symmetric. */
+int pm_ingest_edge_list_gpu(const char* const* files, uint32_t nfiles, int undirected, int device, uint64_t** off,
+                            uint32_t** col, uint64_t* n, int* symmetric);
+/* Context over a GPU-ingested text graph (degree labels; no host copy of the adjacency).
+ * ingest_seconds (may be NULL) receives the parse + CSR build wall time. */
+pm_ctx* pm_create_edge_list(const char* const* files, uint32_t nfiles, int undirected, const char* pattern_dir,
+                            int device, uint32_t nranks, uint64_t hub_threshold, double* ingest_seconds);
+/* Size of the graph a context holds (vertex ids, directed entries, symmetric flag); any pointer may be NULL. */
+int pm_graph_size(const pm_ctx* ctx, uint64_t* n, uint64_t* nnz, int* symmetric);
 /* Host check of the MT19937 jump-ahead (no device): outputs skip .. skip+count-1 of mt19937(seed). */
 int pm_mt19937_jump_outputs(uint32_t seed, uint64_t skip, uint32_t* out, uint64_t count);
 int pm_write_graph(const char* base, uint64_t n, const uint64_t* off, const uint32_t* col, int symmetric,
