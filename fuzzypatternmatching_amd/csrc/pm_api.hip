@@ -217,7 +217,11 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_offp = dalloc<uint64_t>(c->n + 1);
   c->d_offr = dalloc<uint64_t>(c->n + 1);
   // slot buffers carry kTileEntries entries of tail padding (superstep-0 tile loads read whole tiles)
-  c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries);
+  // dense superstep-0 M region behind the tail padding (both buffers: relayout swaps them)
+  if (in.nshards == 1 && c->symmetric && c->nq)
+    c->dcap = std::min<uint64_t>(0xFFFFFFF0ull, std::max<uint64_t>(uint64_t(1) << 16, c->nq / 8));
+  c->dbase = c->nq + kTileEntries;
+  c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap);
   c->d_perm = dalloc<uint32_t>(c->n);
   c->d_pos = dalloc<uint32_t>(c->n);
   c->d_labs = dalloc<uint64_t>(c->n);
@@ -234,7 +238,11 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_tpub[0] = dalloc<uint16_t>(c->n);
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
-  c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries);
+  c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap);
+  if (c->dcap) {
+    c->d_dmoff = dalloc<uint32_t>(c->n);
+    c->d_dctr = dalloc<unsigned long long>(1);
+  }
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
   c->d_slist = dalloc<uint32_t>(c->n);
@@ -301,7 +309,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_dctr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1466,9 +1474,14 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     const int mode = variant >= 256 ? 0 : variant;
     pm::ensure_counts(*ctx, 1);
     pm::lcc_first_prepare(*ctx);
+    // the product launch writes dense M when the search would (counter reset per launch)
+    if (mode == 0) pm::lcc_first_set_dense(*ctx);
     pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
     PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
-    for (int i = 0; i < reps; ++i) pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);
+    for (int i = 0; i < reps; ++i) {
+      if (mode == 0) pm::lcc_first_set_dense(*ctx);
+      pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);
+    }
     PM_HIP_CHECK(hipEventRecord(b, ctx->stream));
     PM_HIP_CHECK(hipEventSynchronize(b));
     float ms = 0.f;
@@ -1476,6 +1489,7 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     if (ms_out) *ms_out = ms / std::max(1, reps);
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
+    ctx->k1_dense = false;
     ctx->tpub_clean = false;  // the timed launches wrote T_pub outside any search
     pm::reset_state(*ctx);
   });

@@ -295,6 +295,15 @@ struct Ctx {
   uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile
   uint64_t* d_tbase = nullptr;    // exclusive scan of the per-tile survivor counts
   uint32_t* d_tcode = nullptr;   // superstep-0 T_pub in 2 bits per position (k_lcc_first -> first later superstep)
+  // dense superstep-0 M (one shard, symmetric graph, diameter >= 2): light tiles
+  // append their contributors to the region [dbase, dbase + dcap) of d_mcol and
+  // d_dmoff[u] gives survivor u's first entry there (kNone: M in u's padded
+  // row); the first later superstep reads M densely and writes the rows of its
+  // survivors into their padded rows
+  uint64_t dbase = 0, dcap = 0;
+  uint32_t* d_dmoff = nullptr;
+  unsigned long long* d_dctr = nullptr;
+  bool k1_dense = false;         // the last superstep-0 launch wrote dense M
   uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile
   uint32_t* d_tstart = nullptr;   // position of a tile's row 0 (heavy tile: its row)
@@ -361,6 +370,7 @@ uint32_t slot_words(const Ctx& c);
 // ev0/ev1 (may be null) bracket the kernel launch alone (roofline timing)
 void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 void lcc_first_prepare(Ctx& c);  // zeroes the heavy-row scratch before a launch
+void lcc_first_set_dense(Ctx& c);  // dense superstep-0 M for this launch (sets k1_dense)
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot);  // variant != 0: diagnostics
 unsigned lcc_first_grid(const Ctx& c);
 // first_after_ss0: the superstep right after superstep 0 of the first call

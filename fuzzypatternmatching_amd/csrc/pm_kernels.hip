@@ -160,6 +160,9 @@ struct K1Out {
   uint32_t* tcnt;    // per tile: survivors
   uint32_t* tstart;  // per tile: position of row 0 (light) or the heavy row
   uint32_t* tcode;   // T_pub in 2 bits per position (tpub_code), OR-ed in
+  uint32_t* dmoff;   // dense M: survivor's first entry in mcol[dbase..] (null: M in padded rows)
+  unsigned long long* dctr;  // dense M: entries appended so far
+  uint64_t dbase, dcap;
 };
 
 
@@ -253,6 +256,7 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = len;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
   atomicOr(&o.tcode[u >> 4], tpub_code(T, tu) << ((u & 15u) << 1));
+  if (o.dmoff) o.dmoff[u] = kNone;  // a heavy row's M stays in its padded row
   if (oa.nranks <= 1) {
     acc.vs += 1;
     acc.es += cnt;
@@ -604,6 +608,17 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
     // no survivor: the half words of verified rows are already 0
     return;
   }
+  // dense M: the tile's whole contributor list goes to one appended block
+  // (coalesced), survivor u's M starts at list index hd[row] of it; a tile that
+  // no longer fits the region keeps the padded-row layout
+  uint64_t dpos = 0;
+  bool dense = false;
+  if (o.dmoff) {
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(o.dctr, static_cast<unsigned long long>(p.nlist));
+    dpos = uniform64(b);
+    dense = dpos + p.nlist <= o.dcap;
+  }
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
 #pragma unroll 1
   for (uint32_t gi = 0; gi < p.ngroups; ++gi) {
@@ -622,10 +637,19 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
         *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
         *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
         atomicOr(&o.tcode[u >> 4], tpub_code(T, p.tu) << ((u & 15u) << 1));
+        if (o.dmoff)
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.dmoff) + b4) =
+              dense ? static_cast<uint32_t>(dpos + st.hd[row]) : kNone;
       }
     }
   }
   if (MODE & 129) return;  // diagnostics: without the M stores
+  if (dense) {
+    uint32_t* const dm = o.mcol + o.dbase + dpos;
+#pragma unroll 1
+    for (uint32_t i = lane; i < p.nlist; i += kWave) dm[i] = st.lx[i] | kAlive;
+    return;
+  }
   char* const mtile = reinterpret_cast<char*>(o.mcol + p.mbase);  // 32-bit in-tile offsets
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < p.nlist; i0 += kWave) {
@@ -860,8 +884,9 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
     const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
-    OwnerArgs oa, uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
-    uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag) {
+    OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
+    uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
+    const uint32_t* __restrict__ dmoff, uint64_t dbase) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -902,8 +927,9 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t i = chunk * kWave + lane;
     uint32_t u = kNone;
     uint16_t Tu = 0, nm = 0, Ts = 0;
-    uint64_t beg = 0;
+    uint64_t beg = 0, pb = 0;
     uint32_t len = 0, alive0 = 0;
+    bool drow = false;  // M read from the dense superstep-0 region
     if (i < nS && ((live >> lane) & 1ull)) {
       u = slist[i];
       // the row's state is loaded with T_pub in one round trip (a removed
@@ -911,9 +937,12 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
       Tu = tcur[u];
       const uint64_t b = offp[u];
       const uint32_t l = mlen[u], a0 = malive[u];
+      const uint32_t dm = dmoff ? dmoff[u] : kNone;
       Ts = tst[u];
       if (Tu) {
-        beg = b;
+        drow = dm != kNone;
+        pb = b;
+        beg = drow ? dbase + dm : b;
         len = l;
         alive0 = a0;
         nm = nbr_mask(Tu, s_adj);
@@ -1009,6 +1038,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
       }
     }
     bool survivor = false, removed = false;
+    if (dmoff) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
     if (Tu) {
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
@@ -1016,11 +1046,15 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         tst[u] = T;
         tnxt[u] = T;
         malive[u] = cnt;
+        // dense M: the survivor's (updated) row moves to its padded row
+        if (drow)
+          for (uint32_t j = 0; j < len; ++j) mcol[pb + j] = mcol[beg + j];
       } else {
         removed = true;
         tnxt[u] = 0;
         malive[u] = 0;
         cnt = 0;
+        if (drow) mlen[u] = 0;  // M[v] cleared (nonunique_ee.hpp:941-964); its padded row was never written
       }
     }
     // live mask of the next superstep (S only shrinks); a vertex removed now
@@ -1532,7 +1566,8 @@ void build_tiling(Ctx& c) {
 }
 
 static K1Out k1_out(Ctx& c) {
-  return K1Out{c.d_tst, c.d_tpub[c.cur], c.d_mcol, c.d_mlen, c.d_malive, c.d_tcnt, c.d_tstart, c.d_tcode};
+  return K1Out{c.d_tst,   c.d_tpub[c.cur], c.d_mcol,  c.d_mlen, c.d_malive, c.d_tcnt,
+               c.d_tstart, c.d_tcode,      c.k1_dense ? c.d_dmoff : nullptr, c.d_dctr, c.dbase, c.dcap};
 }
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
@@ -1575,6 +1610,14 @@ unsigned lcc_first_grid(const Ctx& c) {
   return grid_for(c.ntiles, kWpb, static_cast<unsigned>(cap));
 }
 
+// Dense M when the next superstep is the pull-form k_lcc_step of this call
+// (first call on one shard of a symmetric graph, diameter >= 2); PM_DENSE_M=0 disables it.
+void lcc_first_set_dense(Ctx& c) {
+  static const bool dense_env = !std::getenv("PM_DENSE_M") || std::string(std::getenv("PM_DENSE_M")) != "0";
+  c.k1_dense = dense_env && c.dcap && !c.comm && c.symmetric && c.pattern.graph.diameter >= 2;
+  if (c.k1_dense) PM_HIP_CHECK(hipMemsetAsync(c.d_dctr, 0, sizeof(unsigned long long), c.stream));
+}
+
 void lcc_first_prepare(Ctx& c) {
   if (c.nheavy) PM_HIP_CHECK(hipMemsetAsync(c.d_hscr, 0, 3 * size_t(c.nheavy) * sizeof(uint32_t), c.stream));
 }
@@ -1591,6 +1634,7 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
   const unsigned grid = c.k1_grid;
   lcc_first_prepare(c);
   PM_HIP_CHECK(hipMemsetAsync(c.d_tcode, 0, ((c.n + 15) / 16 + 1) * sizeof(uint32_t), c.stream));
+  lcc_first_set_dense(c);
   if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
   launch_lcc_first_kernel(c, 0, grid, d_slot);
   if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
@@ -1645,8 +1689,9 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 && !c.comm ? c.d_tcode : nullptr, c.lr,
-                     c.diag_step);
+                     c.diag_step, first_after_ss0 && c.k1_dense ? c.d_dmoff : nullptr, c.dbase);
   PM_HIP_CHECK(hipGetLastError());
+  c.k1_dense = false;  // every M row of S is in its padded row from here on
   reduce_into(c, grid, d_slot);
   c.cur ^= 1;
   c.smask_cur ^= 1;
