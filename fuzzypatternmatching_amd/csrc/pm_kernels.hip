@@ -22,7 +22,10 @@
 // through "strips" over M.  Irregular integer work: no MFMA (north_star).
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <stdexcept>
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   flush_block(acc, oa, s_hist, s_red, pp);
 }
 // slist from the superstep-0 survivor masks: an exclusive scan of the
-// per-tile survivor counts (hipcub) gives each tile's base; a tile's mask bit
+// per-tile survivor counts (rocPRIM) gives each tile's base; a tile's mask bit
 // r is row r of the tile, at position tstart + r (a heavy tile: bit 0, its row).
 __global__ void k_slist_write(const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ tstart,
                               const unsigned long long* __restrict__ tmask, const uint64_t* __restrict__ base,
@@ -1318,26 +1321,26 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
     auto* lkey = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_layout_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, n, dkey, ids);
     size_t tmp = 0, tmp2 = 0;
-    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 32,
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 32,
                                                     c.stream));
-    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, lkey, c.d_labs, ids2, c.d_perm, static_cast<int>(n),
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp2, lkey, c.d_labs, ids2, c.d_perm, size_t(n),
                                                     0, 64, c.stream));
     tmp = std::max(tmp, tmp2);
     void* d_tmp = c.arena.get(tmp);
-    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 32,
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 32,
                                                     c.stream));
     if (c.nshards > 1) {
       int obits = 1;
       while ((1u << obits) < c.nshards) ++obits;
       hipLaunchKernelGGL(k_owner_keys, dim3(g), dim3(kBlock), 0, c.stream, ids2, n, c.nshards, dkey);
-      PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids2, ids, static_cast<int>(n), 0,
+      PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids2, ids, size_t(n), 0,
                                                       obits, c.stream));
       hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, ids, n, dkey);
-      PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, dkey, dkey2, ids, ids2, static_cast<int>(n), 0, 6,
+      PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 6,
                                                       c.stream));
     }
     hipLaunchKernelGGL(k_gather_labels, dim3(g), dim3(kBlock), 0, c.stream, c.d_labels, ids2, n, lkey);
-    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, lkey, c.d_labs, ids2, c.d_perm, static_cast<int>(n), 0,
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, lkey, c.d_labs, ids2, c.d_perm, size_t(n), 0,
                                                     64, c.stream));
     hipLaunchKernelGGL(k_inverse_perm, dim3(g), dim3(kBlock), 0, c.stream, c.d_perm, n, c.d_pos);
     // label-major offsets of this shard's rows: padded (slots) and real (degree sums)
@@ -1345,10 +1348,10 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
     auto* rdeg = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
     hipLaunchKernelGGL(k_perm_degrees, dim3(g), dim3(kBlock), 0, c.stream, c.d_offl, c.d_perm, n, pdeg, rdeg);
     size_t tmp3 = 0;
-    PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp3, pdeg, c.d_offp + 1, static_cast<int>(n), c.stream));
+    PM_HIP_CHECK(rocprim::inclusive_scan(nullptr, tmp3, pdeg, c.d_offp + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
     void* d_tmp3 = c.arena.get(tmp3);
-    PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(d_tmp3, tmp3, pdeg, c.d_offp + 1, static_cast<int>(n), c.stream));
-    PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(d_tmp3, tmp3, rdeg, c.d_offr + 1, static_cast<int>(n), c.stream));
+    PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp3, tmp3, pdeg, c.d_offp + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
+    PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp3, tmp3, rdeg, c.d_offr + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_offr, 0, sizeof(uint64_t), c.stream));
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, kWpb, 65535)), dim3(kBlock), 0, c.stream, src_col, src_start,
@@ -1640,10 +1643,9 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
   if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
   reduce_into(c, grid, d_slot);
   // slist = survivors in label-major row order (tiles are in position order)
-  hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> it(c.d_tcnt, Widen());
+  rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> it(c.d_tcnt, Widen());
   size_t tmp = c.scan_tmp_bytes;
-  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(c.d_scan_tmp, tmp, it, c.d_tbase, static_cast<int>(c.ntiles),
-                                                c.stream));
+  PM_HIP_CHECK(rocprim::exclusive_scan(c.d_scan_tmp, tmp, it, c.d_tbase, uint64_t(0), size_t(c.ntiles), rocprim::plus<uint64_t>(), c.stream));
   c.smask_valid = false;
   hipLaunchKernelGGL(k_slist_write, dim3(grid_for(c.ntiles, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_tcnt,
                      c.d_tstart, reinterpret_cast<const unsigned long long*>(c.d_tmask), c.d_tbase, c.ntiles, c.d_slist,
@@ -1652,10 +1654,9 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
 }
 
 size_t slist_scan_tmp_bytes(uint64_t words) {
-  hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> it(nullptr, Widen());
+  rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> it(nullptr, Widen());
   size_t tmp = 0;
-  PM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, static_cast<uint64_t*>(nullptr),
-                                                static_cast<int>(std::max<uint64_t>(words, 1)), hipStream_t(0)));
+  PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, tmp, it, static_cast<uint64_t*>(nullptr), uint64_t(0), size_t(std::max<uint64_t>(words, 1)), rocprim::plus<uint64_t>(), hipStream_t(0)));
   return tmp;
 }
 
@@ -1758,7 +1759,7 @@ LineArgs make_line_args(const Ctx& c, const NlcLine& line) {
 }
 
 // Source selection, nem_1.hpp:387-479 / tds_batch_1.hpp:1067-1135 (over S:
-// T_pub != 0 only for members of S).  Stream compaction of slist (hipcub).
+// T_pub != 0 only for members of S).  Stream compaction of slist (rocPRIM).
 struct SourcePred {
   const uint16_t* tpub;
   LineArgs la;
@@ -2118,11 +2119,11 @@ static T* arena_alloc(Ctx& c, uint64_t n) {
 static uint64_t exclusive_scan_u32_to_u64(Ctx& c, const uint32_t* in, uint64_t* out, uint64_t n) {
   // out[0..n] = exclusive prefix; returns total (synchronizes the stream).
   if (n == 0) return 0;
-  hipcub::TransformInputIterator<uint64_t, hipcub::CastOp<uint64_t>, const uint32_t*> it(in, hipcub::CastOp<uint64_t>());
+  rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> it(in, Widen());
   size_t tmp = 0;
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, it, out + 1, static_cast<int>(n), c.stream));
+  PM_HIP_CHECK(rocprim::inclusive_scan(nullptr, tmp, it, out + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
   void* d_tmp = c.arena.get(tmp);
-  PM_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(d_tmp, tmp, it, out + 1, static_cast<int>(n), c.stream));
+  PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp, tmp, it, out + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(uint64_t), c.stream));
   uint64_t total = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&total, out + n, sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
@@ -2148,15 +2149,15 @@ static void ensure_sources(Ctx& c, const LineArgs& la, int tds, const NlcLine& l
   const int nitems = static_cast<int>(std::max<uint32_t>(c.nS_host, 1));
   PM_HIP_CHECK(hipMemsetAsync(d_ns, 0, 2 * sizeof(int), c.stream));
   if (c.nS_host) {
-    PM_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
-    PM_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp2, c.d_slist, c.d_sources, d_ns, nitems, dpred, c.stream));
+    PM_HIP_CHECK(rocprim::select(nullptr, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
+    PM_HIP_CHECK(rocprim::select(nullptr, tmp2, c.d_slist, c.d_sources, d_ns, nitems, dpred, c.stream));
     void* d_tmp = c.arena.get(std::max(tmp, tmp2));
     if (la.sv) {
-      PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp, c.d_slist, ilist, d_ns + 1, nitems, pred, c.stream));
+      PM_HIP_CHECK(rocprim::select(d_tmp, tmp, c.d_slist, ilist, d_ns + 1, nitems, pred, c.stream));
       tmp2 = std::max(tmp, tmp2);
-      PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp2, c.d_slist, c.d_sources, d_ns, nitems, dpred, c.stream));
+      PM_HIP_CHECK(rocprim::select(d_tmp, tmp2, c.d_slist, c.d_sources, d_ns, nitems, dpred, c.stream));
     } else {
-      PM_HIP_CHECK(hipcub::DeviceSelect::If(d_tmp, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
+      PM_HIP_CHECK(rocprim::select(d_tmp, tmp, c.d_slist, c.d_sources, d_ns, nitems, pred, c.stream));
     }
     hipLaunchKernelGGL(k_mark_sources, dim3(grid_for(c.nS_host, kBlock, 1024)), dim3(kBlock), 0, c.stream,
                        c.d_sources, d_ns, c.d_tsm);
@@ -2191,10 +2192,10 @@ static uint64_t pseen_start(Ctx& c, const NlcLine& line, const unsigned long lon
   hipLaunchKernelGGL(k_pseen_keep, dim3(grid_for(c.npseen, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_pseen,
                      c.npseen, c.d_tpub[c.cur], c.d_labs, line.labels.back(), keep);
   size_t tmp = 0;
-  PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, tmp, c.d_pseen, keep, kept, d_n, static_cast<int>(c.npseen),
+  PM_HIP_CHECK(rocprim::select(nullptr, tmp, c.d_pseen, keep, kept, d_n, size_t(c.npseen),
                                              c.stream));
   void* d_tmp = c.arena.get(tmp);
-  PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(d_tmp, tmp, c.d_pseen, keep, kept, d_n, static_cast<int>(c.npseen),
+  PM_HIP_CHECK(rocprim::select(d_tmp, tmp, c.d_pseen, keep, kept, d_n, size_t(c.npseen),
                                              c.stream));
   int n = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&n, d_n, sizeof(n), hipMemcpyDeviceToHost, c.stream));
@@ -2220,9 +2221,9 @@ static void pseen_end(Ctx& c, const SeenSet& seen) {
   }
   auto* sorted = arena_alloc<unsigned long long>(c, total);
   size_t tmp = 0;
-  PM_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, cat, sorted, static_cast<int>(total), 0, 64, c.stream));
+  PM_HIP_CHECK(rocprim::radix_sort_keys(nullptr, tmp, cat, sorted, size_t(total), 0, 64, c.stream));
   void* d_tmp = c.arena.get(tmp);
-  PM_HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(d_tmp, tmp, cat, sorted, static_cast<int>(total), 0, 64, c.stream));
+  PM_HIP_CHECK(rocprim::radix_sort_keys(d_tmp, tmp, cat, sorted, size_t(total), 0, 64, c.stream));
   if (c.pseen_cap < total) {
     if (c.d_pseen) (void)hipFree(c.d_pseen);
     c.pseen_cap = std::max<uint64_t>(total, 2 * c.pseen_cap);
@@ -2230,9 +2231,9 @@ static void pseen_end(Ctx& c, const SeenSet& seen) {
   }
   auto* d_n = arena_alloc<int>(c, 1);
   tmp = 0;
-  PM_HIP_CHECK(hipcub::DeviceSelect::Unique(nullptr, tmp, sorted, c.d_pseen, d_n, static_cast<int>(total), c.stream));
+  PM_HIP_CHECK(rocprim::unique(nullptr, tmp, sorted, c.d_pseen, d_n, size_t(total), rocprim::equal_to<unsigned long long>(), c.stream));
   d_tmp = c.arena.get(tmp);
-  PM_HIP_CHECK(hipcub::DeviceSelect::Unique(d_tmp, tmp, sorted, c.d_pseen, d_n, static_cast<int>(total), c.stream));
+  PM_HIP_CHECK(rocprim::unique(d_tmp, tmp, sorted, c.d_pseen, d_n, size_t(total), rocprim::equal_to<unsigned long long>(), c.stream));
   int n = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&n, d_n, sizeof(n), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -2336,10 +2337,10 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     auto* keys_s = arena_alloc<unsigned long long>(c, ntok);
     auto* par_s = arena_alloc<uint32_t>(c, ntok);
     size_t tmp = 0;
-    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, keys, keys_s, tp, par_s, static_cast<int>(ntok), 0,
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp, keys, keys_s, tp, par_s, size_t(ntok), 0,
                                                     64, c.stream));
     void* d_tmp = c.arena.get(tmp);
-    PM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tmp, keys, keys_s, tp, par_s, static_cast<int>(ntok), 0,
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, keys, keys_s, tp, par_s, size_t(ntok), 0,
                                                     64, c.stream));
     auto* head = arena_alloc<uint8_t>(c, ntok);
     auto* excl = arena_alloc<uint32_t>(c, ntok);
@@ -2350,10 +2351,10 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     auto* fx = arena_alloc<uint32_t>(c, ntok);
     auto* d_nsel = arena_alloc<int>(c, 1);
     tmp = 0;
-    PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, tmp, keys_s, head, fk, d_nsel, static_cast<int>(ntok), c.stream));
+    PM_HIP_CHECK(rocprim::select(nullptr, tmp, keys_s, head, fk, d_nsel, size_t(ntok), c.stream));
     d_tmp = c.arena.get(tmp);
-    PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(d_tmp, tmp, keys_s, head, fk, d_nsel, static_cast<int>(ntok), c.stream));
-    PM_HIP_CHECK(hipcub::DeviceSelect::Flagged(d_tmp, tmp, excl, head, fx, d_nsel, static_cast<int>(ntok), c.stream));
+    PM_HIP_CHECK(rocprim::select(d_tmp, tmp, keys_s, head, fk, d_nsel, size_t(ntok), c.stream));
+    PM_HIP_CHECK(rocprim::select(d_tmp, tmp, excl, head, fx, d_nsel, size_t(ntok), c.stream));
     int nsel = 0;
     PM_HIP_CHECK(hipMemcpyAsync(&nsel, d_nsel, sizeof(int), hipMemcpyDeviceToHost, c.stream));
     PM_HIP_CHECK(hipStreamSynchronize(c.stream));

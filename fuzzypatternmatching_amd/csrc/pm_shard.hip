@@ -18,7 +18,7 @@
 // Results are identical for every shard count.
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+
 #include <rccl/rccl.h>
 
 #include <algorithm>
