@@ -241,7 +241,6 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap);
   if (c->dcap) {
     c->d_dmoff = dalloc<uint32_t>(c->n);
-    c->d_dctr = dalloc<unsigned long long>(1);
   }
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
@@ -309,7 +308,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_dctr, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1474,7 +1473,7 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     const int mode = variant >= 256 ? 0 : variant;
     pm::ensure_counts(*ctx, 1);
     pm::lcc_first_prepare(*ctx);
-    // the product launch writes dense M when the search would (counter reset per launch)
+    // the product launch writes dense M when the search would
     if (mode == 0) pm::lcc_first_set_dense(*ctx);
     pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
     PM_HIP_CHECK(hipEventRecord(a, ctx->stream));

@@ -296,13 +296,12 @@ struct Ctx {
   uint64_t* d_tbase = nullptr;    // exclusive scan of the per-tile survivor counts
   uint32_t* d_tcode = nullptr;   // superstep-0 T_pub in 2 bits per position (k_lcc_first -> first later superstep)
   // dense superstep-0 M (one shard, symmetric graph, diameter >= 2): light tiles
-  // append their contributors to the region [dbase, dbase + dcap) of d_mcol and
+  // append their contributors to their wave's slice of the region [dbase, dbase + dcap) of d_mcol and
   // d_dmoff[u] gives survivor u's first entry there (kNone: M in u's padded
   // row); the first later superstep reads M densely and writes the rows of its
   // survivors into their padded rows
   uint64_t dbase = 0, dcap = 0;
   uint32_t* d_dmoff = nullptr;
-  unsigned long long* d_dctr = nullptr;
   bool k1_dense = false;         // the last superstep-0 launch wrote dense M
   uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile

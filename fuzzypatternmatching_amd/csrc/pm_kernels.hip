@@ -164,8 +164,8 @@ struct K1Out {
   uint32_t* tstart;  // per tile: position of row 0 (light) or the heavy row
   uint32_t* tcode;   // T_pub in 2 bits per position (tpub_code), OR-ed in
   uint32_t* dmoff;   // dense M: survivor's first entry in mcol[dbase..] (null: M in padded rows)
-  unsigned long long* dctr;  // dense M: entries appended so far
-  uint64_t dbase, dcap;
+  uint64_t dbase;    // dense M: first entry of the region in mcol
+  uint64_t dslice;   // dense M: entries of the region owned by each wave of the grid
 };
 
 
@@ -598,7 +598,8 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
 // survivors in slot order at the start of u's padded row; leaves the tile's
 // TN words zero.
 template <int MODE>
-__device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stage& st) {
+__device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stage& st, uint64_t& dcur,
+                                         uint64_t dend) {
   const int lane = lane_id();
   if (!p.tm) return;
   if (!(MODE & 64) && lane < kSub)
@@ -611,17 +612,14 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
     // no survivor: the half words of verified rows are already 0
     return;
   }
-  // dense M: the tile's whole contributor list goes to one appended block
-  // (coalesced), survivor u's M starts at list index hd[row] of it; a tile that
-  // no longer fits the region keeps the padded-row layout
-  uint64_t dpos = 0;
-  bool dense = false;
-  if (o.dmoff) {
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(o.dctr, static_cast<unsigned long long>(p.nlist));
-    dpos = uniform64(b);
-    dense = dpos + p.nlist <= o.dcap;
-  }
+  // dense M: the tile's whole contributor list is appended to the wave's own
+  // slice of the region (coalesced; a cursor in scalar registers, no atomics:
+  // one counter shared by the grid serialised 2.5 M atomics and cost 20 ms),
+  // survivor u's M starts at list index hd[row] of it; a tile that no longer
+  // fits the slice keeps the padded-row layout
+  const uint64_t dpos = dcur;
+  const bool dense = o.dmoff && dcur + p.nlist <= dend;
+  if (dense) dcur += p.nlist;
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
 #pragma unroll 1
   for (uint32_t gi = 0; gi < p.ngroups; ++gi) {
@@ -766,12 +764,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   if (t < ntiles) cur = k1_desc(kt, r, t);
   uint32_t sc = k1_load(vc, cur, colp, t < ntiles);
   K1Pend pend{};  // the previous light tile's stores
+  // dense M: this wave's slice of the region
+  uint64_t dcur = uniform64((uint64_t(blockIdx.x) * kWpb + wid) * o.dslice);
+  const uint64_t dend = uniform64(dcur + o.dslice);
   while (t < ntiles) {
     t = __builtin_amdgcn_readfirstlane(t);
     const uint32_t tn = t + W;
     // the previous tile's stores go out ahead of the next tile's loads
     k1_pend_uniform(pend);
-    k1_flush<MODE>(pend, o, st);
+    dcur = uniform64(dcur);
+    k1_flush<MODE>(pend, o, st, dcur, dend);
     pend.tm = nullptr;
     K1Desc nxt{};
     if (tn < ntiles) nxt = k1_desc(kt, r, tn);
@@ -800,7 +802,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
   }
   k1_pend_uniform(pend);
-  k1_flush<MODE>(pend, o, st);
+  dcur = uniform64(dcur);
+  k1_flush<MODE>(pend, o, st, dcur, dend);
   // heavy rows, one segment per wave at a time (a separate loop: no slot
   // buffers live, so the light loop's register budget is its own)
   if (!(MODE & 4))
@@ -1568,9 +1571,10 @@ void build_tiling(Ctx& c) {
   c.k1_grid = lcc_first_grid(c);
 }
 
-static K1Out k1_out(Ctx& c) {
+static K1Out k1_out(Ctx& c, unsigned grid) {
   return K1Out{c.d_tst,   c.d_tpub[c.cur], c.d_mcol,  c.d_mlen, c.d_malive, c.d_tcnt,
-               c.d_tstart, c.d_tcode,      c.k1_dense ? c.d_dmoff : nullptr, c.d_dctr, c.dbase, c.dcap};
+               c.d_tstart, c.d_tcode,      c.k1_dense ? c.d_dmoff : nullptr, c.dbase,
+               c.dcap / (uint64_t(std::max(grid, 1u)) * kWpb)};
 }
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
@@ -1578,7 +1582,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
 #define PM_K1_ARGS                                                                                                    \
   dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab,                                    \
       static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,                                                  \
-      c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c), c.d_hscr, c.nheavy, c.nhseg,                         \
+      c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c, grid), c.d_hscr, c.nheavy, c.nhseg,                         \
       reinterpret_cast<unsigned long long*>(c.d_tmask), partials(c, d_slot)
   switch (variant) {
     case 0:
@@ -1618,7 +1622,6 @@ unsigned lcc_first_grid(const Ctx& c) {
 void lcc_first_set_dense(Ctx& c) {
   static const bool dense_env = !std::getenv("PM_DENSE_M") || std::string(std::getenv("PM_DENSE_M")) != "0";
   c.k1_dense = dense_env && c.dcap && !c.comm && c.symmetric && c.pattern.graph.diameter >= 2;
-  if (c.k1_dense) PM_HIP_CHECK(hipMemsetAsync(c.d_dctr, 0, sizeof(unsigned long long), c.stream));
 }
 
 void lcc_first_prepare(Ctx& c) {
