@@ -306,7 +306,7 @@ static void destroy_ctx(pm_ctx* c) {
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
-                  c->d_mlen, c->d_malive, c->d_slist, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
+                  c->d_mlen, c->d_malive, c->d_slist, c->d_slist2, c->d_nS2, c->d_ccnt, c->d_cbase, c->d_ctmp, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
                   c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
                   };
@@ -416,6 +416,9 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       // graph: no cycle flag set yet); push form otherwise (one shard only)
       if (!c.comm && !c.force_pull && (!c.symmetric || !init_step)) launch_lcc_push(c, slot);
       else launch_lcc_step(c, slot, init_step && ss == 1);
+      // S collapses in the first later supersteps (S=28 tree: 9.8 M -> 0.8 M -> 26 k):
+      // the next supersteps, the NLC lines and the next reset walk the live entries only
+      if (!c.comm && init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
       shard_exchange_tpub(c);
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
@@ -667,6 +670,15 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
       f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
       add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
+      if (phase_times) {
+        uint64_t sv = 0, se = 0;
+        for (auto x : lo.vcount[ss]) sv += x;
+        for (auto x : lo.ecount[ss]) se += x;
+        std::fprintf(stderr, "[pm] LP itr %llu superstep %zu: |S| %llu, |M| %llu, traversed %llu, %.1f us\n",
+                     static_cast<unsigned long long>(itr_), ss, static_cast<unsigned long long>(sv),
+                     static_cast<unsigned long long>(se), static_cast<unsigned long long>(lo.trav[ss]),
+                     lo.seconds[ss] * 1e6);
+      }
       s.lcc_edges += lo.trav[ss];
       totals(lo.vcount[ss], lo.ecount[ss]);
       cur_vc = lo.vcount[ss];

@@ -282,6 +282,15 @@ struct Ctx {
   uint32_t* d_malive = nullptr;   // |M[v]|
   uint32_t* d_slist = nullptr;    // S members after superstep 0 (superset of S later), positions
   uint32_t* d_nS = nullptr;       // device count of d_slist
+  // slist compaction (one shard): the live entries of a superstep's mask move
+  // to d_slist2 / d_nS2, then the pointers swap; per-chunk counts and bases
+  uint32_t* d_slist2 = nullptr;
+  uint32_t* d_nS2 = nullptr;
+  uint32_t* d_ccnt = nullptr;
+  uint32_t* d_cbase = nullptr;
+  void* d_ctmp = nullptr;
+  size_t ctmp_bytes = 0;
+  uint64_t ccap = 0;              // chunk capacity of d_ccnt / d_cbase
   // live mask of slist per 64 entries, written by every later superstep
   // (members of S plus vertices removed in that superstep): later passes
   // skip dead chunks without touching them
@@ -379,6 +388,7 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false);
 // LCC calls after the first (M may be asymmetric there).
 void launch_lcc_push(Ctx& c, uint64_t* d_slot);
 void launch_count_state(Ctx& c, uint64_t* d_slot);
+void launch_compact_slist(Ctx& c);  // keeps the live entries of the last superstep's mask
 // Zero T_pub (both buffers) at the slist entries of the last search (every
 // nonzero T_pub entry is one of them, plus the other shards' when sharded).
 void launch_clear_tpub(Ctx& c);

@@ -889,7 +889,7 @@ __device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
 __global__ __launch_bounds__(kBlock) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
-    const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
+    uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
     const uint32_t* __restrict__ dmoff, uint64_t dbase) {
@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         cnt = cntr;
       }
     }
-    bool survivor = false, removed = false;
+    bool survivor = false, removed = false, cleared = false;
     if (dmoff) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
     if (Tu) {
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
@@ -1061,12 +1061,25 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         malive[u] = 0;
         cnt = 0;
         if (drow) mlen[u] = 0;  // M[v] cleared (nonunique_ee.hpp:941-964); its padded row was never written
+        // first later superstep: neighbours read u's T_pub through the 2-bit codes unless u's label has
+        // more than two template vertices, so the buffer read now can be cleared at once and u leaves
+        // the live list (otherwise it stays live one more superstep, which clears the other buffer)
+        if (tcode) {
+          uint32_t tu = 0;
+          for (int l = 0; l < nruns; ++l)
+            if (u - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
+          const uint32_t rest = tu & (tu - 1);
+          if (!(rest & (rest - 1))) {
+            tcur[u] = 0;
+            cleared = true;
+          }
+        }
       }
     }
     // live mask of the next superstep (S only shrinks); a vertex removed now
     // stays live one more superstep so that its 0 also reaches the other
     // T_pub buffer (it is dropped once it arrives with T_pub = 0)
-    const uint64_t lm = __ballot(survivor || removed);
+    const uint64_t lm = __ballot(survivor || (removed && !cleared));
     if (lane == 0) mask_out[chunk] = lm;
     acc.trav += alive0;
     acc.removed |= removed;
@@ -1700,6 +1713,65 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   c.cur ^= 1;
   c.smask_cur ^= 1;
   c.smask_valid = true;
+}
+
+// slist compaction: per 64-entry chunk the live count, then (after an
+// exclusive scan) the live entries in their order, and the new count.
+__global__ void k_live_counts(const unsigned long long* __restrict__ mask, const uint32_t* __restrict__ nSp,
+                              uint64_t cap, uint32_t* __restrict__ cnt) {
+  const uint64_t nch = (uint64_t(*nSp) + kWave - 1) / kWave;
+  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < cap; c += uint64_t(gridDim.x) * blockDim.x)
+    cnt[c] = c < nch ? static_cast<uint32_t>(__builtin_popcountll(mask[c])) : 0u;
+}
+
+__global__ void k_live_write(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ mask,
+                             const uint32_t* __restrict__ nSp, const uint32_t* __restrict__ cnt,
+                             const uint32_t* __restrict__ base, uint64_t cap, uint32_t* __restrict__ out,
+                             uint32_t* __restrict__ nS_out) {
+  const uint64_t nS = *nSp;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t c = i / kWave;
+    const uint32_t b = static_cast<uint32_t>(i % kWave);
+    const unsigned long long m = mask[c];
+    if ((m >> b) & 1ull) out[base[c] + __builtin_popcountll(m & ((1ull << b) - 1))] = slist[i];
+    if (i == nS - 1) *nS_out = base[c] + cnt[c];
+  }
+  if (nS == 0 && blockIdx.x == 0 && threadIdx.x == 0) *nS_out = 0;
+}
+
+void launch_compact_slist(Ctx& c) {
+  const uint64_t cap = (uint64_t(c.nS_host) + kWave - 1) / kWave;  // nS_host: upper bound of the device count
+  if (!cap || !c.smask_valid) return;
+  if (c.ccap < cap) {
+    if (c.d_ccnt) (void)hipFree(c.d_ccnt);
+    if (c.d_cbase) (void)hipFree(c.d_cbase);
+    if (c.d_ctmp) (void)hipFree(c.d_ctmp);
+    c.d_ccnt = c.d_cbase = nullptr;
+    c.d_ctmp = nullptr;
+    const uint64_t words = std::max<uint64_t>(cap, (c.n + kWave - 1) / kWave);
+    PM_HIP_CHECK(hipMalloc(&c.d_ccnt, words * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMalloc(&c.d_cbase, words * sizeof(uint32_t)));
+    PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, c.ctmp_bytes, c.d_ccnt, c.d_cbase, 0u, size_t(words),
+                                         rocprim::plus<uint32_t>(), c.stream));
+    PM_HIP_CHECK(hipMalloc(&c.d_ctmp, std::max<size_t>(c.ctmp_bytes, 1)));
+    c.ccap = words;
+  }
+  if (!c.d_slist2) {
+    PM_HIP_CHECK(hipMalloc(&c.d_slist2, std::max<uint64_t>(c.n, 1) * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMalloc(&c.d_nS2, sizeof(uint32_t)));
+  }
+  const auto* mask = reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur]);
+  hipLaunchKernelGGL(k_live_counts, dim3(grid_for(cap, kBlock, 4096)), dim3(kBlock), 0, c.stream, mask, c.d_nS, cap,
+                     c.d_ccnt);
+  size_t tb = c.ctmp_bytes;
+  PM_HIP_CHECK(rocprim::exclusive_scan(c.d_ctmp, tb, c.d_ccnt, c.d_cbase, 0u, size_t(cap), rocprim::plus<uint32_t>(),
+                                       c.stream));
+  hipLaunchKernelGGL(k_live_write, dim3(grid_for(uint64_t(c.nS_host), kBlock, 8192)), dim3(kBlock), 0, c.stream,
+                     c.d_slist, mask, c.d_nS, c.d_ccnt, c.d_cbase, cap, c.d_slist2, c.d_nS2);
+  PM_HIP_CHECK(hipGetLastError());
+  std::swap(c.d_slist, c.d_slist2);
+  std::swap(c.d_nS, c.d_nS2);
+  c.smask_valid = false;  // every entry of the new list is live
 }
 
 __global__ void k_clear_tpub(const uint32_t* __restrict__ list, const uint32_t* __restrict__ np, uint64_t cap,
