@@ -418,7 +418,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       else launch_lcc_step(c, slot, init_step && ss == 1);
       // S collapses in the first later supersteps (S=28 tree: 9.8 M -> 0.8 M -> 26 k):
       // the next supersteps, the NLC lines and the next reset walk the live entries only
-      if (!c.comm && init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
+      if (!c.comm && init_step && ss >= 1 && ss <= 3 && ss + 1 < D) launch_compact_slist(c);
       shard_exchange_tpub(c);
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));

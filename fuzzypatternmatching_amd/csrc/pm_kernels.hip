@@ -1715,24 +1715,45 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   c.smask_valid = true;
 }
 
-// slist compaction: per 64-entry chunk the live count, then (after an
-// exclusive scan) the live entries in their order, and the new count.
-__global__ void k_live_counts(const unsigned long long* __restrict__ mask, const uint32_t* __restrict__ nSp,
-                              uint64_t cap, uint32_t* __restrict__ cnt) {
-  const uint64_t nch = (uint64_t(*nSp) + kWave - 1) / kWave;
-  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < cap; c += uint64_t(gridDim.x) * blockDim.x)
-    cnt[c] = c < nch ? static_cast<uint32_t>(__builtin_popcountll(mask[c])) : 0u;
+// slist compaction after a later superstep: an entry stays iff it is live in
+// the superstep's mask AND still in S (T_pub just written != 0); a live entry
+// whose T_pub became 0 was removed by that superstep: the T_pub buffer that
+// superstep read is cleared here (the other one holds its 0 already), so it
+// need not stay live one more superstep.  One wave per 64-entry chunk: the
+// keep ballot is the chunk's keep mask; then (after an exclusive scan of the
+// chunk counts) the kept entries in their order, and the new count.
+__global__ void k_live_keep(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ mask,
+                            const uint32_t* __restrict__ nSp, uint64_t cap, const uint16_t* __restrict__ tnew,
+                            uint16_t* __restrict__ told, unsigned long long* __restrict__ kmask,
+                            uint32_t* __restrict__ cnt) {
+  const uint64_t nS = *nSp;
+  const int lane = lane_id();
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;  // a multiple of kWave: a wave stays on one chunk
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cap * kWave; i += stride) {
+    const uint64_t c = i / kWave;
+    bool keep = false;
+    if (i < nS && ((mask[c] >> lane) & 1ull)) {
+      const uint32_t u = slist[i];
+      keep = tnew[u] != 0;
+      if (!keep) told[u] = 0;
+    }
+    const uint64_t b = __ballot(keep);
+    if (lane == 0) {
+      kmask[c] = b;
+      cnt[c] = static_cast<uint32_t>(__builtin_popcountll(b));
+    }
+  }
 }
 
-__global__ void k_live_write(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ mask,
+__global__ void k_live_write(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ kmask,
                              const uint32_t* __restrict__ nSp, const uint32_t* __restrict__ cnt,
-                             const uint32_t* __restrict__ base, uint64_t cap, uint32_t* __restrict__ out,
+                             const uint32_t* __restrict__ base, uint32_t* __restrict__ out,
                              uint32_t* __restrict__ nS_out) {
   const uint64_t nS = *nSp;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint64_t c = i / kWave;
     const uint32_t b = static_cast<uint32_t>(i % kWave);
-    const unsigned long long m = mask[c];
+    const unsigned long long m = kmask[c];
     if ((m >> b) & 1ull) out[base[c] + __builtin_popcountll(m & ((1ull << b) - 1))] = slist[i];
     if (i == nS - 1) *nS_out = base[c] + cnt[c];
   }
@@ -1761,13 +1782,16 @@ void launch_compact_slist(Ctx& c) {
     PM_HIP_CHECK(hipMalloc(&c.d_nS2, sizeof(uint32_t)));
   }
   const auto* mask = reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur]);
-  hipLaunchKernelGGL(k_live_counts, dim3(grid_for(cap, kBlock, 4096)), dim3(kBlock), 0, c.stream, mask, c.d_nS, cap,
-                     c.d_ccnt);
+  // the keep masks replace the superstep's live masks (that buffer is rewritten by the next superstep)
+  auto* kmask = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
+  // after launch_lcc_step: tpub[cur] was just written, tpub[cur ^ 1] was read
+  hipLaunchKernelGGL(k_live_keep, dim3(grid_for(cap * kWave, kBlock, 2048)), dim3(kBlock), 0, c.stream, c.d_slist,
+                     mask, c.d_nS, cap, c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], kmask, c.d_ccnt);
   size_t tb = c.ctmp_bytes;
   PM_HIP_CHECK(rocprim::exclusive_scan(c.d_ctmp, tb, c.d_ccnt, c.d_cbase, 0u, size_t(cap), rocprim::plus<uint32_t>(),
                                        c.stream));
-  hipLaunchKernelGGL(k_live_write, dim3(grid_for(uint64_t(c.nS_host), kBlock, 8192)), dim3(kBlock), 0, c.stream,
-                     c.d_slist, mask, c.d_nS, c.d_ccnt, c.d_cbase, cap, c.d_slist2, c.d_nS2);
+  hipLaunchKernelGGL(k_live_write, dim3(grid_for(uint64_t(c.nS_host), kBlock, 2048)), dim3(kBlock), 0, c.stream,
+                     c.d_slist, kmask, c.d_nS, c.d_ccnt, c.d_cbase, c.d_slist2, c.d_nS2);
   PM_HIP_CHECK(hipGetLastError());
   std::swap(c.d_slist, c.d_slist2);
   std::swap(c.d_nS, c.d_nS2);
