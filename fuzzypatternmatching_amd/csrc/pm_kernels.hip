@@ -633,10 +633,12 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
       if (!(MODE & 128)) {
         // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
         const uint32_t u = p.ustart + row, b2 = u * 2u, b4 = u * 4u;
-        *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
+        // a dense row's T_state (= T_pub) and |M| (= its length) are implied: the first later
+        // superstep, the only reader before they are rewritten, takes them from T_pub and mlen
+        if (!dense) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
         *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
         *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+        if (!dense) *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
         atomicOr(&o.tcode[u >> 4], tpub_code(T, p.tu) << ((u & 15u) << 1));
         if (o.dmoff)
           *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.dmoff) + b4) =
@@ -941,10 +943,19 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
       // the row's state is loaded with T_pub in one round trip (a removed
       // row, T_pub = 0, ignores it)
       Tu = tcur[u];
-      const uint64_t b = offp[u];
-      const uint32_t l = mlen[u], a0 = malive[u];
+      const uint32_t l = mlen[u];
       const uint32_t dm = dmoff ? dmoff[u] : kNone;
-      Ts = tst[u];
+      // a dense superstep-0 row: T_state = T_pub, |M| = its length, and its padded row start is
+      // needed only if it survives (three scattered loads instead of six per row)
+      uint64_t b = 0;
+      uint32_t a0 = l;
+      if (dm == kNone) {
+        b = offp[u];
+        a0 = malive[u];
+        Ts = tst[u];
+      } else {
+        Ts = Tu;
+      }
       if (Tu) {
         drow = dm != kNone;
         pb = b;
@@ -1053,8 +1064,10 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step(
         tnxt[u] = T;
         malive[u] = cnt;
         // dense M: the survivor's (updated) row moves to its padded row
-        if (drow)
+        if (drow) {
+          pb = offp[u];
           for (uint32_t j = 0; j < len; ++j) mcol[pb + j] = mcol[beg + j];
+        }
       } else {
         removed = true;
         tnxt[u] = 0;
