@@ -291,6 +291,7 @@ struct Ctx {
   void* d_ctmp = nullptr;
   size_t ctmp_bytes = 0;
   uint64_t ccap = 0;              // chunk capacity of d_ccnt / d_cbase
+  bool slist_compacted = false;   // d_slist holds S only (shorter than the host bound nS_host)
   // live mask of slist per 64 entries, written by every later superstep
   // (members of S plus vertices removed in that superstep): later passes
   // skip dead chunks without touching them

@@ -1667,6 +1667,7 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
   lcc_first_prepare(c);
   PM_HIP_CHECK(hipMemsetAsync(c.d_tcode, 0, ((c.n + 15) / 16 + 1) * sizeof(uint32_t), c.stream));
   lcc_first_set_dense(c);
+  c.slist_compacted = false;
   if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
   launch_lcc_first_kernel(c, 0, grid, d_slot);
   if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
@@ -1712,7 +1713,8 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   // first later superstep (every slist entry live): one chunk per wave, the
   // latency-bound rows need waves in flight; afterwards few chunks are live
   // and a persistent-style grid skips the dead ones cheaply
-  const unsigned grid = grid_for(chunks, kWpb, c.smask_valid ? kMaxGrid : 16384);
+  // (a compacted list is short: its all-live pass needs no more than a few waves per CU)
+  const unsigned grid = grid_for(chunks, kWpb, c.smask_valid ? kMaxGrid : c.slist_compacted ? 2048 : 16384);
   const unsigned long long* min = c.smask_valid ? reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur])
                                                 : nullptr;
   auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
@@ -1742,7 +1744,9 @@ __global__ void k_live_keep(const uint32_t* __restrict__ slist, const unsigned l
   const uint64_t nS = *nSp;
   const int lane = lane_id();
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;  // a multiple of kWave: a wave stays on one chunk
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cap * kWave; i += stride) {
+  // chunks of the device count only (cap: host upper bound; the scan reads counts below nch alone)
+  const uint64_t end = min(cap, (nS + kWave - 1) / kWave) * kWave;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < end; i += stride) {
     const uint64_t c = i / kWave;
     bool keep = false;
     if (i < nS && ((mask[c] >> lane) & 1ull)) {
@@ -1809,6 +1813,7 @@ void launch_compact_slist(Ctx& c) {
   std::swap(c.d_slist, c.d_slist2);
   std::swap(c.d_nS, c.d_nS2);
   c.smask_valid = false;  // every entry of the new list is live
+  c.slist_compacted = true;
 }
 
 __global__ void k_clear_tpub(const uint32_t* __restrict__ list, const uint32_t* __restrict__ np, uint64_t cap,
