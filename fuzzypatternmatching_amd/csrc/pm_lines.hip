@@ -340,6 +340,24 @@ __device__ __forceinline__ void build_active(const LineKernelArgs& a) {
   const int lane = lane_id();
   const uint32_t nS = *a.nS;
   const uint64_t nch = (uint64_t(nS) + kWave - 1) / kWave;
+  if (nch <= uint64_t(g.nw) * 4) {
+    // a short (compacted) list: one chunk per wave, so that the chunks' dependent
+    // loads and reservations overlap across waves instead of queueing in one
+    for (uint64_t ch = g.gw; ch < nch; ch += g.nw) {
+      const uint64_t live = a.smask ? a.smask[ch] : ~0ull;  // wave-uniform
+      if (!live) continue;
+      const uint64_t i = ch * kWave + lane;
+      uint32_t v = 0;
+      bool ok = false;
+      if (i < nS && ((live >> lane) & 1ull)) {
+        v = a.slist[i];
+        ok = a.tpub[v] != 0;
+      }
+      const uint64_t pos = wave_reserve(a.nact, ok ? 1u : 0u);
+      if (ok) a.act[pos] = v;
+    }
+    return;
+  }
   for (uint64_t c0 = g.gw * kWave; c0 < nch; c0 += g.nw * kWave) {
     const uint64_t ch = c0 + lane;
     const uint64_t lm = ch < nch ? (a.smask ? a.smask[ch] : ~0ull) : 0ull;
