@@ -888,7 +888,7 @@ __device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
   return x;
 }
 
-__global__ __launch_bounds__(kBlock) void k_lcc_step(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
     uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
