@@ -68,6 +68,12 @@ static void require_gfx950(int device) {
   PM_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
     throw std::runtime_error(std::string("device arch ") + prop.gcnArchName + " is not gfx950 (MI355X)");
+  // the driver loop waits on a few small read-backs per search: spin instead of
+  // yielding, so the next launch follows the device at once (PM_SPIN=0: runtime
+  // default; refused once the device's context is active, which then keeps its flags)
+  static const bool spin = !std::getenv("PM_SPIN") || std::string(std::getenv("PM_SPIN")) != "0";
+  if (spin && hipSetDevice(device) == hipSuccess && hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess)
+    (void)hipGetLastError();
 }
 
 // Graph of one context: the whole graph (nshards == 1) or one shard's rows.
