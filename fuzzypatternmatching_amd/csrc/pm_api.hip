@@ -320,6 +320,7 @@ static void destroy_ctx(pm_ctx* c) {
     if (p) (void)hipFree(p);
   delete c->comm_owned;
   if (c->h_pin) (void)hipHostFree(c->h_pin);
+  if (c->h_pin_lines) (void)hipHostFree(c->h_pin_lines);
   free_line_buffers(*c);
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -348,6 +349,7 @@ static void reset_state(Ctx& c) {
     PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[1], 0, c.n * sizeof(uint16_t), c.stream));
   }
   c.tpub_clean = true;
+  c.lines_prelaunched = false;  // (a failed search may leave one behind; the stream has run it)
   // d_tsm needs no reset: only sources are read, and selecting a source resets its entry
   c.smask_valid = false;
   PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
@@ -438,6 +440,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     c.comm->allreduce_sum_u64(c.d_counts, D * W, c.stream);
   }
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  if (c.prelaunch_lines) prelaunch_lines_fused(c);  // the device goes on with the lines while the host parses
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("lcc synced");
   std::vector<uint64_t> host(pin + 1 + D * W, pin + 1 + 2 * D * W);
@@ -701,7 +704,10 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     const auto t_lp = std::chrono::steady_clock::now();
     const bool was_init = init_step;
     auto t0 = tick();
+    // iteration 0 always runs the lines (beta.cpp:686-688): one shard enqueues them behind the LCC
+    c.prelaunch_lines = itr == 0 && !c.comm && c.fused_lines && !P.lines.empty();
     LccOut lo = lcc_call(c, init_step);
+    c.prelaunch_lines = false;
     ph_lcc += since(t0);
     if (was_init) {  // this shard's superstep-0 kernel (roofline bytes)
       first_scanned = c.ss0_trav;

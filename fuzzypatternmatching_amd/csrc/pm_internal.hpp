@@ -261,8 +261,14 @@ struct Ctx {
   size_t xred_cap = 0;
 
   // host side of the driver loop
-  uint64_t* h_pin = nullptr;      // pinned staging for counter / line-stat read-backs
+  uint64_t* h_pin = nullptr;      // pinned staging for counter read-backs
   size_t h_pin_words = 0;
+  uint64_t* h_pin_lines = nullptr;  // pinned staging for the fused lines' read-back
+  size_t h_pin_lines_words = 0;
+  bool prelaunch_lines = false;   // lcc_call enqueues the lines before it waits (run_beta, iteration 0)
+  bool lines_prelaunched = false;
+  size_t pre_pl0 = 0, pre_nl = 0; // the prelaunched batch
+  uint32_t* pre_kept = nullptr;
   bool fine_timing = false;       // per-superstep events (result files / PM_PHASE_TIMES)
   bool tpub_clean = false;        // T_pub is zero outside the last search's slist entries
   // PM_PHASE_TIMES: host timestamps of the driver loop (diagnostics)
@@ -422,6 +428,10 @@ struct FusedLineOut {
 // run the per-position path with token exchange).
 size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
                        size_t max_lines = SIZE_MAX);
+// Enqueues the fused launch of lines [0, all) behind the work already on the stream
+// (the first LCC call of a search, whose lines always run: beta.cpp:686-688); the
+// next run_lines_fused(c, 0, ...) then only waits for it and reads its results.
+void prelaunch_lines_fused(Ctx& c);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);

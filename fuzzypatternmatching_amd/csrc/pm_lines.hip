@@ -814,15 +814,15 @@ static void upload_lines(Ctx& c) {
   c.d_lstats_n = nl;
 }
 
-size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
-                       size_t max_lines) {
+// Enqueues lines [pl0, nl) and the read-back of their results into the lines'
+// pinned buffer; returns nl (pl0 >= nl: nothing launched).
+static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept_out) {
   if (c.comm) throw std::runtime_error("internal: fused lines run on one shard only");
   c.probe("lines entry");
   const size_t nl_all = c.pattern.lines.size();
   const size_t nl = pl0 < nl_all && max_lines < nl_all - pl0 ? pl0 + max_lines : nl_all;
-  overflow = false;
-  outs.clear();
-  if (pl0 >= nl) return 0;
+  kept_out = nullptr;
+  if (pl0 >= nl) return nl;
   for (size_t pl = pl0; pl < nl; ++pl) {
     const NlcLine& line = c.pattern.lines[pl];
     const size_t stride = line.cycle_length + 2;
@@ -901,11 +901,45 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   // read-back through pinned memory: [done | kept slots | line stats]
   static_assert(sizeof(LineStats) % 8 == 0, "LineStats is read back as u64 words");
   const size_t sw = sizeof(LineStats) / 8;
-  uint64_t* pin = pinned(c, 2 + (nl - pl0) * sw);
+  const size_t words = 2 + (nl - pl0) * sw;
+  if (c.h_pin_lines_words < words) {
+    if (c.h_pin_lines) (void)hipHostFree(c.h_pin_lines);
+    c.h_pin_lines = nullptr;
+    const size_t w = std::max<size_t>(words, 1 << 12);
+    PM_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.h_pin_lines), w * sizeof(uint64_t), hipHostMallocDefault));
+    c.h_pin_lines_words = w;
+  }
+  uint64_t* pin = c.h_pin_lines;
   PM_HIP_CHECK(hipMemcpyAsync(pin, d_done, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1, d_kept_ctr, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipMemcpyAsync(pin + 2, c.d_lstats + pl0, (nl - pl0) * sizeof(LineStats), hipMemcpyDeviceToHost,
                               c.stream));
+  kept_out = a.kept;
+  return nl;
+}
+
+void prelaunch_lines_fused(Ctx& c) {
+  c.pre_pl0 = 0;
+  c.pre_nl = launch_lines(c, 0, SIZE_MAX, c.pre_kept);
+  c.lines_prelaunched = true;
+}
+
+size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLineOut>& outs, bool& overflow,
+                       size_t max_lines) {
+  overflow = false;
+  outs.clear();
+  size_t nl;
+  uint32_t* kept_dev = nullptr;
+  if (c.lines_prelaunched && pl0 == c.pre_pl0 && max_lines == SIZE_MAX) {
+    nl = c.pre_nl;
+    kept_dev = c.pre_kept;
+  } else {
+    if (c.lines_prelaunched) throw std::runtime_error("internal: prelaunched NLC lines not consumed in order");
+    nl = launch_lines(c, pl0, max_lines, kept_dev);
+  }
+  c.lines_prelaunched = false;
+  if (pl0 >= nl) return 0;
+  uint64_t* pin = c.h_pin_lines;
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("lines synced");
   std::vector<LineStats> hs(nl - pl0);
@@ -915,7 +949,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   std::vector<uint32_t> kept;
   if (want_walks && kept_slots) {
     kept.resize(kept_slots);
-    PM_HIP_CHECK(hipMemcpy(kept.data(), a.kept, kept_slots * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    PM_HIP_CHECK(hipMemcpy(kept.data(), kept_dev, kept_slots * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
   if (std::getenv("PM_PHASE_TIMES")) {
