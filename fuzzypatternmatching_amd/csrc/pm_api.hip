@@ -426,7 +426,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       else launch_lcc_step(c, slot, init_step && ss == 1);
       // S collapses in the first later supersteps (S=28 tree: 9.8 M -> 0.8 M -> 26 k):
       // the next supersteps, the NLC lines and the next reset walk the live entries only
-      if (!c.comm && init_step && ss >= 1 && ss <= 3 && ss + 1 < D) launch_compact_slist(c);
+      if (!c.comm && init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
       shard_exchange_tpub(c);
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
@@ -645,7 +645,8 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
                                                                std::vector<std::vector<std::string>>(c.nranks));
   pm_run_stats s{};
   c.device_seconds = 0.0;
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  // pattern_time_start (beta.cpp:539): the reset above is only enqueued; the
+  // search's kernels follow it on the stream without a host round trip
   const auto t_pattern = std::chrono::steady_clock::now();
   c.probe("start");
   auto since = [](std::chrono::steady_clock::time_point t) {
