@@ -1499,11 +1499,11 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     pm::ensure_counts(*ctx, 1);
     pm::lcc_first_prepare(*ctx);
     // the product launch writes dense M when the search would
-    if (mode == 0) pm::lcc_first_set_dense(*ctx);
+    if (mode == 0 || mode == 5) pm::lcc_first_set_dense(*ctx);
     pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
     PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
     for (int i = 0; i < reps; ++i) {
-      if (mode == 0) pm::lcc_first_set_dense(*ctx);
+      if (mode == 0 || mode == 5) pm::lcc_first_set_dense(*ctx);
       pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);
     }
     PM_HIP_CHECK(hipEventRecord(b, ctx->stream));

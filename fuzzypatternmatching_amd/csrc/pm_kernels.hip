@@ -731,8 +731,8 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
 // and the label test (checksum), bit4 stops light tiles after phase A, bit5
 // after phase B1.  WIDE: some range has more than four
 // relevant label runs (tbits_rel scans them all).
-template <int MODE, bool WIDE = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_lcc_first(
+template <int MODE, bool WIDE = false, int WMIN = 6>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, uint32_t nhseg, unsigned long long* __restrict__ tmask,
@@ -1625,6 +1625,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 32: hipLaunchKernelGGL(k_lcc_first<32>, PM_K1_ARGS); break;
     case 80: hipLaunchKernelGGL(k_lcc_first<80>, PM_K1_ARGS); break;
     case 128: hipLaunchKernelGGL(k_lcc_first<128>, PM_K1_ARGS); break;
+    case 5: hipLaunchKernelGGL((k_lcc_first<0, false, 5>), PM_K1_ARGS); break;  // 5 waves/SIMD, no spills
     default: throw std::runtime_error("unknown superstep-0 kernel variant");
   }
 #undef PM_K1_ARGS
