@@ -110,3 +110,16 @@ def test_mt19937_jump_ahead_matches_stepping():
     for seed, skip in [(5492, 123457), (7, 624), (11, 623), (13, 0), (5489 + 21, 5 * 28 * 4096 + 3)]:
         got = list(pm.mt19937_jump_outputs(seed, skip, 3))
         assert got == [oracle.mt19937_nth(seed, skip + i + 1) for i in range(3)]
+
+
+def test_gpu_ingest_without_gpu_fails_loudly(tmp_path):
+    """pm_ingest.hip has no CPU fallback: without a gfx950 device the C-ABI reports an error."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    f = tmp_path / "e.txt"
+    f.write_text("0 1\n1 0\n")
+    with pytest.raises(pm.PMError, match="no HIP device|not gfx950"):
+        pm.ingest_edge_list_gpu([str(f)], False)
+    with pytest.raises(pm.PMError, match="no HIP device|not gfx950"):
+        pm.edge_list_matcher([str(f)], os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern"))
