@@ -2422,10 +2422,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   uint64_t ninit = 0;
   ensure_sources(c, la, 0, line, &init, &ninit);
   res.sources = c.nsources;
-  // sharded: a line without an initiator on any shard exchanges nothing at any
-  // position, so every shard skips it (one sum instead of C + 1 token exchanges)
-  // (the sum is collective: every shard takes part, whatever its own count)
-  if (sharded ? shard_allreduce(c, {ninit})[0] == 0 : ninit == 0) {
+  if (ninit == 0 && !sharded) {
     pseen_end(c, seen);
     return res;
   }
@@ -2541,8 +2538,7 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   ensure_sources(c, la, 1, line);
   res.sources = c.nsources;
   const bool sharded = c.comm != nullptr;
-  // sharded: a line without a source on any shard is skipped by every shard (a collective sum)
-  if (sharded ? shard_allreduce(c, {uint64_t(c.nsources)})[0] == 0 : c.nsources == 0) return res;
+  if (c.nsources == 0 && !sharded) return res;
   const uint16_t* tpub = c.d_tpub[c.cur];
   auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
   auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
