@@ -322,7 +322,7 @@ struct Ctx {
   uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile
   uint32_t* d_tstart = nullptr;   // position of a tile's row 0 (heavy tile: its row)
-  void* d_scan_tmp = nullptr;     // hipcub scan workspace for the slist build
+  void* d_scan_tmp = nullptr;     // rocPRIM scan workspace for the slist build
   size_t scan_tmp_bytes = 0;
   uint64_t tmask_words = 0;
   uint64_t last_acked = 0;

@@ -31,16 +31,15 @@
 // through ld_dev (L1-bypassing atomic loads); TDS walk regions are fresh,
 // 128-B aligned memory per position.
 //
-// Launch: an ordinary launch whose grid (at most one 1024-thread block per CU,
-// hipOccupancyMaxActiveBlocksPerMultiprocessor >= 1 checked) is co-resident:
-// the kernel runs alone on its stream after its stream-ordered predecessors,
-// and the only other work a shard's device may carry (RCCL, another in-process
-// shard's kernels; ThreadGroup holds the device during compute) runs to
-// completion without waiting on it, so every block is eventually scheduled.
-// hipLaunchCooperativeKernel is not used: the dedicated cooperative queue it
-// creates crashes libhsa-runtime's exit-time teardown under rocprofv3 (the
-// profile is written, the process then dies with SIGSEGV in
-// libamdhip64 -> libhsa-runtime64; tools/rp_exit.py beta vs beta_nocoop).
+// Launch: hipLaunchCooperativeKernel with at most one 1024-thread block per CU
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor >= 1 checked), so the runtime
+// guarantees that every block of the grid is resident before the software grid
+// barrier below is relied on.  PM_LINES_NOCOOP=1 (profiling only) takes an
+// ordinary launch instead: the dedicated cooperative queue crashes
+// libhsa-runtime's exit-time teardown under rocprofv3 (the profile is written,
+// the process then dies with SIGSEGV in libamdhip64 -> libhsa-runtime64;
+// tools/rp_exit.py beta vs beta_nocoop); the grid is then co-resident only
+// because nothing else runs on the device during a profiled bench.
 
 #include <hip/hip_runtime.h>
 
@@ -49,6 +48,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 
 #include "pm_device.hpp"
 #include "pm_internal.hpp"
@@ -895,8 +895,13 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   // before the first grid barrier completes)
   const unsigned grid = static_cast<unsigned>(
       std::max<uint64_t>(16, std::min<uint64_t>(c.line_grid, (c.live_hint + 255) / 256)));
-  PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args, 0,
-                               c.stream));
+  static const bool nocoop = std::getenv("PM_LINES_NOCOOP") && std::string(std::getenv("PM_LINES_NOCOOP")) == "1";
+  if (nocoop)
+    PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args, 0,
+                                 c.stream));
+  else
+    PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args,
+                                            0, c.stream));
   c.probe("lines launched");
   // read-back through pinned memory: [done | kept slots | line stats]
   static_assert(sizeof(LineStats) % 8 == 0, "LineStats is read back as u64 words");

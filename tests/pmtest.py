@@ -51,6 +51,65 @@ def _strip_time(lines, keep_cols):
     return [", ".join(l.split(", ")[:keep_cols]) for l in lines]
 
 
+def _sha(lines):
+    import hashlib
+    h = hashlib.sha256()
+    for l in lines:
+        h.update(l.encode())
+        h.update(b"\n")
+    return h.hexdigest()
+
+
+def result_digest(result_dir, nranks):
+    """Rank-count-independent digest of a result directory (for fixtures at sizes whose
+    result files are too large to commit, e.g. the S=28 headline).
+
+    * result_pattern_set and result_iteration/step/superstep without the timing columns;
+    * count files summed over the rank files line by line, as the reference's aggregator
+      examples/scripts/total_active_count.py:38-91 does (the tokens of the first file's line
+      minus the last one, then the sum of the last tokens over all rank files);
+    * vertex / edge / subgraph files: the union over ranks with the rank column dropped,
+      as (line count, sha256 of the sorted lines)."""
+    d = os.path.join(result_dir, "0")
+    out = {}
+    ps = _read(os.path.join(result_dir, "result_pattern_set"))
+    # ps, P, iterations, seconds, |E_p|, |V_p|, #NLC (beta.cpp:1375-1381): P and seconds dropped
+    out["result_pattern_set"] = [", ".join(l.split(", ")[:1] + l.split(", ")[2:3] + l.split(", ")[4:]) for l in ps]
+    for name, cols in (("result_iteration", 1), ("result_step", 2), ("result_superstep", 3)):
+        out[name] = _strip_time(_read(os.path.join(d, name)), cols)
+    for sub, stem in (("all_ranks_active_vertices_count", "active_vertices_"),
+                      ("all_ranks_active_edges_count", "active_edges_")):
+        tot = None
+        for r in range(nranks):
+            ls = [l.split(", ") for l in _read(os.path.join(d, sub, stem + str(r)))]
+            if tot is None:
+                tot = [[", ".join(t[:-1]), int(t[-1])] for t in ls]
+            else:
+                assert len(ls) == len(tot), f"{sub}: rank files of different length"
+                for a, t in zip(tot, ls):
+                    a[1] += int(t[-1])
+        out[sub] = [f"{a}, {b}" for a, b in (tot or [])]
+    for sub, stem in (("all_ranks_active_vertices", "active_vertices_"), ("all_ranks_active_edges", "active_edges_")):
+        lines = []
+        for r in range(nranks):
+            lines += [l.split(", ", 1)[1] for l in _read(os.path.join(d, sub, stem + str(r))) if l]
+        lines.sort()
+        out[sub] = {"lines": len(lines), "sha256": _sha(lines)}
+    sg = os.path.join(d, "all_ranks_subgraphs")
+    by_line = {}
+    for fn in sorted(os.listdir(sg)):
+        pl = fn.split("_")[1]
+        by_line.setdefault(pl, [])
+        by_line[pl] += [l.split(", ", 1)[1] for l in _read(os.path.join(sg, fn)) if l]
+    out["all_ranks_subgraphs"] = {pl: {"lines": len(v), "sha256": _sha(sorted(v))} for pl, v in sorted(by_line.items())}
+    return out
+
+
+def digest_diffs(a, b):
+    """Keys on which two result_digest() dicts differ."""
+    return [f"{k}: {a.get(k)} != {b.get(k)}" for k in sorted(set(a) | set(b)) if a.get(k) != b.get(k)]
+
+
 def compare_result_dirs(a, b, nranks):
     """Returns a list of human-readable differences (empty = parity)."""
     diffs = []

@@ -154,3 +154,18 @@ def test_oracle_selected_vertices_known_answer(tmp_path):
     assert so["final_vertices"] == 0
     assert open(tmp_path / "b/0/all_ranks_active_vertices_count/active_vertices_0").read().split("\n")[3] == \
         "0, TP, 1, 3"
+
+
+def test_result_digest_is_rank_count_independent(tmp_path):
+    """pmtest.result_digest (the S=28 fixture's digest) sums count files over ranks and drops
+    the rank column, so one fixture checks any number of ranks / shards."""
+    import pmtest
+    off, col = oracle.rmat_csr(13, 4)
+    pattern = os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern")
+    ds = []
+    for nr in (1, 3):
+        rd = str(tmp_path / f"r{nr}")
+        oracle.run(off, col, pattern, rd, nranks=nr)
+        ds.append(pmtest.result_digest(rd, nr))
+    assert pmtest.digest_diffs(ds[0], ds[1]) == []
+    assert ds[0]["all_ranks_active_vertices"]["lines"] > 0

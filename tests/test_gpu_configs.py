@@ -104,7 +104,33 @@ def test_c5_ingested_edge_list_with_label_files(tmp_path):
     assert pmtest.compare_result_dirs(str(ora), str(out), nranks) == []
 
 
-@pytest.mark.skipif(os.environ.get("PM_BIG") != "1", reason="PM_BIG=1: S=28 one-GPU parity (~100 GB host memory)")
+def check_against_fixture(m, fixture, tmp_path, max_iterations=64):
+    """Runs the search of matcher m with result files and compares them with an oracle
+    fixture made by tests/golden/make_rmat_fixture.py (digest + counters)."""
+    import json
+    fx = json.load(open(fixture))
+    out = tmp_path / "gpu"
+    sg = m.run_beta(str(out), max_iterations)
+    dig = pmtest.result_digest(str(out), fx["nranks"])
+    diffs = pmtest.digest_diffs(fx["digest"], dig)
+    for k_g, k_o in (("iterations", "iterations"), ("terminated", "terminated"), ("final_vertices", "final_vertices"),
+                     ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"),
+                     ("tds_edges", "tds_edges"), ("walks", "paths")):
+        if sg[k_g] != fx["stats"][k_o]:
+            diffs.append(f"{k_g}: gpu {sg[k_g]} != oracle {fx['stats'][k_o]}")
+    return sg, diffs
+
+
 def test_c4_s28_tree_one_gpu(tmp_path):
-    sg = _check(_graph(28, 8), TREE, tmp_path)
-    print(f"S=28 parity: {sg}")
+    """The north_star headline (S=28, P_gen=8, tree) on one GPU, on the bench's path (graph generated
+    and laid out in HBM), against the oracle's S=28 result digest (tests/golden/rmat_s28_p8_tree.json,
+    made once on the GPU box's host by tests/golden/make_rmat_fixture.py: the oracle needs ~100 GB there)."""
+    fixture = os.path.join(pmtest.ROOT, "tests", "golden", "rmat_s28_p8_tree.json")
+    _graphs.clear()
+    m, _ = pm.rmat_matcher(28, 8, TREE, device=0)
+    try:
+        sg, diffs = check_against_fixture(m, fixture, tmp_path)
+    finally:
+        m.close()
+    assert diffs == [], diffs[:5]
+    print(f"S=28 parity vs the oracle fixture: {sg}")
