@@ -15,8 +15,9 @@ import numpy as np
 
 from . import _abi
 
-__all__ = ["Graph", "rmat_graph", "rmat_matcher", "mt19937_jump_outputs", "rmat_edges", "pattern_summary", "write_graph", "read_graph", "PatternMatcher",
-           "ShardedPatternMatcher", "partition_edges", "comm_unique_id", "run_beta_local_shards", "PMError"]
+__all__ = ["Graph", "rmat_graph", "rmat_matcher", "rmat_shard_matcher", "mt19937_jump_outputs", "rmat_edges",
+           "pattern_summary", "write_graph", "read_graph", "PatternMatcher", "ShardedPatternMatcher", "partition_edges",
+           "comm_unique_id", "run_beta_local_shards", "run_rmat_local_shards", "PMError"]
 
 DEFAULT_HUB_THRESHOLD = 1048576  # generate_rmat.cpp:106
 
@@ -211,6 +212,21 @@ def run_beta_local_shards(graph, pattern_dir, nshards, result_dir="", max_iterat
     return st.as_dict()
 
 
+def run_rmat_local_shards(scale, p_gen, pattern_dir, nshards, result_dir="", max_iterations=0, device=0, nranks=1,
+                          hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """The sharded search over the R-MAT graph with `nshards` shards driven by threads of this process
+    on one device: each shard generates its generator ranks' streams on the device and the entries
+    reach their owners in one in-process all-to-all (pm_run_rmat_local_shards)."""
+    if result_dir:
+        os.makedirs(result_dir, exist_ok=True)
+    st = _abi.RunStats()
+    rc = _lib().pm_run_rmat_local_shards(scale, p_gen, pattern_dir.encode(), device, nshards, nranks, hub_threshold,
+                                         result_dir.encode(), max_iterations, ctypes.byref(st))
+    if rc != 0:
+        raise _err()
+    return st.as_dict()
+
+
 def pattern_summary(pattern_dir):
     """Parsed pattern directory (graph.hpp / pattern_util.hpp rules) as a dict."""
     import json
@@ -341,6 +357,23 @@ def rmat_matcher(scale, p_gen, pattern_dir, device=0, nranks=1, hub_threshold=DE
     secs = ctypes.c_double()
     ctx = _lib().pm_create_rmat(scale, p_gen, pattern_dir.encode(), device, nranks, hub_threshold,
                                 ctypes.byref(secs))
+    if not ctx:
+        raise _err()
+    m = PatternMatcher.__new__(PatternMatcher)
+    m._ctx = ctx
+    m.graph = _DeviceGraph(1 << scale, (1 << scale) * 32, nranks, hub_threshold)
+    return m, secs.value
+
+
+def rmat_shard_matcher(scale, p_gen, pattern_dir, nshards, shard, unique_id, device=0, nranks=1,
+                       hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """One rank of a sharded search over the R-MAT graph (one process per GPU, collective): the rank
+    generates its generator ranks' streams on its GPU and the entries reach their owners in one RCCL
+    all-to-all (pm_create_rmat_shard).  Returns (matcher, seconds of generation + exchange + rows)."""
+    secs = ctypes.c_double()
+    uid = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
+    ctx = _lib().pm_create_rmat_shard(scale, p_gen, os.fspath(pattern_dir).encode(), device, nranks, hub_threshold,
+                                      nshards, shard, uid, ctypes.byref(secs))
     if not ctx:
         raise _err()
     m = PatternMatcher.__new__(PatternMatcher)

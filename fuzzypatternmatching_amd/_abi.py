@@ -121,6 +121,10 @@ SIGNATURES = [
     ("pm_rmat_csr_gpu", ctypes.c_int, [c_u64, c_u64, ctypes.c_int, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                        ctypes.POINTER(c_u64)]),
     ("pm_create_rmat", c_vp, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u64, ctypes.POINTER(ctypes.c_double)]),
+    ("pm_create_rmat_shard", c_vp, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u64, c_u32, c_u32, c_vp,
+                                    ctypes.POINTER(ctypes.c_double)]),
+    ("pm_run_rmat_local_shards", ctypes.c_int, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u32, c_u64, c_char_p,
+                                                c_u64, ctypes.POINTER(RunStats)]),
     ("pm_mt19937_jump_outputs", ctypes.c_int, [c_u32, c_u64, c_vp, c_u64]),
     ("pm_vertex_data_files", ctypes.c_int, [c_vp, c_char_p]),
     ("pm_graph_size", ctypes.c_int, [c_vp, ctypes.POINTER(c_u64), ctypes.POINTER(c_u64), ctypes.POINTER(ctypes.c_int)]),

@@ -190,6 +190,12 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   for (int t = 0; t < kMaxTemplateVertices; ++t) c->pa.adj[t] = pg.adj[t];
   c->pa.K = static_cast<int32_t>(pg.vertex_data.size());
   for (int t = 0; t < c->pa.K; ++t) c->pa.plabel[t] = pg.vertex_data[t];
+  // a label of more than two template vertices: its 2-bit code cannot carry T_pub (tpub_code)
+  for (int t = 0; t < c->pa.K; ++t) {
+    int k = 0;
+    for (int u = 0; u < c->pa.K; ++u) k += c->pa.plabel[u] == c->pa.plabel[t];
+    if (k > 2) c->xcode_wide = true;
+  }
   bool any_sv = false;
   for (size_t pl = 0; pl < c->pattern.lines.size(); ++pl) {
     const auto& l = c->pattern.lines[pl];
@@ -203,11 +209,18 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   for (uint64_t v = 0; v < c->n; ++v) {
     const uint64_t d = in.gdeg ? in.gdeg[v] : in.off[v + 1] - in.off[v];
     if (d > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
-    if (in.gdeg && in.off[v + 1] - in.off[v] && (in.off[v + 1] - in.off[v] != d || v % c->nshards != c->shard))
-      throw std::runtime_error("shard rows must be the owned rows (v % nshards == shard) with their full degree");
+    const uint64_t ld = in.off[v + 1] - in.off[v];
+    // a shard holds the whole rows it owns, and of a delegate (degree >= -d) the entries whose target it owns
+    if (in.gdeg && ld && (d >= c->hub_threshold && c->nshards > 1 ? ld > d
+                                                                   : (ld != d || v % c->nshards != c->shard)))
+      throw std::runtime_error("shard rows must be the owned rows (v % nshards == shard) with their full degree, "
+                               "and delegate rows (degree >= hub threshold) split by target owner");
     c->deg_host[v] = static_cast<uint32_t>(d);
     if (d >= c->hub_threshold) c->hubs_host.push_back(v);
   }
+  c->split_hubs = c->nshards > 1 && !c->hubs_host.empty();
+  for (uint64_t j = c->shard; c->split_hubs && j < c->hubs_host.size(); j += c->nshards)
+    c->hub_area += c->deg_host[c->hubs_host[j]];
   std::vector<uint64_t> goff;
   if (in.gdeg) {
     goff.assign(c->n + 1, 0);
@@ -224,10 +237,10 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_offr = dalloc<uint64_t>(c->n + 1);
   // slot buffers carry kTileEntries entries of tail padding (superstep-0 tile loads read whole tiles)
   // dense superstep-0 M region behind the tail padding (both buffers: relayout swaps them)
-  if (in.nshards == 1 && c->symmetric && c->nq)
+  if (c->symmetric && c->nq)
     c->dcap = std::min<uint64_t>(0xFFFFFFF0ull, std::max<uint64_t>(uint64_t(1) << 16, c->nq / 8));
   c->dbase = c->nq + kTileEntries;
-  c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap);
+  c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
   c->d_perm = dalloc<uint32_t>(c->n);
   c->d_pos = dalloc<uint32_t>(c->n);
   c->d_labs = dalloc<uint64_t>(c->n);
@@ -244,7 +257,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_tpub[0] = dalloc<uint16_t>(c->n);
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
-  c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap);
+  c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
   if (c->dcap) {
     c->d_dmoff = dalloc<uint32_t>(c->n);
   }
@@ -314,7 +327,8 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_slist2, c->d_nS2, c->d_ccnt, c->d_cbase, c->d_ctmp, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_xslist, c->d_xnS, c->d_xsend, c->d_xrecv, c->d_xred,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_xsend, c->d_xrecv, c->d_xent_send,
+                  c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -360,6 +374,8 @@ static void reset_state(Ctx& c) {
   c.cur = 0;
   c.nS_host = 0;
   c.lcc_started = false;
+  c.replicated = false;
+  c.k1_dense = false;
   c.nsources = 0;
   c.npseen = 0;
 }
@@ -420,17 +436,22 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       // then later supersteps size their grids by its upper bound
       c.nS_host = static_cast<uint32_t>(std::min<uint64_t>(c.ss0_rows, 0xFFFFFFFFull));
       c.lcc_started = true;
-      shard_after_first(c);  // sharded: every shard's slist, then T_pub
+      // sharded: the delegates' shares meet at their controllers; the survivors' codes of every shard
+      // for the next superstep's pulls; a one-superstep pattern goes to the replica at once
+      if (c.split_hubs) shard_hub_combine(c, slot);
+      if (D >= 2) shard_codes_after_first(c);
+      else shard_replicate(c);
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
       // pull form while M is known symmetric (the first call on a symmetric
-      // graph: no cycle flag set yet); push form otherwise (one shard only)
-      if (!c.comm && !c.force_pull && (!c.symmetric || !init_step)) launch_lcc_push(c, slot);
+      // graph: no cycle flag set yet); push form otherwise
+      if (!c.force_pull && (!c.symmetric || !init_step)) launch_lcc_push(c, slot);
       else launch_lcc_step(c, slot, init_step && ss == 1);
       // S collapses in the first later supersteps (S=28 tree: 9.8 M -> 0.8 M -> 26 k):
       // the next supersteps, the NLC lines and the next reset walk the live entries only
-      if (!c.comm && init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
-      shard_exchange_tpub(c);
+      if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
+      // sharded: after the first later superstep the state of S goes to the replica
+      if (init_step && ss == 1) shard_replicate(c);
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
@@ -438,16 +459,19 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   // read-back through pinned memory: [nS | local counts | summed counts]
   uint64_t* pin = pinned(c, 1 + 2 * D * W);
   PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-  if (c.comm) {  // this shard's counts, then the sums over the shards
+  // sharded: the supersteps before the replica counted this shard's rows only: their slots are summed
+  // over the shards (the replica's supersteps count the whole state on every shard)
+  const uint64_t sharded_slots = c.comm && init_step ? std::min<uint64_t>(D, 2) : 0;
+  if (sharded_slots) {  // this shard's counts, then the sums over the shards
     PM_HIP_CHECK(hipMemcpyAsync(pin + 1, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-    c.comm->allreduce_sum_u64(c.d_counts, D * W, c.stream);
+    c.comm->allreduce_sum_u64(c.d_counts, sharded_slots * W, c.stream);
   }
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   if (c.prelaunch_lines) prelaunch_lines_fused(c);  // the device goes on with the lines while the host parses
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("lcc synced");
   std::vector<uint64_t> host(pin + 1 + D * W, pin + 1 + 2 * D * W);
-  std::vector<uint64_t> local = c.comm ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
+  std::vector<uint64_t> local = sharded_slots ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
   const uint32_t nS = static_cast<uint32_t>(pin[0] & 0xFFFFFFFFull);
   c.nS_host = nS;
   LccOut out;
@@ -498,7 +522,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   if (asym)
     throw std::runtime_error(
         "active-edge map became asymmetric (a cycle-marked edge outlived its neighbour's message) in a pull-form "
-        "superstep (sharded search, or PM_FORCE_PULL=1)");
+        "superstep (PM_FORCE_PULL=1)");
   return out;
 }
 
@@ -556,77 +580,57 @@ static uint32_t owner_host(const Ctx& c, uint64_t v) {
 }
 
 // State by vertex id: T_pub, |M[v]| and the alive M entries (neighbour ids,
-// rows in vertex-id order, entries in the row's id order).
+// rows in vertex-id order, entries in the row's order: neighbour-id order).
+// The rows of S are packed on the device (pack_state: every member of S is an
+// slist entry with T_pub != 0), so only the state map crosses PCIe.  A sharded
+// context holds the replica of the whole state after its first superstep pair,
+// so every shard exports everything.
 static void export_state(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32_t>& mdeg,
                          std::vector<uint32_t>& nbrs) {
   const uint64_t n = c.n;
-  std::vector<uint16_t> tp(n);
-  std::vector<uint32_t> mlen(n), malive(n);
-  std::vector<uint64_t> off(n + 1);
-  PM_HIP_CHECK(hipMemcpy(tp.data(), c.d_tpub[c.cur], n * sizeof(uint16_t), hipMemcpyDeviceToHost));
-  PM_HIP_CHECK(hipMemcpy(mlen.data(), c.d_mlen, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  PM_HIP_CHECK(hipMemcpy(malive.data(), c.d_malive, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  PM_HIP_CHECK(hipMemcpy(off.data(), c.d_offp, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  std::vector<uint32_t> pos(n);
-  for (uint64_t i = 0; i < n; ++i) pos[c.perm_host[i]] = static_cast<uint32_t>(i);
   tpub.assign(n, 0);
   mdeg.assign(n, 0);
   nbrs.clear();
-  std::vector<uint32_t> m(c.nq);  // one bulk copy of the active-edge map
-  if (c.nq) PM_HIP_CHECK(hipMemcpy(m.data(), c.d_mcol, c.nq * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (!c.lcc_started || !c.nS_host) return;
+  if (c.comm && !c.replicated) throw std::runtime_error("pm_export_state: the sharded state is not replicated yet");
+  const uint64_t ne = pack_state_entry_bound(c);
+  const uint64_t nr = pinned(c, 2)[0];
+  uint32_t *d_rec = nullptr, *d_ent = nullptr;
+  PM_HIP_CHECK(hipMalloc(&d_rec, std::max<uint64_t>(c.nS_host, 1) * 16));
+  if (hipMalloc(&d_ent, std::max<uint64_t>(ne, 1) * 4) != hipSuccess) {
+    (void)hipFree(d_rec);
+    throw std::runtime_error("pm_export_state: out of device memory");
+  }
+  std::vector<uint32_t> rec(nr * 4), ent(ne);
+  try {
+    pack_state(c, d_rec, d_ent, ne, c.d_xcnt + 2);
+    if (nr) PM_HIP_CHECK(hipMemcpyAsync(rec.data(), d_rec, nr * 16, hipMemcpyDeviceToHost, c.stream));
+    if (ne) PM_HIP_CHECK(hipMemcpyAsync(ent.data(), d_ent, ne * 4, hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  } catch (...) {
+    (void)hipFree(d_rec);
+    (void)hipFree(d_ent);
+    throw;
+  }
+  (void)hipFree(d_rec);
+  (void)hipFree(d_ent);
+  std::vector<uint64_t> at(n, ~0ull);
+  for (uint64_t i = 0; i < nr; ++i) {
+    const uint32_t v = c.perm_host[rec[4 * i]];
+    tpub[v] = static_cast<uint16_t>(rec[4 * i + 1]);
+    mdeg[v] = rec[4 * i + 2];
+    at[v] = i;
+  }
   for (uint64_t v = 0; v < n; ++v) {
-    const uint32_t p = pos[v];
-    if (!tp[p] || v % c.nshards != c.shard) continue;  // sharded: owned rows only (export_state_all)
-    tpub[v] = tp[p];
-    mdeg[v] = malive[p];
-    const uint32_t L = mlen[p];
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < L; ++i) {
-      const uint32_t x = m[off[p] + i];
-      if (x & kAlive) {
-        nbrs.push_back(c.perm_host[x & kPosMask]);
-        ++k;
-      }
-    }
-    if (k != malive[p]) throw std::runtime_error("internal: alive count mismatch in export");
+    if (at[v] == ~0ull) continue;
+    const uint32_t* r = rec.data() + 4 * at[v];
+    for (uint32_t k = 0; k < r[2]; ++k) nbrs.push_back(c.perm_host[ent[r[3] + k] & kPosMask]);
   }
 }
 
-// Sharded: every shard exports the S members it owns; the records
-// [id, T_pub, |M|, neighbours...] are gathered so that each shard returns the
-// whole state, by vertex id (collective).
 static void export_state_all(Ctx& c, std::vector<uint16_t>& tpub, std::vector<uint32_t>& mdeg,
                              std::vector<uint32_t>& nbrs) {
   export_state(c, tpub, mdeg, nbrs);
-  if (!c.comm) return;
-  std::vector<uint32_t> rec;
-  uint64_t pos = 0;
-  for (uint64_t v = 0; v < c.n; ++v) {
-    if (!tpub[v]) continue;
-    const uint32_t k = mdeg[v];
-    if (v % c.nshards == c.shard) {
-      rec.push_back(static_cast<uint32_t>(v));
-      rec.push_back(tpub[v]);
-      rec.push_back(k);
-      rec.insert(rec.end(), nbrs.begin() + pos, nbrs.begin() + pos + k);
-    }
-    pos += k;
-  }
-  const auto parts = shard_allgatherv(c, rec);
-  tpub.assign(c.n, 0);
-  mdeg.assign(c.n, 0);
-  std::vector<std::pair<const std::vector<uint32_t>*, uint64_t>> at(c.n, {nullptr, 0});
-  for (const auto& part : parts)
-    for (uint64_t i = 0; i < part.size(); i += 3 + part[i + 2]) {
-      const uint32_t v = part[i];
-      tpub[v] = static_cast<uint16_t>(part[i + 1]);
-      mdeg[v] = part[i + 2];
-      at[v] = {&part, i + 3};
-    }
-  nbrs.clear();
-  for (uint64_t v = 0; v < c.n; ++v)
-    if (tpub[v]) nbrs.insert(nbrs.end(), at[v].first->begin() + at[v].second,
-                             at[v].first->begin() + at[v].second + mdeg[v]);
 }
 
 static void write_lines(const std::string& path, const std::vector<std::string>& lines) {
@@ -709,7 +713,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     const bool was_init = init_step;
     auto t0 = tick();
     // iteration 0 always runs the lines (beta.cpp:686-688): one shard enqueues them behind the LCC
-    c.prelaunch_lines = itr == 0 && !c.comm && c.fused_lines && !P.lines.empty();
+    c.prelaunch_lines = itr == 0 && c.fused_lines && !P.lines.empty();
     LccOut lo = lcc_call(c, init_step);
     c.prelaunch_lines = false;
     ph_lcc += since(t0);
@@ -742,34 +746,8 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         FusedLineOut fo;
         bool fused = false;
         auto t1 = tick();
-        if (c.comm) {
-          // sharded: the per-position path with the token / walk exchange
-          // (shard_route), then post-processing of this shard's sources, the
-          // sums over the shards and the T_pub of every shard's slist
-          tr = pl >= 4 ? run_tds_line(c, line, walks, stride) : run_path_line(c, line);
-          deleted = launch_post_tp(c, line);
-          count_state(c, loc_vc, loc_ec);
-          stride = static_cast<uint32_t>(line.cycle_length + 2);
-          std::vector<uint64_t> sums = {deleted, tr.sources, tr.acked, tr.edges, tr.tokens, tr.walks};
-          sums.insert(sums.end(), loc_vc.begin(), loc_vc.end());
-          sums.insert(sums.end(), loc_ec.begin(), loc_ec.end());
-          sums = shard_allreduce(c, sums);
-          deleted = sums[0] ? 1u : 0u;
-          tr.sources = sums[1];
-          tr.acked = sums[2];
-          tr.edges = sums[3];
-          tr.tokens = sums[4];
-          tr.walks = sums[5];
-          vc.assign(sums.begin() + 6, sums.begin() + 6 + c.nranks);
-          ec.assign(sums.begin() + 6 + c.nranks, sums.begin() + 6 + 2 * c.nranks);
-          shard_exchange_tpub(c);
-          if (files && pl >= 4) {
-            std::vector<uint32_t> all;
-            for (auto& part : shard_allgatherv(c, walks)) all.insert(all.end(), part.begin(), part.end());
-            walks.swap(all);
-          }
-          ph_tp += since(t1);
-        } else if (c.fused_lines && pl != exact_at) {
+        if (c.comm && !c.replicated) throw std::runtime_error("internal: NLC line before the sharded state was replicated");
+        if (c.fused_lines && pl != exact_at) {
           if (pl < batch_pl0 || pl >= batch_pl0 + batch.size()) {
             bool overflow = false;
             const size_t n = run_lines_fused(c, pl, files, batch, overflow);
@@ -781,9 +759,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
             fused = true;
           }
         }
-        if (c.comm) {
-          // done above
-        } else if (fused) {
+        if (fused) {
           tr = fo.tr;
           deleted = fo.deleted;
           vc = cur_vc;
@@ -1136,14 +1112,25 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
     const uint64_t n = g->n;
     std::vector<uint32_t> gdeg(n);
     for (uint64_t v = 0; v < n; ++v) gdeg[v] = static_cast<uint32_t>(g->off[v + 1] - g->off[v]);
-    // owner rule: shard q holds the rows of ids v % nshards == q
+    // owner rule: shard q holds the rows of ids v % nshards == q; a delegate's row (degree >= the hub
+    // threshold) is split by target owner: shard q holds its entries u with u % nshards == q
+    // (delegate_partitioned_graph.ipp:818-969, 1402-1648)
     std::vector<std::vector<uint64_t>> offs(nshards, std::vector<uint64_t>(n + 1, 0));
     std::vector<std::vector<uint32_t>> cols(nshards);
     for (uint32_t q = 0; q < nshards; ++q) {
       for (uint64_t v = 0; v < n; ++v) {
-        const bool own = v % nshards == q;
-        offs[q][v + 1] = offs[q][v] + (own ? gdeg[v] : 0);
-        if (own) cols[q].insert(cols[q].end(), g->col + g->off[v], g->col + g->off[v + 1]);
+        uint64_t k = 0;
+        if (nshards > 1 && gdeg[v] >= g->hub_threshold) {
+          for (uint64_t e = g->off[v]; e < g->off[v + 1]; ++e)
+            if (g->col[e] % nshards == q) {
+              cols[q].push_back(g->col[e]);
+              ++k;
+            }
+        } else if (v % nshards == q) {
+          cols[q].insert(cols[q].end(), g->col + g->off[v], g->col + g->off[v + 1]);
+          k = gdeg[v];
+        }
+        offs[q][v + 1] = offs[q][v] + k;
       }
       if (cols[q].empty()) cols[q].push_back(0);
     }
@@ -1316,6 +1303,110 @@ pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, 
     if (s) (void)hipStreamDestroy(s);
     pm::g_last_error = e.what();
     return nullptr;
+  }
+}
+
+}  // extern "C"
+
+namespace pm {
+// One shard of the R-MAT graph built on the device (pm_rmat.hip rmat_shard_device) and its context;
+// the communicator passes to the context.
+static pm_ctx* create_rmat_shard_ctx(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device,
+                                     uint32_t nranks, uint64_t hub_threshold, uint32_t nshards, uint32_t shard,
+                                     Comm* comm, uint32_t inprocess, double* gen_seconds) {
+  std::unique_ptr<Comm> owned(comm);
+  hipStream_t s = nullptr;
+  DevCsr g;
+  try {
+    require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint32_t> gdeg;
+    g = rmat_shard_device(scale, p_gen, hub_threshold, *comm, nshards, shard, gdeg, s);
+    if (gen_seconds) *gen_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<uint64_t> off(g.n + 1);
+    PM_HIP_CHECK(hipMemcpy(off.data(), g.d_off, off.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    (void)hipFree(g.d_off);
+    g.d_off = nullptr;
+    CtxInput in;
+    in.n = g.n;
+    in.off = off.data();
+    in.col = g.d_col;
+    in.col_on_device = true;
+    in.gdeg = gdeg.data();
+    in.symmetric = true;
+    in.nranks = nranks;
+    in.hub_threshold = hub_threshold;
+    in.nshards = nshards;
+    in.shard = shard;
+    in.comm = owned.release();
+    in.inprocess_shards = inprocess;
+    pm_ctx* c = create_ctx(in, pattern_dir, device);
+    (void)hipFree(g.d_col);
+    (void)hipStreamDestroy(s);
+    return c;
+  } catch (...) {
+    if (g.d_off) (void)hipFree(g.d_off);
+    if (g.d_col) (void)hipFree(g.d_col);
+    if (s) (void)hipStreamDestroy(s);
+    throw;
+  }
+}
+}  // namespace pm
+
+extern "C" {
+pm_ctx* pm_create_rmat_shard(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nranks,
+                             uint64_t hub_threshold, uint32_t nshards, uint32_t shard, const uint8_t* unique_id,
+                             double* gen_seconds) {
+  try {
+    if (!unique_id) throw std::runtime_error("pm_create_rmat_shard: null communicator id");
+    PM_HIP_CHECK(hipSetDevice(device));
+    pm::Comm* comm = pm::make_rccl_comm(unique_id, static_cast<int>(nshards), static_cast<int>(shard));
+    return pm::create_rmat_shard_ctx(scale, p_gen, pattern_dir, device, nranks, hub_threshold, nshards, shard, comm, 1,
+                                     gen_seconds);
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
+                             uint32_t nranks, uint64_t hub_threshold, const char* result_dir, uint64_t max_iterations,
+                             pm_run_stats* out) {
+  try {
+    if (nshards == 0 || nshards > 64) throw std::runtime_error("pm_run_rmat_local_shards: 1..64 shards");
+    pm::ThreadGroup grp(static_cast<int>(nshards));
+    std::vector<pm_run_stats> st(nshards);
+    std::vector<std::string> errs(nshards);
+    const std::string dir = result_dir ? result_dir : "";
+    auto work = [&](uint32_t q) {
+      std::unique_lock<std::mutex> dev(grp.device);
+      pm_ctx* ctx = nullptr;
+      try {
+        PM_HIP_CHECK(hipSetDevice(device));
+        ctx = pm::create_rmat_shard_ctx(scale, p_gen, pattern_dir, device, nranks, hub_threshold, nshards, q,
+                                        pm::make_thread_comm(&grp, static_cast<int>(q)), nshards, nullptr);
+        pm::run_beta(*ctx, dir, max_iterations, &st[q]);
+      } catch (const std::exception& e) {
+        errs[q] = e.what();
+        grp.abort();
+      }
+      if (ctx) pm::destroy_ctx(ctx);
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t q = 0; q < nshards; ++q) pool.emplace_back(work, q);
+    for (auto& t : pool) t.join();
+    for (uint32_t q = 0; q < nshards; ++q)
+      if (!errs[q].empty() && errs[q] != "another shard failed")
+        throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
+    for (uint32_t q = 0; q < nshards; ++q)
+      if (!errs[q].empty()) throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
+    if (out) *out = st[0];
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
   }
 }
 

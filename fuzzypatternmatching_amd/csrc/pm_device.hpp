@@ -76,11 +76,6 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t p, const OwnerArgs& oa) {
   return static_cast<uint32_t>(v % oa.nranks);
 }
 
-// Shard owning the vertex at position p of a sharded search (owner = id % G).
-__device__ __forceinline__ uint32_t perm_owner(const uint32_t* perm, uint32_t p, uint32_t G) {
-  return perm[p] % G;
-}
-
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
   const int lane = lane_id();
 #pragma unroll

@@ -65,6 +65,7 @@ struct Comm {
   // recv receives nshards consecutive `bytes` blocks, block g = shard g's send
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   virtual void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) = 0;
+  virtual void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) = 0;
   // all-to-all of variable blocks: block g of send (sbytes[g] bytes, blocks
   // consecutive) goes to shard g; recv holds the blocks from shards 0..G-1
   // consecutively (rbytes[g] from shard g).  Host byte counts, device buffers.
@@ -128,7 +129,17 @@ struct HSeg {
   uint32_t nseg;   // segments of the row
   uint32_t range;  // KRange index
   uint32_t tile;   // tile index (survivor mask slot)
+  uint32_t split;  // a delegate's share of a sharded search: TN / count stay partial (shard_hub_combine)
 };
+// A delegate (hub, degree >= -d) of a sharded search: its row is split over the
+// shards by target owner (delegate_partitioned_graph.ipp:1402-1648), its state
+// lives on the controller, hub ordinal % nshards (ipp:346-355).
+struct HubInfo {
+  uint32_t pos;   // position
+  uint32_t hidx;  // heavy scratch slot of this shard's share (kNoHub: no share here)
+  uint64_t moff;  // controller: first entry of its M row in the hub area of mcol
+};
+static constexpr uint32_t kNoHub = 0xFFFFFFFFu;
 static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
 static constexpr uint32_t kTileEntries = 64 * kSub; // 512
 static constexpr uint32_t kHeavyDeg = kTileEntries; // heavy rows: segments of this many entries
@@ -241,22 +252,38 @@ struct Ctx {
   uint64_t ss0_rows = 0;          // label-matching rows with degree > 0
   uint64_t ss0_trav_all = 0;      // ss0_trav summed over the shards
 
-  // sharding: shard `shard` of `nshards` owns the rows of ids v % nshards ==
-  // shard (superstep-0 scans, M rows, LCC updates, NLCC sources and every
-  // token / walk at such a vertex); T_pub is replicated and refreshed after
-  // every state change by an all-gather of the owned slist entries; NLCC
-  // tokens and TDS walks move to the owner of their next vertex after every
-  // position (shard_route: one all-to-all per position).
+  // sharding: shard `shard` of `nshards` owns the rows of
+  // ids v % nshards == shard (delegate rows: the entries whose target it owns)
+  // and runs superstep 0 and the first later superstep of the first LCC call
+  // over them; in between, the survivors' 2-bit T_pub codes are all-gathered
+  // (shard_codes_after_first).  After that superstep the state of S (T_pub,
+  // T_state, M rows) is all-gathered into a replica held by every shard
+  // (shard_replicate): the rest of the search -- later supersteps, NLC lines,
+  // later LCC calls -- runs on the replica exactly as on one GPU.
   uint32_t nshards = 1, shard = 0;
   Comm* comm = nullptr;
   Comm* comm_owned = nullptr;     // deleted with the context
   uint64_t mcap = 0;              // capacity (entries) of d_colp and d_mcol (nq; + kTileEntries tail padding)
-  uint32_t xmaxS = 0;             // max |slist| over shards (exchange block size)
-  std::vector<uint32_t> xnS;      // |slist| per shard
-  uint32_t* d_xslist = nullptr;   // nshards x xmaxS slist positions of every shard
-  uint32_t* d_xnS = nullptr;      // |slist| per shard (device)
-  uint16_t* d_xsend = nullptr;    // xmaxS T_pub values (packed)
-  uint16_t* d_xrecv = nullptr;    // nshards x xmaxS
+  bool replicated = false;        // the search state is the replica (sharded, after shard_replicate)
+  // delegates of a sharded search (hubs_host order; the shares are rows of this shard's layout)
+  bool split_hubs = false;        // nshards > 1 and some vertex has degree >= hub_threshold
+  uint64_t hub_area = 0;          // entries behind the dense region: M rows of the hubs this shard controls
+  HubInfo* d_hubinfo = nullptr;
+  std::vector<HubInfo> hubinfo;
+  uint64_t* d_moff = nullptr;     // M row starts before the replica: offp with the controlled hubs in the hub area
+  uint64_t* d_hubpart = nullptr;  // (count << 32 | TN) of this shard's shares, then G x H gathered
+  uint64_t* d_rmoff = nullptr;    // replica: M row start per position (V)
+  uint32_t* d_rmcol = nullptr;    // replica: M rows, packed
+  uint64_t rmcap = 0;             // entries of d_rmcol
+  bool xcode_wide = false;        // some label has more than two template vertices: the exchange carries T_pub
+  void* d_xsend = nullptr;        // exchange buffers (grown on demand)
+  void* d_xrecv = nullptr;
+  void* d_xent_send = nullptr;
+  void* d_xent_recv = nullptr;
+  size_t xsend_cap = 0, xrecv_cap = 0, xent_send_cap = 0, xent_recv_cap = 0;
+  uint64_t* d_xcnt = nullptr;     // per-shard counts of the exchanges (device, 4 x 64 words)
+  std::vector<uint64_t> xcode_n;  // records per shard of the last code exchange (u64-mode clear after superstep 1)
+  uint64_t xcode_max = 0;
   uint64_t* d_xred = nullptr;     // host-vector all-reduce staging
   size_t xred_cap = 0;
 
@@ -371,6 +398,12 @@ struct Ctx {
   std::string err;
 };
 
+// The M rows of the search state: the padded rows of the context's own layout,
+// or the replica's packed rows (sharded, after shard_replicate).
+inline const uint64_t* m_off(const Ctx& c) { return c.replicated ? c.d_rmoff : c.d_moff ? c.d_moff : c.d_offp; }
+inline uint32_t* m_col(const Ctx& c) { return c.replicated ? c.d_rmcol : c.d_mcol; }
+inline uint64_t m_cap(const Ctx& c) { return c.replicated ? c.rmcap : c.mcap; }
+
 // Kernel launchers (pm_kernels.hip).
 void launch_degree_labels(Ctx& c);
 // Label-major layout: sorts the vertices by (label, degree, id) and writes the
@@ -440,14 +473,17 @@ LineArgs make_line_args(const Ctx& c, const NlcLine& line);
 
 uint64_t* pinned(Ctx& c, size_t words);  // pinned host staging (pm_api.hip)
 
-// Shard exchanges (pm_shard.hip); no-ops when nshards == 1.
-void shard_after_first(Ctx& c);      // after superstep 0: slists of all shards + T_pub
-void shard_exchange_tpub(Ctx& c);    // T_pub of every shard's slist entries
+// Shard exchanges (pm_shard.hip); no-ops without a communicator.
+// after superstep 0 (sharded, delegates): the shares' TN / counts all-gathered and OR-ed / summed, the
+// shares' M entries sent to the controller (all-to-all), the controller verifies (slot: ss0 counters)
+void shard_hub_combine(Ctx& c, uint64_t* d_slot);
+void shard_codes_after_first(Ctx& c);  // after superstep 0: every shard's survivors' T_pub codes
+void shard_replicate(Ctx& c);          // the state of S of every shard -> the replica (collective)
 std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  // host vector, sum
-// Owner-bucketed all-to-all of n records of `words` u32 (destination: owner
-// of the position in word kw); returns the records received (arena memory).
-uint32_t* shard_route(Ctx& c, const uint32_t* items, uint64_t n, int words, int kw, uint64_t& nout);
-// Variable-size gather of a host u32 vector: every shard receives all blocks.
-std::vector<std::vector<uint32_t>> shard_allgatherv(Ctx& c, const std::vector<uint32_t>& v);
+// S rows of the current state (slist entries with T_pub != 0) packed on the device: per row
+// {position, T_pub | T_state << 16, |M|, first entry} (4 u32) and its alive M entries; counts[0..1] =
+// rows, entries (device).  rec / ent hold nS_host rows / the caller's entry bound.
+void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t* counts);
+uint64_t pack_state_entry_bound(Ctx& c);  // entries of the rows pack_state may write (host sync)
 
 }  // namespace pm

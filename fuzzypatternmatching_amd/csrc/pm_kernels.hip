@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <stdexcept>
+#include <unordered_map>
 
 #include "pm_device.hpp"
 #include "pm_internal.hpp"
@@ -711,7 +712,8 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
     if (TN) atomicOr(&h_tn[hs.h], static_cast<uint32_t>(TN));
     if (cnt) atomicAdd(&h_cnt[hs.h], cnt);
     __threadfence();
-    if (atomicAdd(&h_done[hs.h], 1u) == hs.nseg - 1) {
+    // (a delegate's share: its TN / count stay in the scratch for shard_hub_combine)
+    if (atomicAdd(&h_done[hs.h], 1u) == hs.nseg - 1 && !hs.split) {
       __threadfence();
       const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
       const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
@@ -1322,12 +1324,26 @@ __host__ __device__ inline uint32_t degree_class(uint64_t d) {
   return 1 + light_kind(d);
 }
 
+// hub_thr (sharded searches with delegates): a delegate's share is a heavy row on every shard
+// whatever its length there, so every delegate sorts into the heavy class
 __global__ void k_class_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ ids, uint64_t n,
-                             uint32_t* __restrict__ key) {
+                             uint64_t hub_thr, uint32_t* __restrict__ key) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = ids[i];
-    key[i] = degree_class(off[u + 1] - off[u]);
+    const uint64_t d = off[u + 1] - off[u];
+    key[i] = d >= hub_thr ? kHeavyKind + 1 : degree_class(d);
   }
+}
+
+__global__ void k_gather_pos(const uint32_t* __restrict__ pos, const uint64_t* __restrict__ ids, uint64_t n,
+                             uint32_t* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    out[i] = pos[ids[i]];
+}
+
+__global__ void k_patch_moff(const HubInfo* __restrict__ info, uint32_t nh, uint64_t* __restrict__ moff) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nh; j += gridDim.x * blockDim.x)
+    if (info[j].moff != ~0ull) moff[info[j].pos] = info[j].moff;
 }
 
 void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst) {
@@ -1364,7 +1380,8 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
       hipLaunchKernelGGL(k_owner_keys, dim3(g), dim3(kBlock), 0, c.stream, ids2, n, c.nshards, dkey);
       PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids2, ids, size_t(n), 0,
                                                       obits, c.stream));
-      hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, ids, n, dkey);
+      hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, ids, n,
+                         c.split_hubs ? c.hub_threshold : ~0ull, dkey);
       PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 6,
                                                       c.stream));
     }
@@ -1418,7 +1435,10 @@ void build_tiling(Ctx& c) {
   static constexpr int kLB = kHeavyKind + 3;
   const uint64_t n = c.n;
   auto lab_at = [&](uint64_t i) { return c.labels_host[c.perm_host[i]]; };
-  auto cls_at = [&](uint64_t i) { return degree_class(c.row_degree(c.perm_host[i])); };
+  auto cls_at = [&](uint64_t i) {
+    const uint64_t d = c.row_degree(c.perm_host[i]);
+    return c.split_hubs && d >= c.hub_threshold ? static_cast<uint32_t>(kHeavyKind + 1) : degree_class(d);
+  };
   auto first_where = [](uint64_t lo, uint64_t hi, auto&& pred) {  // first i in [lo, hi) with pred(i)
     while (lo < hi) {
       const uint64_t m = (lo + hi) >> 1;
@@ -1435,9 +1455,10 @@ void build_tiling(Ctx& c) {
     for (uint32_t k = 0; k <= static_cast<uint32_t>(kHeavyKind); ++k)
       B[1 + k] = first_where(B[0], B[kLB - 1], [&](uint64_t i) { return cls_at(i) >= 1 + k; });
   }
-  // this shard's sub-run of [a, b) (positions are owner-sorted inside a run)
-  auto owned = [&](uint64_t a, uint64_t b) {
-    if (c.nshards <= 1) return std::make_pair(a, b);
+  // this shard's sub-run of [a, b) (positions are owner-sorted inside a run); the heavy run whole when
+  // delegates are split (any shard may hold a delegate's share; other rows of the run are empty here)
+  auto owned = [&](uint64_t a, uint64_t b, bool heavy) {
+    if (c.nshards <= 1 || (heavy && c.split_hubs)) return std::make_pair(a, b);
     const uint32_t G = c.nshards, me = c.shard;
     const uint64_t x = first_where(a, b, [&](uint64_t i) { return c.perm_host[i] % G >= me; });
     const uint64_t y = first_where(x, b, [&](uint64_t i) { return c.perm_host[i] % G > me; });
@@ -1460,6 +1481,35 @@ void build_tiling(Ctx& c) {
   uint32_t tiles = 0, nheavy = 0;
   c.ss0_trav = 0;
   c.ss0_rows = 0;
+  // delegates of a sharded search: positions, and the hub area of the ones this shard controls
+  std::unordered_map<uint64_t, uint32_t> hub_at;  // position -> hub ordinal
+  c.hubinfo.clear();
+  if (c.split_hubs) {
+    const uint64_t H = c.hubs_host.size();
+    std::vector<uint32_t> hp(H);
+    uint64_t* d_ids = nullptr;
+    uint32_t* d_hp = nullptr;
+    PM_HIP_CHECK(hipMalloc(&d_ids, H * sizeof(uint64_t)));
+    PM_HIP_CHECK(hipMalloc(&d_hp, H * sizeof(uint32_t)));
+    PM_HIP_CHECK(hipMemcpy(d_ids, c.hubs_host.data(), H * sizeof(uint64_t), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_gather_pos, dim3(grid_for(H, kBlock, 1024)), dim3(kBlock), 0, c.stream, c.d_pos, d_ids, H,
+                       d_hp);
+    PM_HIP_CHECK(hipMemcpyAsync(hp.data(), d_hp, H * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    (void)hipFree(d_ids);
+    (void)hipFree(d_hp);
+    uint64_t area = c.dbase + c.dcap;  // the hub area follows the dense region in mcol
+    for (uint64_t j = 0; j < H; ++j) {
+      HubInfo hi{hp[j], kNoHub, ~0ull};
+      if (j % c.nshards == c.shard) {
+        hi.moff = area;
+        area += c.deg_host[c.hubs_host[j]];
+      }
+      c.hubinfo.push_back(hi);
+      hub_at[hp[j]] = static_cast<uint32_t>(j);
+    }
+    if (area > c.dbase + c.dcap + c.hub_area) throw std::runtime_error("internal: hub area overflow");
+  }
   for (int l = 0; l < nl; ++l) {
     const uint64_t* B = bounds.data() + l * kLB;
     const uint16_t tu = tus[l];
@@ -1476,10 +1526,10 @@ void build_tiling(Ctx& c) {
     if (c.symmetric) c.ss0_trav += dev_at(c.d_offr, hi) - dev_at(c.d_offr, first_nz);
     // kind k = [B[1+k], B[2+k]) for k < kHeavyKind (light class k); kHeavyKind = [B[1+kHeavyKind], hi)
     for (int kind = 0; kind <= kHeavyKind; ++kind) {
-      const auto ab = owned(B[1 + kind], kind == kHeavyKind ? hi : B[2 + kind]);
+      const auto ab = owned(B[1 + kind], kind == kHeavyKind ? hi : B[2 + kind], kind == kHeavyKind);
       const uint64_t a = ab.first, b = ab.second;
       if (b <= a) continue;
-      c.ss0_rows += b - a;
+      if (kind < kHeavyKind) c.ss0_rows += b - a;  // heavy rows: those with entries here (below)
       if (!nm) continue;  // such rows never enter S (TN = 0): scanned by no kernel, counted above
       KRange R{};
       R.tile0 = tiles;
@@ -1537,10 +1587,16 @@ void build_tiling(Ctx& c) {
         PM_HIP_CHECK(hipMemcpy(o.data(), c.d_offp + a, o.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
         for (uint64_t i = a; i < b; ++i) {
           const uint64_t deg = o[i - a + 1] - o[i - a];
+          if (!deg) continue;  // (sharded: another shard's row)
+          ++c.ss0_rows;
           const uint32_t ns = static_cast<uint32_t>((deg + kHeavyDeg - 1) / kHeavyDeg);
+          auto hj = hub_at.find(i);
+          const uint32_t split = hj != hub_at.end() ? 1u : 0u;
+          if (split) c.hubinfo[hj->second].hidx = nheavy;
           for (uint32_t sgm = 0; sgm < ns; ++sgm) {
             const uint32_t tile = tiles + static_cast<uint32_t>(hs.size() - R.aux);
-            hs.push_back(HSeg{static_cast<uint32_t>(i), sgm, nheavy, ns, static_cast<uint32_t>(tab.size()), tile});
+            hs.push_back(
+                HSeg{static_cast<uint32_t>(i), sgm, nheavy, ns, static_cast<uint32_t>(tab.size()), tile, split});
           }
           ++nheavy;
         }
@@ -1595,6 +1651,25 @@ void build_tiling(Ctx& c) {
   c.scan_tmp_bytes = slist_scan_tmp_bytes(std::max<uint64_t>(1, tiles));
   PM_HIP_CHECK(hipMalloc(&c.d_scan_tmp, std::max<size_t>(1, c.scan_tmp_bytes)));
   c.k1_grid = lcc_first_grid(c);
+  if (c.d_hubinfo) (void)hipFree(c.d_hubinfo);
+  if (c.d_moff) (void)hipFree(c.d_moff);
+  if (c.d_hubpart) (void)hipFree(c.d_hubpart);
+  c.d_hubinfo = nullptr;
+  c.d_moff = nullptr;
+  c.d_hubpart = nullptr;
+  if (c.split_hubs) {
+    const uint64_t H = c.hubinfo.size();
+    PM_HIP_CHECK(hipMalloc(&c.d_hubinfo, H * sizeof(HubInfo)));
+    PM_HIP_CHECK(hipMemcpy(c.d_hubinfo, c.hubinfo.data(), H * sizeof(HubInfo), hipMemcpyHostToDevice));
+    PM_HIP_CHECK(hipMalloc(&c.d_hubpart, (uint64_t(c.nshards) + 1) * H * sizeof(uint64_t)));
+    // M row starts until the replica: the layout's, with the controlled delegates in the hub area
+    PM_HIP_CHECK(hipMalloc(&c.d_moff, (c.n + 1) * sizeof(uint64_t)));
+    PM_HIP_CHECK(hipMemcpyAsync(c.d_moff, c.d_offp, (c.n + 1) * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
+    hipLaunchKernelGGL(k_patch_moff, dim3(grid_for(H, kBlock, 1024)), dim3(kBlock), 0, c.stream, c.d_hubinfo,
+                       static_cast<uint32_t>(H), c.d_moff);
+    PM_HIP_CHECK(hipGetLastError());
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  }
 }
 
 static K1Out k1_out(Ctx& c, unsigned grid) {
@@ -1645,10 +1720,10 @@ unsigned lcc_first_grid(const Ctx& c) {
 }
 
 // Dense M when the next superstep is the pull-form k_lcc_step of this call
-// (first call on one shard of a symmetric graph, diameter >= 2); PM_DENSE_M=0 disables it.
+// (first call on a symmetric graph, diameter >= 2); PM_DENSE_M=0 disables it.
 void lcc_first_set_dense(Ctx& c) {
   static const bool dense_env = !std::getenv("PM_DENSE_M") || std::string(std::getenv("PM_DENSE_M")) != "0";
-  c.k1_dense = dense_env && c.dcap && !c.comm && c.symmetric && c.pattern.graph.diameter >= 2;
+  c.k1_dense = dense_env && c.dcap && c.symmetric && c.pattern.graph.diameter >= 2;
 }
 
 void lcc_first_prepare(Ctx& c) {
@@ -1698,11 +1773,11 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
   }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
   const unsigned grid = grid_for(c.nS_host, kBlock, 8192);
-  hipLaunchKernelGGL(k_lcc_push_send, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS,
-                     c.d_tpub[c.cur], c.pa, c.d_perm, c.d_mcol, c.d_mlen, c.d_malive, c.d_tn,
+  hipLaunchKernelGGL(k_lcc_push_send, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS,
+                     c.d_tpub[c.cur], c.pa, c.d_perm, m_col(c), c.d_mlen, c.d_malive, c.d_tn,
                      reinterpret_cast<unsigned long long*>(d_slot + 2 * P));
-  hipLaunchKernelGGL(k_lcc_push_verify, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS,
-                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
+  hipLaunchKernelGGL(k_lcc_push_verify, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS,
+                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, c.d_tn, partials(c, d_slot));
   PM_HIP_CHECK(hipGetLastError());
   c.cur ^= 1;
@@ -1719,9 +1794,9 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   const unsigned long long* min = c.smask_valid ? reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur])
                                                 : nullptr;
   auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
-  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, c.d_offp, c.d_slist, c.d_nS, min, mout,
-                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), c.d_mcol, c.d_mlen,
-                     c.d_malive, partials(c, d_slot), first_after_ss0 && !c.comm ? c.d_tcode : nullptr, c.lr,
+  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
+                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
+                     c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                      c.diag_step, first_after_ss0 && c.k1_dense ? c.d_dmoff : nullptr, c.dbase);
   PM_HIP_CHECK(hipGetLastError());
   c.k1_dense = false;  // every M row of S is in its padded row from here on
@@ -1831,12 +1906,6 @@ void launch_clear_tpub(Ctx& c) {
   if (c.nS_host)
     hipLaunchKernelGGL(k_clear_tpub, dim3(grid_for(c.nS_host, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_slist,
                        c.d_nS, uint64_t(c.nS_host), c.d_tpub[0], c.d_tpub[1]);
-  if (c.comm && c.d_xslist)  // the other shards' entries (replicated T_pub)
-    for (uint32_t g = 0; g < c.nshards; ++g)
-      if (g != c.shard && c.xnS[g])
-        hipLaunchKernelGGL(k_clear_tpub, dim3(grid_for(c.xnS[g], kBlock, 4096)), dim3(kBlock), 0, c.stream,
-                           c.d_xslist + uint64_t(g) * c.xmaxS, c.d_xnS + g, uint64_t(c.xnS[g]), c.d_tpub[0],
-                           c.d_tpub[1]);
   PM_HIP_CHECK(hipGetLastError());
 }
 
@@ -2029,37 +2098,20 @@ __global__ void k_tp_expand_write(const unsigned long long* __restrict__ fk, con
 
 // Terminal position C+1 (nem_1.hpp:661-791): path -> ack the source when the
 // walk does not end on it; cycle -> mark the source and the closing edge.
-// Acknowledgement of source s (tsm[s] = 2).  Sharded: a source owned by
-// another shard is appended to `acks` instead (routed to its owner after the
-// terminal step).
-struct AckSink {
-  const uint32_t* perm;
-  uint32_t G, me;
-  uint32_t* acks;
-  unsigned long long* nacks;
-};
-__device__ __forceinline__ void ack_source(uint32_t s, uint8_t* tsm, const AckSink& a) {
-  if (a.G > 1 && perm_owner(a.perm, s, a.G) != a.me) {
-    a.acks[atomicAdd(a.nacks, 1ull)] = s;
-  } else {
-    tsm[s] = 2;
-  }
-}
-
 __global__ void k_tp_terminal(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts,
                               const uint32_t* __restrict__ tp, uint64_t ntok, LineArgs la,
                               const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
                               uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen,
-                              const uint32_t* __restrict__ perm, uint8_t* __restrict__ tsm, AckSink ak) {
+                              const uint32_t* __restrict__ perm, uint8_t* __restrict__ tsm) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntok; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = tu[i], s = ts[i];
     if (!pos_ok(tpub[u], la.C + 1, la)) continue;
     if (!la.VC) {
       if (u == s) continue;
-      if (tpub[s]) ack_source(s, tsm, ak);  // ack visitor needs an active source (nem_1.hpp:101, :326-336)
+      if (tpub[s]) tsm[s] = 2;  // ack visitor needs an active source (nem_1.hpp:101, :326-336)
     } else {
       if (u != s) continue;
-      tsm[s] = 2;  // u == s: this shard owns s
+      tsm[s] = 2;
       // mark M[s][parent]: rows hold positions in neighbour-id order
       const uint32_t p = tp[i], pid = perm[p];
       uint64_t lo = offp[s], hi = offp[s] + mlen[s];
@@ -2089,29 +2141,6 @@ __global__ void k_tp_terminal_sv(const uint32_t* __restrict__ tu, const uint32_t
     bool found = false;
     for (int l = 0; l < seen.count && !found; ++l) found = sorted_contains(seen.keys[l], seen.n[l], key);
     if (found) tsm[u] = 2;
-  }
-}
-
-__global__ void k_set_acked(const uint32_t* __restrict__ acks, uint64_t n, uint8_t* __restrict__ tsm) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
-    tsm[acks[i]] = 2;
-}
-
-// Tokens (u, s, p) between the three-array form and interleaved records.
-__global__ void k_tok_pack(const uint32_t* __restrict__ tu, const uint32_t* __restrict__ ts,
-                           const uint32_t* __restrict__ tp, uint64_t n, uint32_t* __restrict__ out) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-    out[3 * i] = tu[i];
-    out[3 * i + 1] = ts[i];
-    out[3 * i + 2] = tp[i];
-  }
-}
-__global__ void k_tok_unpack(const uint32_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ tu,
-                             uint32_t* __restrict__ ts, uint32_t* __restrict__ tp) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-    tu[i] = in[3 * i];
-    ts[i] = in[3 * i + 1];
-    tp[i] = in[3 * i + 2];
   }
 }
 
@@ -2181,7 +2210,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
 // Terminal position C+1 (tds_batch_1.hpp:641-758).
 __global__ void k_tds_terminal(const uint32_t* __restrict__ win, uint64_t nw, int stride, LineArgs la,
                                const uint16_t* __restrict__ tpub, uint8_t* __restrict__ tsm,
-                               uint8_t* __restrict__ keep, AckSink ak) {
+                               uint8_t* __restrict__ keep) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nw; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t* w = win + i * stride;
     const int k = la.C + 1;
@@ -2191,7 +2220,7 @@ __global__ void k_tds_terminal(const uint32_t* __restrict__ win, uint64_t nw, in
       if (!la.VC) {
         if (u != s) {
           kp = 1;
-          if (tpub[s]) ack_source(s, tsm, ak);
+          if (tpub[s]) tsm[s] = 2;
         }
       } else if (u == s) {
         kp = 1;
@@ -2358,54 +2387,9 @@ static void pseen_end(Ctx& c, const SeenSet& seen) {
   c.npseen = static_cast<uint64_t>(n);
 }
 
-// Sharded searches: tokens and walks travel to the shard owning their next
-// vertex after every position (shard_route: one all-to-all per position, the
-// BSP form of the visitor queue's mailbox), so that the (vertex, source)
-// dedup, M[u] and the terminal checks are always local; acknowledgements of
-// another shard's source travel to its owner after the terminal step.
-static void route_tokens(Ctx& c, uint32_t*& tu, uint32_t*& ts, uint32_t*& tp, uint64_t& ntok) {
-  if (!c.comm) return;
-  auto* rec = arena_alloc<uint32_t>(c, std::max<uint64_t>(ntok, 1) * 3);
-  if (ntok)
-    hipLaunchKernelGGL(k_tok_pack, dim3(grid_for(ntok, kBlock, 4096)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
-                       rec);
-  uint64_t nr = 0;
-  const uint32_t* got = shard_route(c, rec, ntok, 3, 0, nr);
-  tu = arena_alloc<uint32_t>(c, std::max<uint64_t>(nr, 1));
-  ts = arena_alloc<uint32_t>(c, std::max<uint64_t>(nr, 1));
-  tp = arena_alloc<uint32_t>(c, std::max<uint64_t>(nr, 1));
-  if (nr)
-    hipLaunchKernelGGL(k_tok_unpack, dim3(grid_for(nr, kBlock, 4096)), dim3(kBlock), 0, c.stream, got, nr, tu, ts, tp);
-  PM_HIP_CHECK(hipGetLastError());
-  ntok = nr;
-}
-
-static AckSink ack_sink(Ctx& c, uint64_t cap) {
-  AckSink a{c.d_perm, c.comm ? c.nshards : 1u, c.shard, nullptr, nullptr};
-  if (c.comm) {
-    a.nacks = arena_alloc<unsigned long long>(c, 1);
-    a.acks = arena_alloc<uint32_t>(c, cap);
-    PM_HIP_CHECK(hipMemsetAsync(a.nacks, 0, sizeof(unsigned long long), c.stream));
-  }
-  return a;
-}
-
-static void route_acks(Ctx& c, const AckSink& a) {
-  if (!c.comm) return;
-  unsigned long long n = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(&n, a.nacks, sizeof(n), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  uint64_t nr = 0;
-  const uint32_t* got = shard_route(c, a.acks, n, 1, 0, nr);
-  if (nr)
-    hipLaunchKernelGGL(k_set_acked, dim3(grid_for(nr, kBlock, 4096)), dim3(kBlock), 0, c.stream, got, nr, c.d_tsm);
-  PM_HIP_CHECK(hipGetLastError());
-}
-
 TpResult run_path_line(Ctx& c, const NlcLine& line) {
   TpResult res;
   c.arena.reset();
-  const bool sharded = c.comm != nullptr;
   const LineArgs la = make_line_args(c, line);
   auto* d_trav = arena_alloc<unsigned long long>(c, 1);
   PM_HIP_CHECK(hipMemsetAsync(d_trav, 0, sizeof(unsigned long long), c.stream));
@@ -2422,7 +2406,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   uint64_t ninit = 0;
   ensure_sources(c, la, 0, line, &init, &ninit);
   res.sources = c.nsources;
-  if (ninit == 0 && !sharded) {
+  if (ninit == 0) {
     pseen_end(c, seen);
     return res;
   }
@@ -2431,24 +2415,18 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   auto* cnt = arena_alloc<uint32_t>(c, ninit);
   auto* obase = arena_alloc<uint64_t>(c, ninit + 1);
   hipLaunchKernelGGL(k_row_alive, dim3(grid_for(ninit, kBlock, 4096)), dim3(kBlock), 0, c.stream, init, ninit, 1, 0,
-                     c.d_offp, c.d_malive, cnt);
+                     m_off(c), c.d_malive, cnt);
   uint64_t ntok = exclusive_scan_u32_to_u64(c, cnt, obase, ninit);
   uint64_t trav_init = ntok;  // sources scan all of M[s]
   auto* tu = arena_alloc<uint32_t>(c, ntok);
   auto* ts = arena_alloc<uint32_t>(c, ntok);
   auto* tp = arena_alloc<uint32_t>(c, ntok);
   hipLaunchKernelGGL(k_tp_init, dim3(grid_for(ninit, kBlock, 4096)), dim3(kBlock), 0, c.stream, init, ninit, obase,
-                     c.d_offp, c.d_mcol, c.d_mlen, tu, ts, tp);
+                     m_off(c), m_col(c), c.d_mlen, tu, ts, tp);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += ntok;
-  route_tokens(c, tu, ts, tp, ntok);
   const int C = la.C;
-  // sharded: every shard runs every position (the token exchange is collective)
-  for (int k = 1; k <= C && (ntok > 0 || sharded); ++k) {
-    if (ntok == 0) {  // sharded, nothing here at this position: take part in the exchange
-      route_tokens(c, tu, ts, tp, ntok);
-      continue;
-    }
+  for (int k = 1; k <= C && ntok > 0; ++k) {
     auto* keys = arena_alloc<unsigned long long>(c, ntok);
     hipLaunchKernelGGL(k_tp_filter, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, ntok, k,
                        la, tpub, keys);
@@ -2484,36 +2462,31 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
     }
     if (nf == 0) {
       ntok = 0;
-      if (!sharded) break;
-      route_tokens(c, tu, ts, tp, ntok);
-      continue;
+      break;
     }
     auto* ecnt = arena_alloc<uint32_t>(c, nf);
     hipLaunchKernelGGL(k_tp_expand_count, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf,
-                       c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, ecnt, d_trav);
+                       m_off(c), m_col(c), c.d_mlen, c.d_malive, ecnt, d_trav);
     auto* eb = arena_alloc<uint64_t>(c, nf + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, ecnt, eb, nf);
     tu = arena_alloc<uint32_t>(c, nnext);
     ts = arena_alloc<uint32_t>(c, nnext);
     tp = arena_alloc<uint32_t>(c, nnext);
     hipLaunchKernelGGL(k_tp_expand_write, dim3(grid_for(nf, kBlock, 1024)), dim3(kBlock), 0, c.stream, fk, fx, nf, eb,
-                       c.d_offp, c.d_mcol, c.d_mlen, tu, ts, tp);
+                       m_off(c), m_col(c), c.d_mlen, tu, ts, tp);
     PM_HIP_CHECK(hipGetLastError());
     ntok = nnext;
     res.tokens += ntok;
-    route_tokens(c, tu, ts, tp, ntok);  // to the owners of the next vertices
   }
-  AckSink ak = ack_sink(c, std::max<uint64_t>(ntok, 1));
-  if (ntok > 0 && la.sv) {  // the terminal vertex is verified here (tokens were routed to its owner)
+  if (ntok > 0 && la.sv) {  // the terminal vertex is verified here
     hipLaunchKernelGGL(k_tp_terminal_sv, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, ntok,
                        la, tpub, c.d_perm, c.d_tsm, seen);
     PM_HIP_CHECK(hipGetLastError());
   } else if (ntok > 0) {
     hipLaunchKernelGGL(k_tp_terminal, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, tp, ntok,
-                       la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_perm, c.d_tsm, ak);
+                       la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_perm, c.d_tsm);
     PM_HIP_CHECK(hipGetLastError());
   }
-  route_acks(c, ak);
   pseen_end(c, seen);
   unsigned long long trav = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&trav, d_trav, sizeof(trav), hipMemcpyDeviceToHost, c.stream));
@@ -2537,48 +2510,40 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   c.npseen = 0;  // token-source sets are dropped at the start of a non-selected line (beta.cpp:791-793)
   ensure_sources(c, la, 1, line);
   res.sources = c.nsources;
-  const bool sharded = c.comm != nullptr;
-  if (c.nsources == 0 && !sharded) return res;
+  if (c.nsources == 0) return res;
   const uint16_t* tpub = c.d_tpub[c.cur];
   auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
   auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
   hipLaunchKernelGGL(k_row_alive, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, 1, 0, c.d_offp, c.d_malive, cnt);
+                     c.nsources, 1, 0, m_off(c), c.d_malive, cnt);
   uint64_t nw = exclusive_scan_u32_to_u64(c, cnt, obase, c.nsources);
   const uint64_t trav_init = nw;
   auto* walks = arena_alloc<uint32_t>(c, nw * stride);
   hipLaunchKernelGGL(k_tds_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, c.d_offp, c.d_mcol, c.d_mlen, stride, walks);
+                     c.nsources, obase, m_off(c), m_col(c), c.d_mlen, stride, walks);
   PM_HIP_CHECK(hipGetLastError());
   res.tokens += nw;
-  if (sharded) walks = shard_route(c, walks, nw, stride, 1, nw);  // to the owners of the walks' last vertices
-  for (int k = 1; k <= C && (nw > 0 || sharded); ++k) {
-    if (nw == 0) {
-      walks = shard_route(c, walks, 0, stride, k + 1, nw);
-      continue;
-    }
+  for (int k = 1; k <= C && nw > 0; ++k) {
     auto* wc = arena_alloc<uint32_t>(c, nw);
     hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                       stride, la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, wc,
+                       stride, la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_malive, wc,
                        static_cast<const uint64_t*>(nullptr), static_cast<uint32_t*>(nullptr), d_trav);
     auto* wb = arena_alloc<uint64_t>(c, nw + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
     auto* wn = arena_alloc<uint32_t>(c, nnext * stride);
     if (nnext) {
       hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                         stride, la, tpub, c.d_offp, c.d_mcol, c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
+                         stride, la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
       PM_HIP_CHECK(hipGetLastError());
     }
     walks = wn;
     nw = nnext;
     res.tokens += nw;
-    if (sharded) walks = shard_route(c, walks, nw, stride, k + 1, nw);
   }
-  AckSink ak = ack_sink(c, std::max<uint64_t>(nw, 1));
   if (nw > 0) {
     auto* keep = arena_alloc<uint8_t>(c, nw);
     hipLaunchKernelGGL(k_tds_terminal, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, stride,
-                       la, tpub, c.d_tsm, keep, ak);
+                       la, tpub, c.d_tsm, keep);
     PM_HIP_CHECK(hipGetLastError());
     std::vector<uint32_t> all(nw * stride);
     std::vector<uint8_t> kp(nw);
@@ -2588,7 +2553,6 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
     for (uint64_t i = 0; i < nw; ++i)
       if (kp[i]) walks_out.insert(walks_out.end(), all.begin() + i * stride, all.begin() + (i + 1) * stride);
   }
-  route_acks(c, ak);
   res.walks = walks_out.size() / stride;
   unsigned long long trav = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&trav, d_trav, sizeof(trav), hipMemcpyDeviceToHost, c.stream));

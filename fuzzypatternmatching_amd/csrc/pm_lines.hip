@@ -817,7 +817,7 @@ static void upload_lines(Ctx& c) {
 // Enqueues lines [pl0, nl) and the read-back of their results into the lines'
 // pinned buffer; returns nl (pl0 >= nl: nothing launched).
 static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept_out) {
-  if (c.comm) throw std::runtime_error("internal: fused lines run on one shard only");
+  if (c.comm && !c.replicated) throw std::runtime_error("internal: fused lines before the sharded state was replicated");
   c.probe("lines entry");
   const size_t nl_all = c.pattern.lines.size();
   const size_t nl = pl0 < nl_all && max_lines < nl_all - pl0 ? pl0 + max_lines : nl_all;
@@ -852,8 +852,8 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   PM_HIP_CHECK(hipMemsetAsync(c.d_lstats + pl0, 0, (nl - pl0) * sizeof(LineStats), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(d_done, 0, 64 * sizeof(unsigned), c.stream));
   LineKernelArgs a{};
-  a.offp = c.d_offp;
-  a.mcol = c.d_mcol;
+  a.offp = m_off(c);
+  a.mcol = m_col(c);
   a.mlen = c.d_mlen;
   a.malive = c.d_malive;
   a.tpub = c.d_tpub[c.cur];

@@ -279,6 +279,41 @@ struct DevBuf {
   }
 };
 
+// Sharded build: out-degree of every source (the keys hold both directions of every pair).
+__global__ void k_key_degrees(const uint64_t* __restrict__ keys, uint64_t n, int S, uint32_t* __restrict__ deg) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    atomicAdd(&deg[keys[i] >> S], 1u);
+}
+
+// Owner of a directed entry (delegate_partitioned_graph.ipp:818-969 low-degree rows by source,
+// :1402-1648 delegate rows by target).
+__device__ __forceinline__ uint32_t entry_owner(uint64_t key, int S, const uint32_t* deg, uint64_t thr, uint32_t G) {
+  const uint64_t u = key >> S, v = key & ((1ull << S) - 1);
+  return static_cast<uint32_t>((deg[u] >= thr ? v : u) % G);
+}
+
+__global__ void k_owner_count(const uint64_t* __restrict__ keys, uint64_t n, int S, const uint32_t* __restrict__ deg,
+                              uint64_t thr, uint32_t G, unsigned long long* __restrict__ cnt) {
+  __shared__ unsigned long long s_cnt[64];
+  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) s_cnt[g] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    atomicAdd(&s_cnt[entry_owner(keys[i], S, deg, thr, G)], 1ull);
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x)
+    if (s_cnt[g]) atomicAdd(&cnt[g], s_cnt[g]);
+}
+
+// Entries into their owner's block (order inside a block is free: the receiver sorts).
+__global__ void k_owner_scatter(const uint64_t* __restrict__ keys, uint64_t n, int S, const uint32_t* __restrict__ deg,
+                                uint64_t thr, uint32_t G, unsigned long long* __restrict__ cursor,
+                                uint64_t* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t k = keys[i];
+    out[atomicAdd(&cursor[entry_owner(k, S, deg, thr, G)], 1ull)] = k;
+  }
+}
+
 }  // namespace
 
 RmatPlan rmat_plan(uint64_t scale, uint64_t p_gen) {
@@ -332,6 +367,98 @@ void rmat_keys_device(const RmatPlan& p, const std::vector<uint64_t>& vranks, ui
                      p.per_rank, p.esub, static_cast<int>(p.scale), ring, d_keys);
   PM_HIP_CHECK(hipGetLastError());
   PM_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+// Sorted keys (2 * scale bits) -> device CSR of n = 2^scale rows; frees the key buffers.
+static DevCsr csr_from_unsorted(uint64_t scale, DevBuf& ka, DevBuf& kb, uint64_t nkeys, hipStream_t stream) {
+  DevCsr g;
+  g.n = uint64_t(1) << scale;
+  g.nnz = nkeys;
+  uint64_t* a = static_cast<uint64_t*>(ka.p);
+  uint64_t* b = static_cast<uint64_t*>(kb.p);
+  DevBuf tmp;
+  rocprim::double_buffer<uint64_t> db(a, b);
+  size_t tb = 0;
+  PM_HIP_CHECK(rocprim::radix_sort_keys(nullptr, tb, db, nkeys, 0u, static_cast<unsigned>(2 * scale), stream));
+  void* d_tmp = tmp.alloc<char>(tb);
+  PM_HIP_CHECK(rocprim::radix_sort_keys(d_tmp, tb, db, nkeys, 0u, static_cast<unsigned>(2 * scale), stream));
+  PM_HIP_CHECK(hipStreamSynchronize(stream));
+  tmp.reset();
+  const uint64_t* sorted = db.current();
+  if (sorted == a) kb.reset(); else ka.reset();
+  PM_HIP_CHECK(hipMalloc(&g.d_off, (g.n + 1) * sizeof(uint64_t)));
+  PM_HIP_CHECK(hipMalloc(&g.d_col, std::max<uint64_t>(nkeys, 1) * sizeof(uint32_t)));
+  if (nkeys) {
+    hipLaunchKernelGGL(k_csr_from_keys, dim3(grid_of(nkeys, 256, 1u << 20)), dim3(256), 0, stream, sorted, nkeys,
+                       static_cast<int>(scale), g.n, g.d_off, g.d_col);
+  } else {
+    hipLaunchKernelGGL(k_fill_u64, dim3(grid_of(g.n + 1, 256, 8192)), dim3(256), 0, stream, g.d_off, g.n + 1, 0ull);
+  }
+  PM_HIP_CHECK(hipGetLastError());
+  PM_HIP_CHECK(hipStreamSynchronize(stream));
+  ka.reset();
+  kb.reset();
+  return g;
+}
+
+DevCsr rmat_shard_device(uint64_t scale, uint64_t p_gen, uint64_t hub_threshold, Comm& comm, uint32_t nshards,
+                         uint32_t shard, std::vector<uint32_t>& gdeg, hipStream_t stream) {
+  if (nshards == 0 || nshards > 64 || shard >= nshards) throw std::runtime_error("rmat shard: 1..64 shards");
+  const RmatPlan p = rmat_plan(scale, p_gen);
+  std::vector<uint64_t> mine;
+  for (uint64_t r = shard; r < p_gen; r += nshards) mine.push_back(r);
+  const uint64_t nkeys = 2 * p.per_rank * mine.size();
+  const uint64_t n = uint64_t(1) << scale;
+  const int S = static_cast<int>(scale);
+  DevBuf ka, kb, bdeg, bcnt;
+  uint64_t* a = ka.alloc<uint64_t>(nkeys);
+  rmat_keys_device(p, mine, a, stream);
+  // global degrees (delegates are decided on them): a histogram of the sources, summed over the shards
+  uint32_t* deg = bdeg.alloc<uint32_t>(n);
+  PM_HIP_CHECK(hipMemsetAsync(deg, 0, n * sizeof(uint32_t), stream));
+  if (nkeys)
+    hipLaunchKernelGGL(k_key_degrees, dim3(grid_of(nkeys, 256, 1u << 16)), dim3(256), 0, stream, a, nkeys, S, deg);
+  comm.allreduce_sum_u32(deg, n, stream);
+  gdeg.resize(n);
+  PM_HIP_CHECK(hipMemcpyAsync(gdeg.data(), deg, n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  PM_HIP_CHECK(hipStreamSynchronize(stream));
+  uint64_t nrecv = nkeys;
+  if (nshards > 1) {
+    // owners' blocks: counts, the G x G count matrix, then one all-to-all of the 8-B entries
+    const uint32_t G = nshards;
+    auto* cnt = bcnt.alloc<unsigned long long>(2 * G + uint64_t(G) * G);
+    PM_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * G * sizeof(unsigned long long), stream));
+    if (nkeys)
+      hipLaunchKernelGGL(k_owner_count, dim3(grid_of(nkeys, 256, 4096)), dim3(256), 0, stream, a, nkeys, S, deg,
+                         hub_threshold, G, cnt);
+    comm.allgather(cnt, cnt + 2 * G, G * sizeof(uint64_t), stream);
+    std::vector<uint64_t> m(uint64_t(G) * G);
+    PM_HIP_CHECK(hipMemcpyAsync(m.data(), cnt + 2 * G, m.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+    PM_HIP_CHECK(hipStreamSynchronize(stream));
+    std::vector<uint64_t> sb(G), rb(G), cur(G, 0);
+    nrecv = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+      sb[g] = m[uint64_t(shard) * G + g] * sizeof(uint64_t);
+      rb[g] = m[uint64_t(g) * G + shard] * sizeof(uint64_t);
+      nrecv += m[uint64_t(g) * G + shard];
+      if (g) cur[g] = cur[g - 1] + m[uint64_t(shard) * G + g - 1];
+    }
+    uint64_t* send = kb.alloc<uint64_t>(nkeys);
+    PM_HIP_CHECK(hipMemcpyAsync(cnt + G, cur.data(), G * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+    if (nkeys)
+      hipLaunchKernelGGL(k_owner_scatter, dim3(grid_of(nkeys, 256, 1u << 16)), dim3(256), 0, stream, a, nkeys, S,
+                         deg, hub_threshold, G, cnt + G, send);
+    PM_HIP_CHECK(hipGetLastError());
+    PM_HIP_CHECK(hipStreamSynchronize(stream));
+    ka.reset();
+    uint64_t* recv = ka.alloc<uint64_t>(nrecv);
+    comm.alltoallv(send, sb.data(), recv, rb.data(), stream);
+    PM_HIP_CHECK(hipStreamSynchronize(stream));
+    kb.reset();
+  }
+  bdeg.reset();
+  kb.alloc<uint64_t>(nrecv);  // the sort's second buffer
+  return csr_from_unsorted(scale, ka, kb, nrecv, stream);
 }
 
 DevCsr rmat_csr_device(uint64_t scale, uint64_t p_gen, hipStream_t stream) {

@@ -29,4 +29,13 @@ void rmat_keys_device(const RmatPlan& p, const std::vector<uint64_t>& vranks, ui
 // The whole symmetrized graph of P_gen generator ranks on the current device.
 DevCsr rmat_csr_device(uint64_t scale, uint64_t p_gen, hipStream_t stream);
 
+struct Comm;
+// One shard of a sharded search over the R-MAT graph, built on the current device: this shard
+// generates the streams of generator ranks r = shard (mod nshards); every directed entry (u, v)
+// travels to its owner -- u % nshards, or v % nshards when u is a delegate (global degree >=
+// hub_threshold) -- in one all-to-all; the received entries are radix-sorted into the shard's
+// row-sorted CSR (rows it does not hold are empty).  gdeg receives the global degrees (host).
+DevCsr rmat_shard_device(uint64_t scale, uint64_t p_gen, uint64_t hub_threshold, Comm& comm, uint32_t nshards,
+                         uint32_t shard, std::vector<uint32_t>& gdeg, hipStream_t stream);
+
 }  // namespace pm

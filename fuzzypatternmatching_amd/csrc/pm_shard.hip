@@ -1,25 +1,27 @@
-// Sharded search (DESIGN.md §6): the exchanges between the shards of one
+// Sharded search (DESIGN.md section 6): the exchanges between the shards of one
 // pattern search and the two Comm implementations.
 //
 // The reference partitions vertices 1D-cyclically (owner = id % P,
 // delegate_partitioned_graph.ipp:1679-1696) and moves every LCC/NLCC message
 // through the MPI mailbox (new_mailbox.hpp:289-713); state sync of delegates
 // uses MPI_Allreduce (impl/vertex_data.hpp:114-126).  Here shard q owns the
-// rows of ids v % nshards == q and the per-superstep exchange is BSP:
-//   * LCC: every row pulls its neighbours' T_pub, so after each superstep the
-//     shards all-gather the T_pub of their slist entries (the only vertices
-//     that can be in S) -- 2 B per entry, no per-edge messages;
-//   * NLCC / TDS: after every walk position the tokens (vertex, source,
-//     parent) and walks move to the owner of their next vertex in one RCCL
-//     all-to-all (shard_route: ncclSend / ncclRecv pairs in a group), so the
-//     (vertex, source) dedup of nem_1.hpp:131-139, M[u] and the terminal
-//     checks stay local; acknowledgements travel to the source's owner;
-//   * counters and flags: one u64 sum all-reduce per LCC call / NLC line.
+// rows of ids v % nshards == q and the search is BSP with three exchanges:
+//   * after superstep 0 (the full-adjacency scan, split over the shards): the
+//     survivors' T_pub codes, all-gathered (2 bits per survivor + its position),
+//     which is all the first later superstep's row pulls read of other shards;
+//   * after that superstep (S has collapsed: S=28 tree 9.8 M -> 0.8 M vertices,
+//     31 M -> 0.85 M edges): the state of S -- T_pub, T_state, M rows --
+//     all-gathered into a replica that every shard holds; the rest of the
+//     search (later supersteps, NLC lines, later LCC calls) runs on the replica
+//     with no further exchange, identically on every shard;
+//   * counters: one u64 sum all-reduce over the sharded supersteps' slots.
 // Results are identical for every shard count.
 
 #include <hip/hip_runtime.h>
 
 #include <rccl/rccl.h>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <condition_variable>
@@ -64,6 +66,10 @@ class RcclComm : public Comm {
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
     if (!count) return;
     PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm_, s));
+  }
+  void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    if (!count) return;
+    PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, comm_, s));
   }
   // grouped point-to-point sends / receives over xGMI (one pair per peer)
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
@@ -191,6 +197,23 @@ class ThreadComm : public Comm {
     if (count) PM_HIP_CHECK(hipMemcpyAsync(buf, sum.data(), count * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     PM_HIP_CHECK(hipStreamSynchronize(s));
   }
+  void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));
+    DeviceReleased rel(g_);
+    std::vector<uint32_t> h(count);
+    std::vector<uint64_t> hv(count);
+    if (count) PM_HIP_CHECK(hipMemcpyAsync(h.data(), buf, count * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < count; ++i) hv[i] = h[i];
+    g_->hvec[rank_] = &hv;
+    g_->barrier();
+    std::vector<uint32_t> sum(count, 0);
+    for (int q = 0; q < g_->n; ++q)
+      for (size_t i = 0; i < count; ++i) sum[i] += static_cast<uint32_t>((*g_->hvec[q])[i]);
+    g_->barrier();
+    if (count) PM_HIP_CHECK(hipMemcpyAsync(buf, sum.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));
+  }
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                  hipStream_t s) override {
     PM_HIP_CHECK(hipStreamSynchronize(s));
@@ -225,46 +248,279 @@ Comm* make_thread_comm(ThreadGroup* g, int rank) { return new ThreadComm(g, rank
 // exchange kernels
 static constexpr int kXBlock = 256;
 
+// Per-shard counts of one gather, passed by value (G <= 64): rows / entries and
+// their first index in the concatenation over the shards.
+struct XCounts {
+  uint64_t n[64], m[64], base[64], ebase[64];
+};
+
 static unsigned xgrid(uint64_t items) {
   uint64_t g = (items + kXBlock - 1) / kXBlock;
   return static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(g, 65535)));
 }
 
-__global__ void k_pack_tpub(const uint32_t* __restrict__ slist, uint32_t nS, const uint16_t* __restrict__ tpub,
-                            uint16_t* __restrict__ out) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x)
-    out[i] = tpub[slist[i]];
+template <typename T>
+static T* grow(void*& p, size_t& cap, size_t bytes) {
+  if (cap < bytes || !p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    const size_t b = std::max<size_t>(bytes + bytes / 8, 4096);
+    PM_HIP_CHECK(hipMalloc(&p, b));
+    cap = b;
+  }
+  return static_cast<T*>(p);
 }
 
-// Entries of the other shards: tpub[xslist[g][i]] = recv[g][i].
-__global__ void k_unpack_tpub(const uint32_t* __restrict__ xslist, const uint32_t* __restrict__ xnS, uint32_t maxS,
-                              uint32_t G, uint32_t me, const uint16_t* __restrict__ recv, uint16_t* __restrict__ tpub) {
+__global__ void k_count_to_u64(const uint32_t* __restrict__ n, uint64_t* __restrict__ out) { *out = *n; }
+
+// Code records of this shard's superstep-0 survivors: position | code << 30
+// (2-bit tpub_code), or, when some label has more than two template vertices
+// (its code 3 means "gather T_pub"), position | T_pub << 32 | code << 62.
+__global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
+                             const uint32_t* __restrict__ tcode, const uint16_t* __restrict__ tpub, int wide,
+                             uint32_t* __restrict__ out32, unsigned long long* __restrict__ out64) {
+  const uint64_t n = *nSp;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t p = slist[i];
+    const uint32_t code = (tcode[p >> 4] >> ((p & 15u) << 1)) & 3u;
+    if (wide) out64[i] = p | (static_cast<unsigned long long>(tpub[p]) << 32) | (static_cast<unsigned long long>(code) << 62);
+    else out32[i] = p | (code << 30);
+  }
+}
+
+// The other shards' code records into this shard's 2-bit codes (and T_pub).
+__global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned long long* __restrict__ in64,
+                               uint64_t maxS, uint32_t G, uint32_t me, XCounts x, uint32_t* __restrict__ tcode,
+                               uint16_t* __restrict__ tpub) {
   const uint64_t total = uint64_t(G) * maxS;
   for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t g = static_cast<uint32_t>(j / maxS), i = static_cast<uint32_t>(j % maxS);
-    if (g != me && i < xnS[g]) tpub[xslist[j]] = recv[j];
+    const uint32_t g = static_cast<uint32_t>(j / maxS);
+    if (g == me || j % maxS >= x.n[g]) continue;
+    uint32_t p, code;
+    if (in64) {
+      const unsigned long long r = in64[j];
+      p = static_cast<uint32_t>(r & 0x3FFFFFFFull);
+      code = static_cast<uint32_t>(r >> 62);
+      tpub[p] = static_cast<uint16_t>(r >> 32);
+    } else {
+      p = in32[j] & 0x3FFFFFFFu;
+      code = in32[j] >> 30;
+    }
+    atomicOr(&tcode[p >> 4], code << ((p & 15u) << 1));
   }
 }
 
-// Owner-bucketed routing of fixed-size records (the mailbox exchange of
-// new_mailbox.hpp:289-713 as one RCCL all-to-all per BSP step): record i is
-// `words` u32, its destination the owner of the position in word kw.
-__global__ void k_route_count(const uint32_t* __restrict__ items, uint64_t n, int words, int kw,
-                              const uint32_t* __restrict__ perm, uint32_t G, uint32_t* __restrict__ dest,
-                              unsigned long long* __restrict__ cnt) {
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t g = perm[items[i * words + kw]] % G;
-    dest[i] = g;
-    atomicAdd(&cnt[g], 1ull);
+// u64 mode, after the first later superstep: the T_pub buffer superstep 0
+// wrote (read by that superstep) is cleared at the other shards' survivors.
+__global__ void k_clear_codes(const unsigned long long* __restrict__ in64, uint64_t maxS, uint32_t G, uint32_t me,
+                              XCounts x, uint16_t* __restrict__ tpub) {
+  const uint64_t total = uint64_t(G) * maxS;
+  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t g = static_cast<uint32_t>(j / maxS);
+    if (g == me || j % maxS >= x.n[g]) continue;
+    tpub[static_cast<uint32_t>(in64[j] & 0x3FFFFFFFull)] = 0;
   }
 }
 
-__global__ void k_route_scatter(const uint32_t* __restrict__ items, uint64_t n, int words,
-                                const uint32_t* __restrict__ dest, unsigned long long* __restrict__ cursor,
-                                uint32_t* __restrict__ out) {
+// pack_state, pass 1: per slist entry whether it is in S and its alive M count.
+// A dense superstep-0 row (dmoff != kNone) holds only alive entries; T_state = T_pub there.
+__global__ void k_pack_count(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp, uint64_t cap,
+                             const uint16_t* __restrict__ tpub, const uint32_t* __restrict__ mlen,
+                             const uint32_t* __restrict__ malive, const uint32_t* __restrict__ dmoff,
+                             uint32_t* __restrict__ keep, uint32_t* __restrict__ cnt) {
+  const uint64_t n = min(static_cast<uint64_t>(*nSp), cap);
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cap; i += uint64_t(gridDim.x) * blockDim.x) {
+    uint32_t k = 0, m = 0;
+    if (i < n) {
+      const uint32_t u = slist[i];
+      if (tpub[u]) {
+        k = 1;
+        m = (dmoff && dmoff[u] != kNone) ? mlen[u] : malive[u];
+      }
+    }
+    keep[i] = k;
+    cnt[i] = m;
+  }
+}
+
+// pass 2: rows {position, T_pub | T_state << 16, |M|, first entry} and their alive entries.
+__global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp, uint64_t cap,
+                             const uint32_t* __restrict__ keep, const uint32_t* __restrict__ ridx,
+                             const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ eoff,
+                             const uint16_t* __restrict__ tpub, const uint16_t* __restrict__ tst,
+                             const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ moff,
+                             const uint32_t* __restrict__ mcol, const uint32_t* __restrict__ dmoff, uint64_t dbase,
+                             uint32_t* __restrict__ rec, uint32_t* __restrict__ ent, uint64_t ent_cap,
+                             unsigned long long* __restrict__ totals) {
+  const uint64_t n = min(static_cast<uint64_t>(*nSp), cap);
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t o = atomicAdd(&cursor[dest[i]], 1ull);
-    for (int w = 0; w < words; ++w) out[o * words + w] = items[i * words + w];
+    if (i == n - 1) {
+      totals[0] = ridx[i] + keep[i];
+      totals[1] = eoff[i] + cnt[i];
+    }
+    if (!keep[i] || !rec) continue;
+    const uint32_t u = slist[i];
+    const bool dense = dmoff && dmoff[u] != kNone;
+    const uint64_t b = dense ? dbase + dmoff[u] : moff[u];
+    const uint32_t L = mlen[u];
+    const uint16_t T = tpub[u];
+    const uint64_t e0 = eoff[i];
+    uint32_t* r = rec + 4 * uint64_t(ridx[i]);
+    r[0] = u;
+    r[1] = T | (static_cast<uint32_t>(dense ? T : tst[u]) << 16);
+    r[2] = cnt[i];
+    r[3] = static_cast<uint32_t>(e0);
+    uint64_t k = e0;
+    for (uint32_t j = 0; j < L; ++j) {
+      const uint32_t m = mcol[b + j];
+      if ((m & kAlive) && k < ent_cap) ent[k++] = m;
+    }
+  }
+  if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) totals[0] = totals[1] = 0;
+}
+
+// The replica: every shard's rows (block g of the gather, x.n[g] rows) in shard order.
+__global__ void k_unpack_rows(const uint32_t* __restrict__ rec, uint64_t maxR, uint32_t G, XCounts x,
+                              uint32_t* __restrict__ slist, uint16_t* __restrict__ tpub, uint16_t* __restrict__ tst,
+                              uint32_t* __restrict__ mlen, uint32_t* __restrict__ malive,
+                              uint64_t* __restrict__ rmoff) {
+  const uint64_t total = uint64_t(G) * maxR;
+  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t g = static_cast<uint32_t>(j / maxR);
+    const uint64_t i = j % maxR;
+    if (i >= x.n[g]) continue;
+    const uint32_t* r = rec + 4 * j;
+    const uint32_t u = r[0];
+    slist[x.base[g] + i] = u;
+    tpub[u] = static_cast<uint16_t>(r[1]);
+    tst[u] = static_cast<uint16_t>(r[1] >> 16);
+    mlen[u] = r[2];
+    malive[u] = r[2];
+    rmoff[u] = x.ebase[g] + r[3];
+  }
+}
+
+__global__ void k_unpack_entries(const uint32_t* __restrict__ ent, uint64_t maxE, uint32_t G, XCounts x,
+                                 uint32_t* __restrict__ rmcol) {
+  const uint64_t total = uint64_t(G) * maxE;
+  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t g = static_cast<uint32_t>(j / maxE);
+    const uint64_t e = j % maxE;
+    if (e < x.m[g]) rmcol[x.ebase[g] + e] = ent[j];
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Delegates (hubs) of a sharded search.  A hub's row is split over the shards
+// by target owner (delegate_partitioned_graph.ipp:1402-1648); superstep 0
+// scans every share like a heavy row but leaves its TN / distinct count in the
+// heavy scratch.  The shares meet at the controller (hub ordinal % nshards,
+// ipp:346-355): the partial (count, TN) pairs are all-gathered and OR-ed /
+// summed -- the all-gather + OR that stands in for the delegates'
+// all_max_reduce (impl/vertex_data.hpp:114-126; RCCL has no bitwise-OR
+// reduction) -- and the shares' M entries travel to the controller in one
+// all-to-all (grouped ncclSend / ncclRecv), which verifies the hub and holds
+// its whole M row (the reference's controller also owns the hub's full
+// active-edge map after superstep 0, nonunique_ee.hpp:589-624).
+__global__ void k_hub_partials(const HubInfo* __restrict__ info, uint32_t H, const uint32_t* __restrict__ hscr,
+                               uint32_t nheavy, unsigned long long* __restrict__ out) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < H; j += gridDim.x * blockDim.x) {
+    const uint32_t h = info[j].hidx;
+    out[j] = h == kNoHub ? 0ull : (static_cast<unsigned long long>(hscr[nheavy + h]) << 32) | hscr[h];
+  }
+}
+
+// This shard's share of hub j: its alive M entries in row order to send[soff[j]..].
+__global__ void k_hub_pack(const HubInfo* __restrict__ info, uint32_t H, const uint64_t* __restrict__ soff,
+                           const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
+                           uint32_t* __restrict__ send) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x / 64);
+  for (uint32_t j = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; j < H; j += nw) {
+    if (soff[j] == ~0ull) continue;
+    const uint32_t p = info[j].pos;
+    const uint64_t b = offp[p], len = offp[p + 1] - b;
+    uint64_t o = soff[j];
+    for (uint64_t i0 = 0; i0 < len; i0 += 64) {
+      const uint64_t i = i0 + lane;
+      const uint32_t m = i < len ? mcol[b + i] : 0u;
+      const bool alive = i < len && (m & kAlive);
+      const uint64_t bal = __ballot(alive);
+      if (alive) send[o + __builtin_popcountll(bal & ((1ull << lane) - 1))] = m;
+      o += __builtin_popcountll(bal);
+    }
+  }
+}
+
+struct HubFinishArgs {
+  const uint32_t* ctrl;               // hub ordinals this shard controls
+  uint32_t nctrl, G, H, P, nranks;
+  const unsigned long long* part;     // G x H (count << 32 | TN)
+  const uint64_t* roff;               // nctrl x G: where shard g's share of hub ctrl[k] starts in recv
+  const uint32_t* recv;
+  const HubInfo* info;
+  LabelRuns lr;
+  PatArgs pa;
+  uint16_t* tpub;
+  uint16_t* tst;
+  uint32_t* mlen;
+  uint32_t* malive;
+  uint32_t* tcode;
+  uint32_t* dmoff;                    // dense superstep-0 M in use: the hub's row is not dense (kNone)
+  uint32_t* mcol;
+  uint32_t* slist;
+  uint32_t* nS;
+  unsigned long long* slot;           // superstep-0 counters
+};
+
+// The controller's verify of each hub it controls (global verify_and_update_vertex_state,
+// nonunique_ee.hpp:886-977, on the combined TN) and its whole M row in the hub area.
+__global__ void k_hub_finish(HubFinishArgs a) {
+  __shared__ uint16_t s_adj[16];
+  load_adj(s_adj, a.pa);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x / 64);
+  for (uint32_t k = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; k < a.nctrl; k += nw) {
+    const uint32_t j = a.ctrl[k];
+    uint32_t TN = 0;
+    uint64_t cnt = 0;
+    for (uint32_t g = 0; g < a.G; ++g) {
+      const unsigned long long x = a.part[uint64_t(g) * a.H + j];
+      TN |= static_cast<uint32_t>(x & 0xFFFFu);
+      cnt += x >> 32;
+    }
+    if (!TN) continue;  // no compatible neighbour: never entered S
+    const uint32_t p = a.info[j].pos;
+    uint32_t tu = 0;
+    for (int l = 0; l < a.lr.n; ++l)
+      if (p - a.lr.lo[l] < a.lr.len[l]) tu = a.lr.tu[l];
+    const uint16_t T = keep_bits(static_cast<uint16_t>(tu), static_cast<uint16_t>(TN), s_adj);
+    if (lane == 0) {
+      if (!T) {
+        atomicAdd(&a.slot[2 * a.P + 2], 1ull);  // removed from S (not_finished)
+      } else {
+        a.tst[p] = T;
+        a.tpub[p] = T;
+        a.mlen[p] = static_cast<uint32_t>(cnt);
+        a.malive[p] = static_cast<uint32_t>(cnt);
+        atomicOr(&a.tcode[p >> 4], tpub_code(T, tu) << ((p & 15u) << 1));
+        if (a.dmoff) a.dmoff[p] = kNone;
+        a.slist[atomicAdd(a.nS, 1u)] = p;
+        const uint32_t r = a.nranks <= 1 ? 0u : j % a.nranks;  // owner rule of a delegate
+        atomicAdd(&a.slot[r], 1ull);
+        atomicAdd(&a.slot[a.P + r], static_cast<unsigned long long>(cnt));
+      }
+    }
+    if (!T) continue;
+    uint32_t* dst = a.mcol + a.info[j].moff;
+    for (uint32_t g = 0; g < a.G; ++g) {
+      const uint64_t n = a.part[uint64_t(g) * a.H + j] >> 32;
+      const uint32_t* src = a.recv + a.roff[uint64_t(k) * a.G + g];
+      for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+      dst += n;
+    }
   }
 }
 
@@ -290,111 +546,225 @@ std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v) {
   return out;
 }
 
-std::vector<std::vector<uint32_t>> shard_allgatherv(Ctx& c, const std::vector<uint32_t>& v) {
-  if (!c.comm) return {v};
+// words u64 of every shard: d_xcnt[0 .. words) of this shard -> host [g * words + k] (one host sync)
+static std::vector<uint64_t> gather_counts(Ctx& c, int words) {
   const uint32_t G = c.nshards;
-  std::vector<uint64_t> sz(G, 0);
-  sz[c.shard] = v.size();
-  sz = shard_allreduce(c, sz);
-  const uint64_t maxL = std::max<uint64_t>(1, *std::max_element(sz.begin(), sz.end()));
-  uint32_t *d_send = nullptr, *d_recv = nullptr;
-  PM_HIP_CHECK(hipMalloc(&d_send, maxL * sizeof(uint32_t)));
-  PM_HIP_CHECK(hipMalloc(&d_recv, G * maxL * sizeof(uint32_t)));
-  std::vector<uint32_t> all(G * maxL);
-  try {
-    if (!v.empty())
-      PM_HIP_CHECK(hipMemcpyAsync(d_send, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-    c.comm->allgather(d_send, d_recv, maxL * sizeof(uint32_t), c.stream);
-    PM_HIP_CHECK(hipMemcpyAsync(all.data(), d_recv, all.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  } catch (...) {
-    (void)hipFree(d_send);
-    (void)hipFree(d_recv);
-    throw;
-  }
-  (void)hipFree(d_send);
-  (void)hipFree(d_recv);
-  std::vector<std::vector<uint32_t>> out(G);
-  for (uint32_t g = 0; g < G; ++g) out[g].assign(all.begin() + g * maxL, all.begin() + g * maxL + sz[g]);
-  return out;
+  c.comm->allgather(c.d_xcnt, c.d_xcnt + 64, words * sizeof(uint64_t), c.stream);
+  uint64_t* pin = pinned(c, uint64_t(G) * words);
+  PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_xcnt + 64, uint64_t(G) * words * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  return std::vector<uint64_t>(pin, pin + uint64_t(G) * words);
 }
 
-uint32_t* shard_route(Ctx& c, const uint32_t* items, uint64_t n, int words, int kw, uint64_t& nout) {
-  const uint32_t G = c.nshards;
-  auto* cnt = static_cast<unsigned long long*>(c.arena.get(2 * G * sizeof(unsigned long long)));
-  auto* cursor = cnt + G;
-  auto* allc = static_cast<uint64_t*>(c.arena.get(uint64_t(G) * G * sizeof(uint64_t)));
-  PM_HIP_CHECK(hipMemsetAsync(cnt, 0, G * sizeof(unsigned long long), c.stream));
-  auto* dest = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  if (n)
-    hipLaunchKernelGGL(k_route_count, dim3(xgrid(n)), dim3(kXBlock), 0, c.stream, items, n, words, kw, c.d_perm, G,
-                       dest, cnt);
-  c.comm->allgather(cnt, allc, G * sizeof(uint64_t), c.stream);  // allc[q * G + g]: shard q -> shard g
-  std::vector<uint64_t> m(uint64_t(G) * G);
-  PM_HIP_CHECK(hipMemcpyAsync(m.data(), allc, m.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+static void ensure_xcnt(Ctx& c) {
+  if (c.nshards > 64) throw std::runtime_error("more than 64 shards");
+  if (!c.d_xcnt) PM_HIP_CHECK(hipMalloc(&c.d_xcnt, (64 + 4 * 64) * sizeof(uint64_t)));
+}
+
+
+void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
+  if (!c.comm || !c.split_hubs) return;
+  const uint32_t G = c.nshards, me = c.shard;
+  const uint32_t H = static_cast<uint32_t>(c.hubinfo.size());
+  auto* part = reinterpret_cast<unsigned long long*>(c.d_hubpart);
+  hipLaunchKernelGGL(k_hub_partials, dim3(xgrid(H)), dim3(kXBlock), 0, c.stream, c.d_hubinfo, H, c.d_hscr, c.nheavy,
+                     part);
+  c.comm->allgather(part, part + H, uint64_t(H) * sizeof(uint64_t), c.stream);
+  uint64_t* pin = pinned(c, uint64_t(G) * H);
+  PM_HIP_CHECK(hipMemcpyAsync(pin, part + H, uint64_t(G) * H * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  std::vector<uint64_t> sb(G), rb(G), soff(G, 0);
-  uint64_t nrecv = 0;
-  for (uint32_t g = 0; g < G; ++g) {
-    sb[g] = m[uint64_t(c.shard) * G + g] * words * sizeof(uint32_t);
-    rb[g] = m[uint64_t(g) * G + c.shard] * words * sizeof(uint32_t);
-    nrecv += m[uint64_t(g) * G + c.shard];
-    if (g) soff[g] = soff[g - 1] + m[uint64_t(c.shard) * G + g - 1];
-  }
-  auto* send = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(n, 1) * words * sizeof(uint32_t)));
-  auto* recv = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(nrecv, 1) * words * sizeof(uint32_t)));
-  if (n) {
-    PM_HIP_CHECK(hipMemcpyAsync(cursor, soff.data(), G * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_route_scatter, dim3(xgrid(n)), dim3(kXBlock), 0, c.stream, items, n, words, dest, cursor,
-                       send);
-  }
-  PM_HIP_CHECK(hipGetLastError());
+  const std::vector<uint64_t> all(pin, pin + uint64_t(G) * H);
+  auto cnt = [&](uint32_t g, uint32_t j) { return all[uint64_t(g) * H + j] >> 32; };
+  // send: this shard's shares grouped by controller, hubs in order; receive: the shares of the hubs this
+  // shard controls, shard by shard
+  std::vector<uint64_t> soff(H, ~0ull), sb(G, 0), rb(G, 0), roff;
+  std::vector<uint32_t> ctrl;
+  uint64_t so = 0;
+  for (uint32_t g = 0; g < G; ++g)
+    for (uint32_t j = g; j < H; j += G)
+      if (cnt(me, j)) {
+        soff[j] = so;
+        so += cnt(me, j);
+        sb[g] += cnt(me, j) * sizeof(uint32_t);
+      }
+  for (uint32_t j = me; j < H; j += G) ctrl.push_back(j);
+  roff.assign(ctrl.size() * G, 0);
+  uint64_t ro = 0;
+  for (uint32_t g = 0; g < G; ++g)
+    for (size_t k = 0; k < ctrl.size(); ++k) {
+      roff[k * G + g] = ro;
+      ro += cnt(g, ctrl[k]);
+      rb[g] += cnt(g, ctrl[k]) * sizeof(uint32_t);
+    }
+  c.arena.reset();
+  auto* d_soff = static_cast<uint64_t*>(c.arena.get(std::max<size_t>(H, 1) * sizeof(uint64_t)));
+  auto* d_roff = static_cast<uint64_t*>(c.arena.get(std::max<size_t>(roff.size(), 1) * sizeof(uint64_t)));
+  auto* d_ctrl = static_cast<uint32_t*>(c.arena.get(std::max<size_t>(ctrl.size(), 1) * sizeof(uint32_t)));
+  PM_HIP_CHECK(hipMemcpyAsync(d_soff, soff.data(), H * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  if (!roff.empty())
+    PM_HIP_CHECK(hipMemcpyAsync(d_roff, roff.data(), roff.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  if (!ctrl.empty())
+    PM_HIP_CHECK(hipMemcpyAsync(d_ctrl, ctrl.data(), ctrl.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  auto* send = grow<uint32_t>(c.d_xsend, c.xsend_cap, std::max<uint64_t>(so, 1) * sizeof(uint32_t));
+  auto* recv = grow<uint32_t>(c.d_xrecv, c.xrecv_cap, std::max<uint64_t>(ro, 1) * sizeof(uint32_t));
+  if (so)
+    hipLaunchKernelGGL(k_hub_pack, dim3(xgrid(uint64_t(H) * 64)), dim3(kXBlock), 0, c.stream, c.d_hubinfo, H, d_soff,
+                       c.d_offp, c.d_mcol, send);
   c.comm->alltoallv(send, sb.data(), recv, rb.data(), c.stream);
-  nout = nrecv;
-  return recv;
+  HubFinishArgs a{};
+  a.ctrl = d_ctrl;
+  a.nctrl = static_cast<uint32_t>(ctrl.size());
+  a.G = G;
+  a.H = H;
+  a.nranks = c.nranks;
+  a.P = c.nranks <= 1 ? 1 : c.nranks;
+  a.part = part + H;
+  a.roff = d_roff;
+  a.recv = recv;
+  a.info = c.d_hubinfo;
+  a.lr = c.lr;
+  a.pa = c.pa;
+  a.tpub = c.d_tpub[c.cur];
+  a.tst = c.d_tst;
+  a.mlen = c.d_mlen;
+  a.malive = c.d_malive;
+  a.tcode = c.d_tcode;
+  a.dmoff = c.k1_dense ? c.d_dmoff : nullptr;
+  a.mcol = c.d_mcol;
+  a.slist = c.d_slist;
+  a.nS = c.d_nS;
+  a.slot = reinterpret_cast<unsigned long long*>(d_slot);
+  if (a.nctrl)
+    hipLaunchKernelGGL(k_hub_finish, dim3(xgrid(uint64_t(a.nctrl) * 64)), dim3(kXBlock), 0, c.stream, a);
+  PM_HIP_CHECK(hipGetLastError());
+  c.nS_host += a.nctrl;  // (an upper bound until the code exchange reads the count)
 }
 
-void shard_exchange_tpub(Ctx& c) {
-  if (!c.comm) return;
-  const uint32_t G = c.nshards, maxS = c.xmaxS, nS = c.xnS[c.shard];
-  if (nS) hipLaunchKernelGGL(k_pack_tpub, dim3(xgrid(nS)), dim3(kXBlock), 0, c.stream, c.d_slist, nS, c.d_tpub[c.cur],
-                             c.d_xsend);
-  c.comm->allgather(c.d_xsend, c.d_xrecv, size_t(maxS) * sizeof(uint16_t), c.stream);
-  hipLaunchKernelGGL(k_unpack_tpub, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream, c.d_xslist, c.d_xnS,
-                     maxS, G, c.shard, c.d_xrecv, c.d_tpub[c.cur]);
+void shard_codes_after_first(Ctx& c) {
+  if (!c.comm || c.replicated) return;
+  ensure_xcnt(c);
+  const uint32_t G = c.nshards;
+  hipLaunchKernelGGL(k_count_to_u64, dim3(1), dim3(1), 0, c.stream, c.d_nS, c.d_xcnt);
+  const std::vector<uint64_t> n = gather_counts(c, 1);
+  uint64_t maxS = 1;
+  for (uint32_t g = 0; g < G; ++g) maxS = std::max(maxS, n[g]);
+  c.nS_host = static_cast<uint32_t>(n[c.shard]);
+  c.xcode_n = n;
+  c.xcode_max = maxS;
+  const size_t rb = c.xcode_wide ? 8 : 4;
+  auto* send = grow<char>(c.d_xsend, c.xsend_cap, maxS * rb);
+  auto* recv = grow<char>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxS * rb);
+  hipLaunchKernelGGL(k_pack_codes, dim3(xgrid(c.nS_host)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tcode,
+                     c.d_tpub[c.cur], c.xcode_wide ? 1 : 0, reinterpret_cast<uint32_t*>(send),
+                     reinterpret_cast<unsigned long long*>(send));
+  c.comm->allgather(send, recv, maxS * rb, c.stream);
+  XCounts x{};
+  for (uint32_t g = 0; g < G; ++g) x.n[g] = n[g];
+  hipLaunchKernelGGL(k_unpack_codes, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream,
+                     c.xcode_wide ? nullptr : reinterpret_cast<const uint32_t*>(recv),
+                     c.xcode_wide ? reinterpret_cast<const unsigned long long*>(recv) : nullptr, maxS, G, c.shard, x,
+                     c.d_tcode, c.d_tpub[c.cur]);
   PM_HIP_CHECK(hipGetLastError());
 }
 
-void shard_after_first(Ctx& c) {
-  if (!c.comm) return;
-  const uint32_t G = c.nshards;
-  uint32_t nS = 0;
-  PM_HIP_CHECK(hipMemcpyAsync(&nS, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t* counts);
+
+uint64_t pack_state_entry_bound(Ctx& c) {
+  // the exact count: pass 1 + scans, then one read-back (the caller sizes its buffer)
+  ensure_xcnt(c);
+  pack_state(c, nullptr, nullptr, 0, c.d_xcnt);
+  uint64_t* pin = pinned(c, 2);
+  PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_xcnt, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  c.nS_host = nS;
-  std::vector<uint64_t> cnt(G, 0);
-  cnt[c.shard] = nS;
-  cnt = shard_allreduce(c, cnt);
-  c.xnS.assign(G, 0);
-  uint32_t maxS = 1;
+  return pin[1];
+}
+
+void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t* counts) {
+  const uint64_t cap = c.nS_host;
+  const uint32_t* dmoff = c.k1_dense ? c.d_dmoff : nullptr;
+  c.arena.reset();
+  auto* keep = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
+  auto* cnt = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
+  auto* ridx = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
+  auto* eoff = static_cast<uint64_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint64_t)));
+  PM_HIP_CHECK(hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), c.stream));
+  if (!cap) return;
+  hipLaunchKernelGGL(k_pack_count, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap,
+                     c.d_tpub[c.cur], c.d_mlen, c.d_malive, dmoff, keep, cnt);
+  size_t t1 = 0, t2 = 0;
+  PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, t1, keep, ridx, 0u, size_t(cap), rocprim::plus<uint32_t>(), c.stream));
+  rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> wc(cnt, Widen());
+  PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, t2, wc, eoff, uint64_t(0), size_t(cap), rocprim::plus<uint64_t>(),
+                                       c.stream));
+  void* tmp = c.arena.get(std::max(t1, t2));
+  PM_HIP_CHECK(rocprim::exclusive_scan(tmp, t1, keep, ridx, 0u, size_t(cap), rocprim::plus<uint32_t>(), c.stream));
+  PM_HIP_CHECK(rocprim::exclusive_scan(tmp, t2, wc, eoff, uint64_t(0), size_t(cap), rocprim::plus<uint64_t>(),
+                                       c.stream));
+  // rec == nullptr: totals only (the rows are not written)
+  hipLaunchKernelGGL(k_pack_write, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap, keep,
+                     ridx, cnt, eoff, c.d_tpub[c.cur], c.d_tst, c.d_mlen, m_off(c), m_col(c), dmoff, c.dbase,
+                     rec, ent, rec ? ent_cap : 0, reinterpret_cast<unsigned long long*>(counts));
+  PM_HIP_CHECK(hipGetLastError());
+}
+
+void shard_replicate(Ctx& c) {
+  if (!c.comm || c.replicated) return;
+  ensure_xcnt(c);
+  const uint32_t G = c.nshards;
+  XCounts x{};
+  // u64 code mode: the other shards' T_pub that superstep 0's buffer received (the superstep that
+  // read it is done; the buffer becomes the next superstep's output)
+  if (c.xcode_wide && !c.xcode_n.empty()) {
+    for (uint32_t g = 0; g < G; ++g) x.n[g] = c.xcode_n[g];
+    hipLaunchKernelGGL(k_clear_codes, dim3(xgrid(uint64_t(G) * c.xcode_max)), dim3(kXBlock), 0, c.stream,
+                       reinterpret_cast<const unsigned long long*>(c.d_xrecv), c.xcode_max, G, c.shard, x,
+                       c.d_tpub[c.cur ^ 1]);
+  }
+  c.xcode_n.clear();
+  // this shard's rows of S: counts first, then one gather of every shard's counts (one host sync)
+  pack_state(c, nullptr, nullptr, 0, c.d_xcnt);
+  const std::vector<uint64_t> cn = gather_counts(c, 2);
+  uint64_t maxR = 1, maxE = 1, rows = 0, ents = 0;
   for (uint32_t g = 0; g < G; ++g) {
-    c.xnS[g] = static_cast<uint32_t>(cnt[g]);
-    maxS = std::max(maxS, c.xnS[g]);
+    x.n[g] = cn[2 * g];
+    x.m[g] = cn[2 * g + 1];
+    x.base[g] = rows;
+    x.ebase[g] = ents;
+    rows += x.n[g];
+    ents += x.m[g];
+    maxR = std::max(maxR, x.n[g]);
+    maxE = std::max(maxE, x.m[g]);
   }
-  if (maxS > c.xmaxS || !c.d_xslist) {
-    void* ptrs[] = {c.d_xslist, c.d_xnS, c.d_xsend, c.d_xrecv};
-    for (void* p : ptrs)
-      if (p) (void)hipFree(p);
-    PM_HIP_CHECK(hipMalloc(&c.d_xslist, size_t(G) * maxS * sizeof(uint32_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_xnS, G * sizeof(uint32_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_xsend, size_t(maxS) * sizeof(uint16_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_xrecv, size_t(G) * maxS * sizeof(uint16_t)));
+  if (x.m[c.shard] >= (1ull << 32)) throw std::runtime_error("replica: more than 2^32 M entries on one shard");
+  if (rows > c.n) throw std::runtime_error("internal: replica larger than the vertex set");
+  // every shard's send block is read up to the largest count
+  auto* rsend = grow<uint32_t>(c.d_xsend, c.xsend_cap, maxR * 16);
+  auto* esend = grow<uint32_t>(c.d_xent_send, c.xent_send_cap, maxE * 4);
+  pack_state(c, rsend, esend, maxE, c.d_xcnt + 2);
+  auto* rrecv = grow<uint32_t>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxR * 16);
+  auto* erecv = grow<uint32_t>(c.d_xent_recv, c.xent_recv_cap, uint64_t(G) * maxE * 4);
+  c.comm->allgather(rsend, rrecv, maxR * 16, c.stream);
+  c.comm->allgather(esend, erecv, maxE * 4, c.stream);
+  if (!c.d_rmoff) PM_HIP_CHECK(hipMalloc(&c.d_rmoff, std::max<uint64_t>(c.n, 1) * sizeof(uint64_t)));
+  if (c.rmcap < ents + 1 || !c.d_rmcol) {
+    if (c.d_rmcol) (void)hipFree(c.d_rmcol);
+    c.rmcap = std::max<uint64_t>(ents + ents / 4, 1 << 16);
+    PM_HIP_CHECK(hipMalloc(&c.d_rmcol, c.rmcap * sizeof(uint32_t)));
   }
-  c.xmaxS = maxS;
-  PM_HIP_CHECK(hipMemcpyAsync(c.d_xnS, c.xnS.data(), G * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
-  // d_slist holds V entries >= maxS: the block past nS is padding
-  c.comm->allgather(c.d_slist, c.d_xslist, size_t(maxS) * sizeof(uint32_t), c.stream);
-  shard_exchange_tpub(c);
+  hipLaunchKernelGGL(k_unpack_rows, dim3(xgrid(uint64_t(G) * maxR)), dim3(kXBlock), 0, c.stream, rrecv, maxR, G, x,
+                     c.d_slist, c.d_tpub[c.cur], c.d_tst, c.d_mlen, c.d_malive, c.d_rmoff);
+  hipLaunchKernelGGL(k_unpack_entries, dim3(xgrid(uint64_t(G) * maxE)), dim3(kXBlock), 0, c.stream, erecv, maxE, G, x,
+                     c.d_rmcol);
+  const uint32_t nrows = static_cast<uint32_t>(rows);
+  PM_HIP_CHECK(hipMemcpyAsync(c.d_nS, &nrows, sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+  PM_HIP_CHECK(hipGetLastError());
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));  // (nrows lives on the host stack)
+  c.nS_host = nrows;
+  c.slist_compacted = true;
+  c.smask_valid = false;
+  c.k1_dense = false;
+  c.replicated = true;
 }
 
 }  // namespace pm

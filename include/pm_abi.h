@@ -176,6 +176,22 @@ int pm_run_beta_local_shards(const pm_graph_desc* graph, const char* pattern_dir
                              const uint64_t* labels, const char* result_dir, uint64_t max_iterations,
                              pm_run_stats* out);
 
+/* One shard of a sharded search over the R-MAT graph of generate_rmat, built on the device
+ * (collective over the nshards processes): shard q generates the edge streams of generator ranks
+ * r = q (mod nshards) (src/generate_rmat.cpp:202-213), every directed entry travels to its owner in
+ * one RCCL all-to-all -- the source's owner id % nshards, or for a delegate (global degree >=
+ * hub_threshold) the target's owner (delegate_partitioned_graph.ipp:818-969, 1402-1648) -- and
+ * the received entries are sorted into the shard's rows.  Same input as pm_create_rmat for every
+ * nshards.  gen_seconds (may be NULL): generation + exchange + row build. */
+pm_ctx* pm_create_rmat_shard(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nranks,
+                             uint64_t hub_threshold, uint32_t nshards, uint32_t shard, const uint8_t* unique_id,
+                             double* gen_seconds);
+/* The same with nshards shards driven by threads of this process on one device (in-process exchange):
+ * the whole sharded path -- generation, all-to-all, delegates, replica -- on a one-GPU box. */
+int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
+                             uint32_t nranks, uint64_t hub_threshold, const char* result_dir, uint64_t max_iterations,
+                             pm_run_stats* out);
+
 /* Host-side input builders (no device needed). */
 /* Directed pairs (u,v),(v,u) of generator ranks first, first + stride, ... < p_gen. */
 int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t stride, uint32_t** src, uint32_t** dst,

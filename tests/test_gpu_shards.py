@@ -41,10 +41,12 @@ def _check(so, sg):
     assert sg["walks"] == so["paths"]
 
 
-def _run_both(off, col, pattern, tmp_path, shards, labels=None, nranks=1, max_iterations=100):
+def _run_both(off, col, pattern, tmp_path, shards, labels=None, nranks=1, max_iterations=100,
+              hub_threshold=pm.DEFAULT_HUB_THRESHOLD):
     a, b = tmp_path / "oracle", tmp_path / "shards"
-    so = oracle.run(off, col, pattern, str(a), labels=labels, nranks=nranks, max_iterations=max_iterations)
-    g = pm.Graph(off, col, True, nranks)
+    so = oracle.run(off, col, pattern, str(a), labels=labels, nranks=nranks, max_iterations=max_iterations,
+                    hub_threshold=hub_threshold)
+    g = pm.Graph(off, col, True, nranks, hub_threshold)
     sg = pm.run_beta_local_shards(g, pattern, shards, str(b), max_iterations=max_iterations, labels=labels)
     return so, sg, pmtest.compare_result_dirs(str(a), str(b), nranks)
 
@@ -54,6 +56,25 @@ def test_sharded_rmat_matches_oracle(pat, scale, p_gen, alphabet, nranks, shards
     g = pm.rmat_graph(scale, p_gen)
     labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
     so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, shards, labels, nranks)
+    assert diffs == []
+    _check(so, sg)
+
+
+# delegates: rows of degree >= -d split over the shards by target owner, combined at the controller
+# (hub ordinal % shards); small thresholds so that hubs carry pattern labels (tree: label 7 = degree 64..127)
+DELEGATE_CASES = [
+    ("tree", 16, 4, 64, 4, 4),
+    ("tree", 15, 4, 100, 1, 3),
+    ("cycle", 13, 4, 16, 2, 2),
+    ("tree", 14, 1, 32, 3, 5),
+]
+
+
+@pytest.mark.parametrize("pat,scale,p_gen,thr,nranks,shards", DELEGATE_CASES)
+def test_sharded_delegates_match_oracle(pat, scale, p_gen, thr, nranks, shards, tmp_path):
+    g = pm.rmat_graph(scale, p_gen)
+    assert int((np.diff(g.off) >= thr).sum()) > 0  # some delegates
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, shards, None, nranks, hub_threshold=thr)
     assert diffs == []
     _check(so, sg)
 
@@ -100,6 +121,33 @@ def test_rccl_shard_single_rank(tmp_path):
     m = pm.ShardedPatternMatcher(g.n, g.off, g.col, deg, PATTERNS["tree"], 1, 0, uid, nranks=2)
     sg = m.run_beta(str(tmp_path / "rccl"), max_iterations=100)
     m.close()
+    so = oracle.run(g.off, g.col, PATTERNS["tree"], str(tmp_path / "oracle"), nranks=2, max_iterations=100)
+    assert pmtest.compare_result_dirs(str(tmp_path / "oracle"), str(tmp_path / "rccl"), 2) == []
+    _check(so, sg)
+
+
+# the GPU-generated sharded input (pm_run_rmat_local_shards): each shard draws its generator
+# ranks' streams on the device, the entries reach their owners (delegates by target) in one
+# all-to-all; results equal the oracle's on the one-GPU graph for every shard count
+@pytest.mark.parametrize("scale,p_gen,shards,thr,nranks", [(14, 4, 2, pm.DEFAULT_HUB_THRESHOLD, 1),
+                                                           (15, 4, 4, 64, 4), (14, 8, 3, 48, 2)])
+def test_gpu_generated_shards_match_oracle(scale, p_gen, shards, thr, nranks, tmp_path):
+    g = pm.rmat_graph(scale, p_gen)
+    a, b = tmp_path / "oracle", tmp_path / "shards"
+    so = oracle.run(g.off, g.col, PATTERNS["tree"], str(a), nranks=nranks, hub_threshold=thr, max_iterations=100)
+    sg = pm.run_rmat_local_shards(scale, p_gen, PATTERNS["tree"], shards, str(b), max_iterations=100, nranks=nranks,
+                                  hub_threshold=thr)
+    assert pmtest.compare_result_dirs(str(a), str(b), nranks) == []
+    _check(so, sg)
+
+
+def test_rccl_rmat_shard_single_rank(tmp_path):
+    # pm_create_rmat_shard with one RCCL rank: the bench's N-GPU construction path at N = 1
+    uid = pm.comm_unique_id()
+    m, secs = pm.rmat_shard_matcher(14, 4, PATTERNS["tree"], 1, 0, uid, nranks=2)
+    sg = m.run_beta(str(tmp_path / "rccl"), max_iterations=100)
+    m.close()
+    g = pm.rmat_graph(14, 4)
     so = oracle.run(g.off, g.col, PATTERNS["tree"], str(tmp_path / "oracle"), nranks=2, max_iterations=100)
     assert pmtest.compare_result_dirs(str(tmp_path / "oracle"), str(tmp_path / "rccl"), 2) == []
     _check(so, sg)
