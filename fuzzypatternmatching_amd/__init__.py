@@ -143,12 +143,14 @@ def rmat_edges(scale, p_gen, first=0, stride=1):
     return out[0], out[1]
 
 
-def partition_edges(src, dst, n, group=None, device="cpu"):
-    """Owner partitioning of a distributed edge list (delegate_partitioned_graph.ipp:818-969
-    without delegates): every process holds some directed edges; they are exchanged with one
-    all-to-all so that process q receives the edges whose source v has v % world == q.
+def partition_edges(src, dst, n, group=None, device="cpu", hub_threshold=DEFAULT_HUB_THRESHOLD):
+    """Owner partitioning of a distributed edge list, the host form of what pm_create_rmat_shard does
+    on the GPUs (delegate_partitioned_graph.ipp:818-969, 1402-1648): every process holds some directed
+    edges; the global out-degrees are summed over the processes, then every edge (u, v) goes in one
+    all-to-all to the owner of u (u % world), or, when u is a delegate (global degree >=
+    hub_threshold, more than one process), to the owner of v.
 
-    Returns (off[n+1] u64 by id -- other owners' rows empty, col u32 sorted within each row,
+    Returns (off[n+1] u64 by id -- rows held elsewhere empty, col u32 sorted within each row,
     degree[n] u32 global degrees).  Collective over `group` (gloo on CPU, nccl = RCCL on GPU)."""
     import torch
     import torch.distributed as dist
@@ -156,13 +158,16 @@ def partition_edges(src, dst, n, group=None, device="cpu"):
     # u32 ids travel as int32 and widen on the device
     s = torch.from_numpy(np.ascontiguousarray(src, dtype=np.uint32).view(np.int32)).to(device).long() & 0xFFFFFFFF
     d = torch.from_numpy(np.ascontiguousarray(dst, dtype=np.uint32).view(np.int32)).to(device).long() & 0xFFFFFFFF
+    # global out-degrees (scatter-add of this process's sources, summed over the processes)
+    gdeg = torch.zeros(n, dtype=torch.int32, device=device).index_add_(
+        0, s, torch.ones(s.shape[0], dtype=torch.int32, device=device))
+    dist.all_reduce(gdeg, group=group)
     if G == 1:  # nothing to exchange
         rs, rd = s, d
     else:
-        owner = s % G
+        owner = torch.where(gdeg[s] >= hub_threshold, d, s) % G
         order = torch.argsort(owner, stable=True)
         s, d, owner = s[order], d[order], owner[order]
-        # counts by scatter-add (torch.bincount of constant data raised SIGFPE on this image)
         send = torch.zeros(G, dtype=torch.int64, device=device).index_add_(0, owner, torch.ones_like(owner))
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=group)
@@ -178,9 +183,6 @@ def partition_edges(src, dst, n, group=None, device="cpu"):
     del key
     deg = torch.zeros(n, dtype=torch.int32, device=device).index_add_(
         0, rs, torch.ones(rs.shape[0], dtype=torch.int32, device=device))
-    gdeg = deg.clone()
-    if G > 1:  # (a one-rank RCCL all-reduce of a large buffer raises SIGFPE on this image)
-        dist.all_reduce(gdeg, group=group)
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(deg.cpu().numpy().astype(np.uint64))
     return off, rd.to(torch.int32).cpu().numpy().view(np.uint32).copy(), gdeg.cpu().numpy().view(np.uint32).copy()

@@ -259,7 +259,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_tst = dalloc<uint16_t>(c->n);
   c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
   if (c->dcap) {
-    c->d_dmoff = dalloc<uint32_t>(c->n);
+    c->d_s0rec = dalloc<uint64_t>(c->n);
   }
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
@@ -327,7 +327,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_slist2, c->d_nS2, c->d_ccnt, c->d_cbase, c->d_ctmp, c->d_smask[0], c->d_smask[1], c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_dmoff, c->d_xsend, c->d_xrecv, c->d_xent_send,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_s0rec, c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart,
                   };
   for (void* p : ptrs)
@@ -1306,6 +1306,72 @@ pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, 
   }
 }
 
+}  // extern "C"
+
+namespace pm {
+// HBM copy bandwidth (the measured ceiling beside the 8 TB/s datasheet peak): 16-B nontemporal loads
+// and stores, four in flight per lane, a grid of resident blocks.
+typedef uint32_t cp_u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copy16(const cp_u32x4* __restrict__ src, cp_u32x4* __restrict__ dst,
+                                                uint64_t n) {
+  const uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  if (i >= n) return;
+  if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  else dst[i] = src[i];
+}
+}  // namespace pm
+
+extern "C" {
+int pm_debug_copy_gbs(int device, uint64_t bytes, int reps, double* gbs) {
+  void *a = nullptr, *b = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  try {
+    pm::require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    const uint64_t n = std::max<uint64_t>(bytes / 16, 1);
+    PM_HIP_CHECK(hipMalloc(&a, n * 16));
+    PM_HIP_CHECK(hipMalloc(&b, n * 16));
+    PM_HIP_CHECK(hipMemset(a, 1, n * 16));
+    PM_HIP_CHECK(hipEventCreate(&e0));
+    PM_HIP_CHECK(hipEventCreate(&e1));
+    // one 16-B element per thread, the whole buffer in one grid; the faster of plain and nontemporal
+    const unsigned grid = static_cast<unsigned>((n + 255) / 256);
+    float best = 0.f;
+    for (int nt = 0; nt < 2; ++nt) {
+      auto launch = [&] {
+        if (nt)
+          hipLaunchKernelGGL(pm::k_copy16<true>, dim3(grid), dim3(256), 0, 0, static_cast<const pm::cp_u32x4*>(a),
+                             static_cast<pm::cp_u32x4*>(b), n);
+        else
+          hipLaunchKernelGGL(pm::k_copy16<false>, dim3(grid), dim3(256), 0, 0, static_cast<const pm::cp_u32x4*>(a),
+                             static_cast<pm::cp_u32x4*>(b), n);
+      };
+      launch();  // warm
+      PM_HIP_CHECK(hipEventRecord(e0, 0));
+      for (int r = 0; r < std::max(reps, 1); ++r) launch();
+      PM_HIP_CHECK(hipEventRecord(e1, 0));
+      PM_HIP_CHECK(hipEventSynchronize(e1));
+      float t = 0.f;
+      PM_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+      if (best == 0.f || t < best) best = t;
+    }
+    const float ms = best;
+    if (gbs) *gbs = 2.0 * n * 16 * std::max(reps, 1) / (ms * 1e-3) / 1e9;  // read + write bytes
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return 0;
+  } catch (const std::exception& e) {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
 }  // extern "C"
 
 namespace pm {

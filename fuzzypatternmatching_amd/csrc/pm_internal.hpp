@@ -276,6 +276,7 @@ struct Ctx {
   uint32_t* d_rmcol = nullptr;    // replica: M rows, packed
   uint64_t rmcap = 0;             // entries of d_rmcol
   bool xcode_wide = false;        // some label has more than two template vertices: the exchange carries T_pub
+  bool xcode_in_tpub = false;     // ... and it landed in T_pub (no superstep-0 records): cleared after superstep 1
   void* d_xsend = nullptr;        // exchange buffers (grown on demand)
   void* d_xrecv = nullptr;
   void* d_xent_send = nullptr;
@@ -338,13 +339,15 @@ struct Ctx {
   uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile
   uint64_t* d_tbase = nullptr;    // exclusive scan of the per-tile survivor counts
   uint32_t* d_tcode = nullptr;   // superstep-0 T_pub in 2 bits per position (k_lcc_first -> first later superstep)
-  // dense superstep-0 M (one shard, symmetric graph, diameter >= 2): light tiles
-  // append their contributors to their wave's slice of the region [dbase, dbase + dcap) of d_mcol and
-  // d_dmoff[u] gives survivor u's first entry there (kNone: M in u's padded
-  // row); the first later superstep reads M densely and writes the rows of its
+  // dense superstep-0 M (symmetric graph, diameter >= 2): light tiles append
+  // their contributors to their wave's slice of the region [dbase, dbase + dcap)
+  // of d_mcol, and every survivor u gets one record d_s0rec[u] = T_pub | |M| << 16
+  // | first entry << 32 (first entry kNone: M in u's padded row, T_state / |M| in
+  // their arrays) instead of scattered T_pub / |M| / offset stores; the first
+  // later superstep reads the records and M densely and writes the rows of its
   // survivors into their padded rows
   uint64_t dbase = 0, dcap = 0;
-  uint32_t* d_dmoff = nullptr;
+  uint64_t* d_s0rec = nullptr;
   bool k1_dense = false;         // the last superstep-0 launch wrote dense M
   uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile

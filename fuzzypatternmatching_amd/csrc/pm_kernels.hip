@@ -164,7 +164,7 @@ struct K1Out {
   uint32_t* tcnt;    // per tile: survivors
   uint32_t* tstart;  // per tile: position of row 0 (light) or the heavy row
   uint32_t* tcode;   // T_pub in 2 bits per position (tpub_code), OR-ed in
-  uint32_t* dmoff;   // dense M: survivor's first entry in mcol[dbase..] (null: M in padded rows)
+  unsigned long long* rec;  // dense M: per survivor T | |M| << 16 | first entry in mcol[dbase..] << 32 (null: no dense M)
   uint64_t dbase;    // dense M: first entry of the region in mcol
   uint64_t dslice;   // dense M: entries of the region owned by each wave of the grid
 };
@@ -256,11 +256,12 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
   // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
   const uint32_t b2 = u * 2u, b4 = u * 4u;
   *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
-  *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = len;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
   atomicOr(&o.tcode[u >> 4], tpub_code(T, tu) << ((u & 15u) << 1));
-  if (o.dmoff) o.dmoff[u] = kNone;  // a heavy row's M stays in its padded row
+  // dense mode: T_pub in the record (a heavy row's M stays in its padded row: no first entry)
+  if (o.rec) o.rec[u] = T | (static_cast<unsigned long long>(kNone) << 32);
+  else *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
   if (oa.nranks <= 1) {
     acc.vs += 1;
     acc.es += cnt;
@@ -603,23 +604,24 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
                                          uint64_t dend) {
   const int lane = lane_id();
   if (!p.tm) return;
-  if (!(MODE & 64) && lane < kSub)
-    p.tm[lane] = static_cast<uint32_t>(lane) < p.ngroups ? st.sm[lane] : 0ull;  // bit r = row r
   if (lane == 0) {
     o.tcnt[p.tile] = p.any;
     o.tstart[p.tile] = p.ustart;
   }
   if (!p.any) {
-    // no survivor: the half words of verified rows are already 0
+    // no survivor: the half words of verified rows are already 0; the slist build reads no mask word of a
+    // tile without survivors
     return;
   }
+  // the mask words that hold survivors (the slist build stops at the tile's count)
+  if (!(MODE & 64) && static_cast<uint32_t>(lane) < p.ngroups) p.tm[lane] = st.sm[lane];  // bit r = row r
   // dense M: the tile's whole contributor list is appended to the wave's own
   // slice of the region (coalesced; a cursor in scalar registers, no atomics:
   // one counter shared by the grid serialised 2.5 M atomics and cost 20 ms),
   // survivor u's M starts at list index hd[row] of it; a tile that no longer
   // fits the slice keeps the padded-row layout
   const uint64_t dpos = dcur;
-  const bool dense = o.dmoff && dcur + p.nlist <= dend;
+  const bool dense = o.rec && dcur + p.nlist <= dend;
   if (dense) dcur += p.nlist;
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
 #pragma unroll 1
@@ -634,16 +636,20 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
       if (!(MODE & 128)) {
         // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
         const uint32_t u = p.ustart + row, b2 = u * 2u, b4 = u * 4u;
-        // a dense row's T_state (= T_pub) and |M| (= its length) are implied: the first later
-        // superstep, the only reader before they are rewritten, takes them from T_pub and mlen
-        if (!dense) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
-        *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
-        if (!dense) *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+        // dense: one 8-B record (T_pub, |M|, first entry); T_state (= T_pub) and the alive count (= |M|)
+        // are implied: the first later superstep, the only reader before they are rewritten, takes them
+        // from the record.  A tile outside the region: the state arrays (T_pub still in the record)
+        if (dense) {
+          o.rec[u] = T | (static_cast<unsigned long long>(cnt) << 16) |
+                     (static_cast<unsigned long long>(dpos + st.hd[row]) << 32);
+        } else {
+          *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+          if (o.rec) o.rec[u] = T | (static_cast<unsigned long long>(kNone) << 32);
+          else *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+        }
         atomicOr(&o.tcode[u >> 4], tpub_code(T, p.tu) << ((u & 15u) << 1));
-        if (o.dmoff)
-          *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.dmoff) + b4) =
-              dense ? static_cast<uint32_t>(dpos + st.hd[row]) : kNone;
       }
     }
   }
@@ -720,7 +726,7 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
       surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
     }
   }
-  if (lane < kSub && !(MODE & 8)) tm[lane] = (lane == 0 && surv) ? 1ull : 0ull;
+  if (lane == 0 && surv && !(MODE & 8)) tm[0] = 1ull;  // (read only when the tile count is 1)
   if (lane == 0 && !(MODE & 8)) {
     o.tcnt[hs.tile] = surv ? 1u : 0u;
     o.tstart[hs.tile] = hs.row;
@@ -896,7 +902,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
-    const uint32_t* __restrict__ dmoff, uint64_t dbase) {
+    const unsigned long long* __restrict__ rec, uint64_t dbase) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -924,7 +930,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     for (int l = 0; l < nruns; ++l)
       if (p - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
     const uint32_t rest = tu & (tu - 1);
-    if (rest & (rest - 1)) return tcur[p];
+    if (rest & (rest - 1)) return rec ? static_cast<uint16_t>(rec[p]) : tcur[p];
     return static_cast<uint16_t>(((code & 1u) ? (tu & (0u - tu)) : 0u) | ((code & 2u) ? rest : 0u));
   };
   BlockAcc acc;
@@ -944,11 +950,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
       u = slist[i];
       // the row's state is loaded with T_pub in one round trip (a removed
       // row, T_pub = 0, ignores it)
-      Tu = tcur[u];
-      const uint32_t l = mlen[u];
-      const uint32_t dm = dmoff ? dmoff[u] : kNone;
+      uint32_t l, dm = kNone;
+      if (rec) {  // dense superstep-0 output: the record (T_pub, |M|, first entry) of u
+        const unsigned long long r = rec[u];
+        Tu = static_cast<uint16_t>(r);
+        dm = static_cast<uint32_t>(r >> 32);
+        l = dm != kNone ? static_cast<uint32_t>(r >> 16) & 0xFFFFu : mlen[u];
+      } else {
+        Tu = tcur[u];
+        l = mlen[u];
+      }
       // a dense superstep-0 row: T_state = T_pub, |M| = its length, and its padded row start is
-      // needed only if it survives (three scattered loads instead of six per row)
+      // needed only if it survives (one scattered load instead of six per row)
       uint64_t b = 0;
       uint32_t a0 = l;
       if (dm == kNone) {
@@ -1057,7 +1070,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
       }
     }
     bool survivor = false, removed = false, cleared = false;
-    if (dmoff) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
+    if (rec) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
     if (Tu) {
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
@@ -1069,6 +1082,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         if (drow) {
           pb = offp[u];
           for (uint32_t j = 0; j < len; ++j) mcol[pb + j] = mcol[beg + j];
+          mlen[u] = len;
         }
       } else {
         removed = true;
@@ -1674,7 +1688,7 @@ void build_tiling(Ctx& c) {
 
 static K1Out k1_out(Ctx& c, unsigned grid) {
   return K1Out{c.d_tst,   c.d_tpub[c.cur], c.d_mcol,  c.d_mlen, c.d_malive, c.d_tcnt,
-               c.d_tstart, c.d_tcode,      c.k1_dense ? c.d_dmoff : nullptr, c.dbase,
+               c.d_tstart, c.d_tcode,      c.k1_dense ? reinterpret_cast<unsigned long long*>(c.d_s0rec) : nullptr, c.dbase,
                c.dcap / (uint64_t(std::max(grid, 1u)) * kWpb)};
 }
 
@@ -1690,6 +1704,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
       if (c.k1_wide) hipLaunchKernelGGL((k_lcc_first<0, true>), PM_K1_ARGS);
       else hipLaunchKernelGGL(k_lcc_first<0>, PM_K1_ARGS);
       break;
+#ifdef PM_DIAG_VARIANTS  // ablation builds of the kernel: lib/libpm_diag.so only (make diag; tools/k1_*.py)
     case 1: hipLaunchKernelGGL(k_lcc_first<1>, PM_K1_ARGS); break;
     case 2: hipLaunchKernelGGL(k_lcc_first<2>, PM_K1_ARGS); break;
     case 4: hipLaunchKernelGGL(k_lcc_first<4>, PM_K1_ARGS); break;
@@ -1701,7 +1716,8 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 80: hipLaunchKernelGGL(k_lcc_first<80>, PM_K1_ARGS); break;
     case 128: hipLaunchKernelGGL(k_lcc_first<128>, PM_K1_ARGS); break;
     case 5: hipLaunchKernelGGL((k_lcc_first<0, false, 5>), PM_K1_ARGS); break;  // 5 waves/SIMD, no spills
-    default: throw std::runtime_error("unknown superstep-0 kernel variant");
+#endif
+    default: throw std::runtime_error("unknown superstep-0 kernel variant (ablation variants: lib/libpm_diag.so)");
   }
 #undef PM_K1_ARGS
   PM_HIP_CHECK(hipGetLastError());
@@ -1797,7 +1813,9 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
-                     c.diag_step, first_after_ss0 && c.k1_dense ? c.d_dmoff : nullptr, c.dbase);
+                     c.diag_step,
+                     first_after_ss0 && c.k1_dense ? reinterpret_cast<const unsigned long long*>(c.d_s0rec) : nullptr,
+                     c.dbase);
   PM_HIP_CHECK(hipGetLastError());
   c.k1_dense = false;  // every M row of S is in its padded row from here on
   reduce_into(c, grid, d_slot);

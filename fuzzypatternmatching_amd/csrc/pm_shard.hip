@@ -277,13 +277,15 @@ __global__ void k_count_to_u64(const uint32_t* __restrict__ n, uint64_t* __restr
 // (2-bit tpub_code), or, when some label has more than two template vertices
 // (its code 3 means "gather T_pub"), position | T_pub << 32 | code << 62.
 __global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
-                             const uint32_t* __restrict__ tcode, const uint16_t* __restrict__ tpub, int wide,
-                             uint32_t* __restrict__ out32, unsigned long long* __restrict__ out64) {
+                             const uint32_t* __restrict__ tcode, const uint16_t* __restrict__ tpub,
+                             const unsigned long long* __restrict__ rec, int wide, uint32_t* __restrict__ out32,
+                             unsigned long long* __restrict__ out64) {
   const uint64_t n = *nSp;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t p = slist[i];
     const uint32_t code = (tcode[p >> 4] >> ((p & 15u) << 1)) & 3u;
-    if (wide) out64[i] = p | (static_cast<unsigned long long>(tpub[p]) << 32) | (static_cast<unsigned long long>(code) << 62);
+    const uint16_t T = rec ? static_cast<uint16_t>(rec[p]) : tpub[p];  // dense superstep 0: T_pub in the record
+    if (wide) out64[i] = p | (static_cast<unsigned long long>(T) << 32) | (static_cast<unsigned long long>(code) << 62);
     else out32[i] = p | (code << 30);
   }
 }
@@ -291,7 +293,7 @@ __global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t*
 // The other shards' code records into this shard's 2-bit codes (and T_pub).
 __global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned long long* __restrict__ in64,
                                uint64_t maxS, uint32_t G, uint32_t me, XCounts x, uint32_t* __restrict__ tcode,
-                               uint16_t* __restrict__ tpub) {
+                               uint16_t* __restrict__ tpub, unsigned long long* __restrict__ rec) {
   const uint64_t total = uint64_t(G) * maxS;
   for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t g = static_cast<uint32_t>(j / maxS);
@@ -301,7 +303,9 @@ __global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned
       const unsigned long long r = in64[j];
       p = static_cast<uint32_t>(r & 0x3FFFFFFFull);
       code = static_cast<uint32_t>(r >> 62);
-      tpub[p] = static_cast<uint16_t>(r >> 32);
+      // where the next superstep's gathers look up a code-3 T_pub (k_lcc_step tpub_of)
+      if (rec) rec[p] = (r >> 32) & 0xFFFFull;
+      else tpub[p] = static_cast<uint16_t>(r >> 32);
     } else {
       p = in32[j] & 0x3FFFFFFFu;
       code = in32[j] >> 30;
@@ -323,10 +327,8 @@ __global__ void k_clear_codes(const unsigned long long* __restrict__ in64, uint6
 }
 
 // pack_state, pass 1: per slist entry whether it is in S and its alive M count.
-// A dense superstep-0 row (dmoff != kNone) holds only alive entries; T_state = T_pub there.
 __global__ void k_pack_count(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp, uint64_t cap,
-                             const uint16_t* __restrict__ tpub, const uint32_t* __restrict__ mlen,
-                             const uint32_t* __restrict__ malive, const uint32_t* __restrict__ dmoff,
+                             const uint16_t* __restrict__ tpub, const uint32_t* __restrict__ malive,
                              uint32_t* __restrict__ keep, uint32_t* __restrict__ cnt) {
   const uint64_t n = min(static_cast<uint64_t>(*nSp), cap);
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < cap; i += uint64_t(gridDim.x) * blockDim.x) {
@@ -335,7 +337,7 @@ __global__ void k_pack_count(const uint32_t* __restrict__ slist, const uint32_t*
       const uint32_t u = slist[i];
       if (tpub[u]) {
         k = 1;
-        m = (dmoff && dmoff[u] != kNone) ? mlen[u] : malive[u];
+        m = malive[u];
       }
     }
     keep[i] = k;
@@ -349,8 +351,8 @@ __global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t*
                              const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ eoff,
                              const uint16_t* __restrict__ tpub, const uint16_t* __restrict__ tst,
                              const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ moff,
-                             const uint32_t* __restrict__ mcol, const uint32_t* __restrict__ dmoff, uint64_t dbase,
-                             uint32_t* __restrict__ rec, uint32_t* __restrict__ ent, uint64_t ent_cap,
+                             const uint32_t* __restrict__ mcol, uint32_t* __restrict__ rec, uint32_t* __restrict__ ent,
+                             uint64_t ent_cap,
                              unsigned long long* __restrict__ totals) {
   const uint64_t n = min(static_cast<uint64_t>(*nSp), cap);
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
@@ -360,14 +362,13 @@ __global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t*
     }
     if (!keep[i] || !rec) continue;
     const uint32_t u = slist[i];
-    const bool dense = dmoff && dmoff[u] != kNone;
-    const uint64_t b = dense ? dbase + dmoff[u] : moff[u];
+    const uint64_t b = moff[u];
     const uint32_t L = mlen[u];
     const uint16_t T = tpub[u];
     const uint64_t e0 = eoff[i];
     uint32_t* r = rec + 4 * uint64_t(ridx[i]);
     r[0] = u;
-    r[1] = T | (static_cast<uint32_t>(dense ? T : tst[u]) << 16);
+    r[1] = T | (static_cast<uint32_t>(tst[u]) << 16);
     r[2] = cnt[i];
     r[3] = static_cast<uint32_t>(e0);
     uint64_t k = e0;
@@ -467,7 +468,7 @@ struct HubFinishArgs {
   uint32_t* mlen;
   uint32_t* malive;
   uint32_t* tcode;
-  uint32_t* dmoff;                    // dense superstep-0 M in use: the hub's row is not dense (kNone)
+  unsigned long long* rec;            // dense superstep-0 M in use: the hub's record (its row is not dense)
   uint32_t* mcol;
   uint32_t* slist;
   uint32_t* nS;
@@ -506,7 +507,7 @@ __global__ void k_hub_finish(HubFinishArgs a) {
         a.mlen[p] = static_cast<uint32_t>(cnt);
         a.malive[p] = static_cast<uint32_t>(cnt);
         atomicOr(&a.tcode[p >> 4], tpub_code(T, tu) << ((p & 15u) << 1));
-        if (a.dmoff) a.dmoff[p] = kNone;
+        if (a.rec) a.rec[p] = T | (static_cast<unsigned long long>(kNone) << 32);
         a.slist[atomicAdd(a.nS, 1u)] = p;
         const uint32_t r = a.nranks <= 1 ? 0u : j % a.nranks;  // owner rule of a delegate
         atomicAdd(&a.slot[r], 1ull);
@@ -630,7 +631,7 @@ void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
   a.mlen = c.d_mlen;
   a.malive = c.d_malive;
   a.tcode = c.d_tcode;
-  a.dmoff = c.k1_dense ? c.d_dmoff : nullptr;
+  a.rec = c.k1_dense ? reinterpret_cast<unsigned long long*>(c.d_s0rec) : nullptr;
   a.mcol = c.d_mcol;
   a.slist = c.d_slist;
   a.nS = c.d_nS;
@@ -655,8 +656,9 @@ void shard_codes_after_first(Ctx& c) {
   const size_t rb = c.xcode_wide ? 8 : 4;
   auto* send = grow<char>(c.d_xsend, c.xsend_cap, maxS * rb);
   auto* recv = grow<char>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxS * rb);
+  auto* rec = c.k1_dense ? reinterpret_cast<unsigned long long*>(c.d_s0rec) : nullptr;
   hipLaunchKernelGGL(k_pack_codes, dim3(xgrid(c.nS_host)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tcode,
-                     c.d_tpub[c.cur], c.xcode_wide ? 1 : 0, reinterpret_cast<uint32_t*>(send),
+                     c.d_tpub[c.cur], rec, c.xcode_wide ? 1 : 0, reinterpret_cast<uint32_t*>(send),
                      reinterpret_cast<unsigned long long*>(send));
   c.comm->allgather(send, recv, maxS * rb, c.stream);
   XCounts x{};
@@ -664,7 +666,8 @@ void shard_codes_after_first(Ctx& c) {
   hipLaunchKernelGGL(k_unpack_codes, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream,
                      c.xcode_wide ? nullptr : reinterpret_cast<const uint32_t*>(recv),
                      c.xcode_wide ? reinterpret_cast<const unsigned long long*>(recv) : nullptr, maxS, G, c.shard, x,
-                     c.d_tcode, c.d_tpub[c.cur]);
+                     c.d_tcode, c.d_tpub[c.cur], rec);
+  c.xcode_in_tpub = c.xcode_wide && !rec;
   PM_HIP_CHECK(hipGetLastError());
 }
 
@@ -682,7 +685,8 @@ uint64_t pack_state_entry_bound(Ctx& c) {
 
 void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t* counts) {
   const uint64_t cap = c.nS_host;
-  const uint32_t* dmoff = c.k1_dense ? c.d_dmoff : nullptr;
+  // (the state right after superstep 0 is never packed: with dense M the first later superstep follows)
+  if (c.k1_dense) throw std::runtime_error("internal: pack_state of a dense superstep-0 state");
   c.arena.reset();
   auto* keep = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
   auto* cnt = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
@@ -691,7 +695,7 @@ void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t
   PM_HIP_CHECK(hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), c.stream));
   if (!cap) return;
   hipLaunchKernelGGL(k_pack_count, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap,
-                     c.d_tpub[c.cur], c.d_mlen, c.d_malive, dmoff, keep, cnt);
+                     c.d_tpub[c.cur], c.d_malive, keep, cnt);
   size_t t1 = 0, t2 = 0;
   PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, t1, keep, ridx, 0u, size_t(cap), rocprim::plus<uint32_t>(), c.stream));
   rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> wc(cnt, Widen());
@@ -703,8 +707,8 @@ void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t
                                        c.stream));
   // rec == nullptr: totals only (the rows are not written)
   hipLaunchKernelGGL(k_pack_write, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap, keep,
-                     ridx, cnt, eoff, c.d_tpub[c.cur], c.d_tst, c.d_mlen, m_off(c), m_col(c), dmoff, c.dbase,
-                     rec, ent, rec ? ent_cap : 0, reinterpret_cast<unsigned long long*>(counts));
+                     ridx, cnt, eoff, c.d_tpub[c.cur], c.d_tst, c.d_mlen, m_off(c), m_col(c), rec, ent,
+                     rec ? ent_cap : 0, reinterpret_cast<unsigned long long*>(counts));
   PM_HIP_CHECK(hipGetLastError());
 }
 
@@ -715,7 +719,7 @@ void shard_replicate(Ctx& c) {
   XCounts x{};
   // u64 code mode: the other shards' T_pub that superstep 0's buffer received (the superstep that
   // read it is done; the buffer becomes the next superstep's output)
-  if (c.xcode_wide && !c.xcode_n.empty()) {
+  if (c.xcode_in_tpub && !c.xcode_n.empty()) {
     for (uint32_t g = 0; g < G; ++g) x.n[g] = c.xcode_n[g];
     hipLaunchKernelGGL(k_clear_codes, dim3(xgrid(uint64_t(G) * c.xcode_max)), dim3(kXBlock), 0, c.stream,
                        reinterpret_cast<const unsigned long long*>(c.d_xrecv), c.xcode_max, G, c.shard, x,

@@ -232,6 +232,9 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out);
 /* Diagnostics: a one-rank RCCL collective of `bytes` (op 0 ncclAllGather, 1 ncclAllReduce u64 sum),
    result checked: 0 = right, 1 = wrong, -1 = error (pm_last_error). */
 int pm_debug_rccl_selftest(int device, uint64_t bytes, int op);
+/* Diagnostics: HBM copy bandwidth of a 16-B nontemporal copy kernel over two `bytes` buffers (read + write
+   bytes per second / 1e9), the measured ceiling beside the datasheet peak. */
+int pm_debug_copy_gbs(int device, uint64_t bytes, int reps, double* gbs);
 /* Diagnostics: superstep-0 tiling statistics (real entries, loaded slots, rows, tiles, ranges, heavy rows). */
 int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n);
 

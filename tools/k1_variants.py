@@ -8,6 +8,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the ablation variants live in the diagnostics build (make -C fuzzypatternmatching_amd/csrc diag)
+os.environ.setdefault("PM_LIB", os.path.join(ROOT, "fuzzypatternmatching_amd", "lib", "libpm_diag.so"))
 sys.path.insert(0, ROOT)
 import fuzzypatternmatching_amd as pm  # noqa: E402
 from fuzzypatternmatching_amd import _abi  # noqa: E402
