@@ -339,15 +339,28 @@ struct Ctx {
   uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile
   uint64_t* d_tbase = nullptr;    // exclusive scan of the per-tile survivor counts
   uint32_t* d_tcode = nullptr;   // superstep-0 T_pub in 2 bits per position (k_lcc_first -> first later superstep)
-  // dense superstep-0 M (symmetric graph, diameter >= 2): light tiles append
+  // dense superstep-0 output (symmetric graph, diameter >= 2): light tiles append
   // their contributors to their wave's slice of the region [dbase, dbase + dcap)
-  // of d_mcol, and every survivor u gets one record d_s0rec[u] = T_pub | |M| << 16
-  // | first entry << 32 (first entry kNone: M in u's padded row, T_state / |M| in
-  // their arrays) instead of scattered T_pub / |M| / offset stores; the first
-  // later superstep reads the records and M densely and writes the rows of its
-  // survivors into their padded rows
+  // of d_mcol, and their survivors' 16-B records {position, T_pub | |M| << 16,
+  // first entry (kNone: M in the padded row, state in its arrays), 0} to the
+  // wave's slice of d_rarea (bounded by the rows of the wave's tiles, d_rbase);
+  // heavy rows to d_hrec.  The slist and the slist-aligned records d_srec are
+  // built from them; the first later superstep reads d_srec and M densely and
+  // writes the rows of its survivors into their padded rows.  Nothing is stored
+  // by position except the 2-bit codes (and T_pub of labels of more than two
+  // template vertices).
   uint64_t dbase = 0, dcap = 0;
-  uint64_t* d_s0rec = nullptr;
+  uint4* d_rarea = nullptr;       // record slices of the superstep-0 waves
+  uint64_t* d_rbase = nullptr;    // first record of each wave's slice (k1_grid * kWpb + 1)
+  uint32_t* d_rcnt = nullptr;     // records each wave wrote
+  uint64_t* d_rofs = nullptr;     // exclusive scan of d_rcnt
+  uint4* d_hrec = nullptr;        // heavy rows' records (w = 1: survivor)
+  uint4* d_srec = nullptr;        // records in slist order (the first later superstep)
+  uint64_t rarea_cap = 0, srec_cap = 0;
+  uint32_t rwaves = 0;            // waves of the superstep-0 grid the slices were sized for
+  void* d_rscan_tmp = nullptr;
+  size_t rscan_tmp_bytes = 0;
+  bool k1_records = false;        // the last superstep-0 launch wrote records (and no tile masks)
   bool k1_dense = false;         // the last superstep-0 launch wrote dense M
   uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile

@@ -164,7 +164,14 @@ struct K1Out {
   uint32_t* tcnt;    // per tile: survivors
   uint32_t* tstart;  // per tile: position of row 0 (light) or the heavy row
   uint32_t* tcode;   // T_pub in 2 bits per position (tpub_code), OR-ed in
-  unsigned long long* rec;  // dense M: per survivor T | |M| << 16 | first entry in mcol[dbase..] << 32 (null: no dense M)
+  // dense M: survivor records {position, T_pub | |M| << 16, first entry in mcol[dbase..] (kNone: M in the
+  // padded row, T_state / |M| / alive count in their arrays), 0}, appended to the wave's slice of rarea
+  // (rbase[w] .. + its rows bound; count to rcnt[w]); heavy rows to hrec[h] (w = 1: survivor).  Null: no
+  // dense M (tile masks, position-indexed state)
+  uint4* rarea;
+  const uint64_t* rbase;
+  uint32_t* rcnt;
+  uint4* hrec;
   uint64_t dbase;    // dense M: first entry of the region in mcol
   uint64_t dslice;   // dense M: entries of the region owned by each wave of the grid
 };
@@ -259,9 +266,9 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = len;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
   atomicOr(&o.tcode[u >> 4], tpub_code(T, tu) << ((u & 15u) << 1));
-  // dense mode: T_pub in the record (a heavy row's M stays in its padded row: no first entry)
-  if (o.rec) o.rec[u] = T | (static_cast<unsigned long long>(kNone) << 32);
-  else *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+  // dense mode: T_pub in the record (a heavy row's M stays in its padded row: no first entry); a
+  // label of more than two template vertices also keeps its position-indexed T_pub (code 3 gathers)
+  if (!o.rarea || tpub_code(T, tu) == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
   if (oa.nranks <= 1) {
     acc.vs += 1;
     acc.es += cnt;
@@ -601,10 +608,10 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
 // TN words zero.
 template <int MODE>
 __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stage& st, uint64_t& dcur,
-                                         uint64_t dend) {
+                                         uint64_t dend, uint64_t& rcur) {
   const int lane = lane_id();
   if (!p.tm) return;
-  if (lane == 0) {
+  if (lane == 0 && !o.rarea) {  // (dense mode: the slist comes from the records)
     o.tcnt[p.tile] = p.any;
     o.tstart[p.tile] = p.ustart;
   }
@@ -614,20 +621,22 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
     return;
   }
   // the mask words that hold survivors (the slist build stops at the tile's count)
-  if (!(MODE & 64) && static_cast<uint32_t>(lane) < p.ngroups) p.tm[lane] = st.sm[lane];  // bit r = row r
+  if (!(MODE & 64) && !o.rarea && static_cast<uint32_t>(lane) < p.ngroups) p.tm[lane] = st.sm[lane];  // bit r = row r
   // dense M: the tile's whole contributor list is appended to the wave's own
   // slice of the region (coalesced; a cursor in scalar registers, no atomics:
   // one counter shared by the grid serialised 2.5 M atomics and cost 20 ms),
   // survivor u's M starts at list index hd[row] of it; a tile that no longer
   // fits the slice keeps the padded-row layout
   const uint64_t dpos = dcur;
-  const bool dense = o.rec && dcur + p.nlist <= dend;
+  const bool dense = o.rarea && dcur + p.nlist <= dend;
   if (dense) dcur += p.nlist;
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
 #pragma unroll 1
   for (uint32_t gi = 0; gi < p.ngroups; ++gi) {
     const uint64_t m = uniform64(st.sm[gi]);
     if (!m) continue;
+    const uint64_t rslot = rcur + __builtin_popcountll(m & ((1ull << lane) - 1));
+    if (o.rarea) rcur = uniform64(rcur + __builtin_popcountll(m));
     if ((m >> lane) & 1ull) {
       const uint32_t row = gi * kWave + lane;
       const uint16_t T = tn16[row];
@@ -636,20 +645,28 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
       if (!(MODE & 128)) {
         // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
         const uint32_t u = p.ustart + row, b2 = u * 2u, b4 = u * 4u;
-        // dense: one 8-B record (T_pub, |M|, first entry); T_state (= T_pub) and the alive count (= |M|)
-        // are implied: the first later superstep, the only reader before they are rewritten, takes them
-        // from the record.  A tile outside the region: the state arrays (T_pub still in the record)
-        if (dense) {
-          o.rec[u] = T | (static_cast<unsigned long long>(cnt) << 16) |
-                     (static_cast<unsigned long long>(dpos + st.hd[row]) << 32);
+        // dense mode: one 16-B record in the wave's slice (consecutive survivors: coalesced) instead of
+        // position-indexed stores that land in partial cache lines; T_state (= T_pub) and the alive
+        // count (= |M|) are implied: the first later superstep, the only reader before they are
+        // rewritten, takes them from the record.  A tile outside the M region: its state arrays, and a
+        // record without a first entry.  A label of more than two template vertices keeps its
+        // position-indexed T_pub (the next superstep's code-3 gathers).
+        const uint32_t code = tpub_code(T, p.tu);
+        if (o.rarea) {
+          if (!dense) {
+            *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
+            *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
+            *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
+          }
+          if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+          o.rarea[rslot] = make_uint4(u, T | (cnt << 16), dense ? static_cast<uint32_t>(dpos + st.hd[row]) : kNone, 0u);
         } else {
           *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
+          *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
           *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
           *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
-          if (o.rec) o.rec[u] = T | (static_cast<unsigned long long>(kNone) << 32);
-          else *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
         }
-        atomicOr(&o.tcode[u >> 4], tpub_code(T, p.tu) << ((u & 15u) << 1));
+        atomicOr(&o.tcode[u >> 4], code << ((u & 15u) << 1));
       }
     }
   }
@@ -724,12 +741,16 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
       const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
       const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
       surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
+      // dense mode: the heavy row's record (its M in the padded row); hrec was zeroed before the launch
+      if (surv && o.hrec) o.hrec[hs.h] = make_uint4(hs.row, 0u, kNone, 1u);
     }
   }
-  if (lane == 0 && surv && !(MODE & 8)) tm[0] = 1ull;  // (read only when the tile count is 1)
-  if (lane == 0 && !(MODE & 8)) {
-    o.tcnt[hs.tile] = surv ? 1u : 0u;
-    o.tstart[hs.tile] = hs.row;
+  if (!o.rarea) {
+    if (lane == 0 && surv && !(MODE & 8)) tm[0] = 1ull;  // (read only when the tile count is 1)
+    if (lane == 0 && !(MODE & 8)) {
+      o.tcnt[hs.tile] = surv ? 1u : 0u;
+      o.tstart[hs.tile] = hs.row;
+    }
   }
   return acc;
 }
@@ -777,13 +798,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
   // dense M: this wave's slice of the region
   uint64_t dcur = uniform64((uint64_t(blockIdx.x) * kWpb + wid) * o.dslice);
   const uint64_t dend = uniform64(dcur + o.dslice);
+  // dense mode: this wave's record slice
+  const uint32_t gw = blockIdx.x * kWpb + wid;
+  uint64_t rcur = o.rarea ? uniform64(o.rbase[gw]) : 0;
   while (t < ntiles) {
     t = __builtin_amdgcn_readfirstlane(t);
     const uint32_t tn = t + W;
     // the previous tile's stores go out ahead of the next tile's loads
     k1_pend_uniform(pend);
     dcur = uniform64(dcur);
-    k1_flush<MODE>(pend, o, st, dcur, dend);
+    rcur = uniform64(rcur);
+    k1_flush<MODE>(pend, o, st, dcur, dend, rcur);
     pend.tm = nullptr;
     K1Desc nxt{};
     if (tn < ntiles) nxt = k1_desc(kt, r, tn);
@@ -813,7 +838,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
   }
   k1_pend_uniform(pend);
   dcur = uniform64(dcur);
-  k1_flush<MODE>(pend, o, st, dcur, dend);
+  rcur = uniform64(rcur);
+  k1_flush<MODE>(pend, o, st, dcur, dend, rcur);
+  if (o.rarea && lane_id() == 0) o.rcnt[gw] = static_cast<uint32_t>(rcur - o.rbase[gw]);
   // heavy rows, one segment per wave at a time (a separate loop: no slot
   // buffers live, so the light loop's register budget is its own)
   if (!(MODE & 4))
@@ -902,7 +929,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
-    const unsigned long long* __restrict__ rec, uint64_t dbase) {
+    const uint4* __restrict__ srec, uint64_t dbase) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -930,7 +957,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     for (int l = 0; l < nruns; ++l)
       if (p - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
     const uint32_t rest = tu & (tu - 1);
-    if (rest & (rest - 1)) return rec ? static_cast<uint16_t>(rec[p]) : tcur[p];
+    if (rest & (rest - 1)) return tcur[p];
     return static_cast<uint16_t>(((code & 1u) ? (tu & (0u - tu)) : 0u) | ((code & 2u) ? rest : 0u));
   };
   BlockAcc acc;
@@ -947,16 +974,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     uint32_t len = 0, alive0 = 0;
     bool drow = false;  // M read from the dense superstep-0 region
     if (i < nS && ((live >> lane) & 1ull)) {
-      u = slist[i];
       // the row's state is loaded with T_pub in one round trip (a removed
       // row, T_pub = 0, ignores it)
       uint32_t l, dm = kNone;
-      if (rec) {  // dense superstep-0 output: the record (T_pub, |M|, first entry) of u
-        const unsigned long long r = rec[u];
-        Tu = static_cast<uint16_t>(r);
-        dm = static_cast<uint32_t>(r >> 32);
-        l = dm != kNone ? static_cast<uint32_t>(r >> 16) & 0xFFFFu : mlen[u];
+      if (srec) {  // dense superstep-0 output: the records, in slist order (coalesced)
+        const uint4 r = srec[i];
+        u = r.x;
+        Tu = static_cast<uint16_t>(r.y);
+        dm = r.z;
+        l = dm != kNone ? r.y >> 16 : mlen[u];
       } else {
+        u = slist[i];
         Tu = tcur[u];
         l = mlen[u];
       }
@@ -1070,7 +1098,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
       }
     }
     bool survivor = false, removed = false, cleared = false;
-    if (rec) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
+    if (srec) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
     if (Tu) {
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
@@ -1086,10 +1114,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         }
       } else {
         removed = true;
-        tnxt[u] = 0;
-        malive[u] = 0;
         cnt = 0;
-        if (drow) mlen[u] = 0;  // M[v] cleared (nonunique_ee.hpp:941-964); its padded row was never written
+        // dense superstep-0 records: both T_pub buffers of u are still clean (superstep 0 wrote u's
+        // T_pub only into its record) and its state arrays were never written, so a removed row writes
+        // nothing -- M[v] cleared (nonunique_ee.hpp:941-964) is its absence from every later list
+        if (!srec || !drow) {
+          tnxt[u] = 0;
+          malive[u] = 0;
+        }
         // first later superstep: neighbours read u's T_pub through the 2-bit codes unless u's label has
         // more than two template vertices, so the buffer read now can be cleared at once and u leaves
         // the live list (otherwise it stays live one more superstep, which clears the other buffer)
@@ -1099,7 +1131,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             if (u - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
           const uint32_t rest = tu & (tu - 1);
           if (!(rest & (rest - 1))) {
-            tcur[u] = 0;
+            if (!srec) tcur[u] = 0;  // (with records it was never written)
             cleared = true;
           }
         }
@@ -1665,6 +1697,49 @@ void build_tiling(Ctx& c) {
   c.scan_tmp_bytes = slist_scan_tmp_bytes(std::max<uint64_t>(1, tiles));
   PM_HIP_CHECK(hipMalloc(&c.d_scan_tmp, std::max<size_t>(1, c.scan_tmp_bytes)));
   c.k1_grid = lcc_first_grid(c);
+  // record slices of the superstep-0 waves (dense mode): each wave's bound is the rows of the light tiles
+  // it visits (tiles t, t + W, ... of a persistent grid of W waves)
+  {
+    void* ptrs[] = {c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.d_hrec, c.d_srec, c.d_rscan_tmp};
+    for (void* q : ptrs)
+      if (q) (void)hipFree(q);
+    c.d_rarea = c.d_hrec = c.d_srec = nullptr;
+    c.d_rbase = c.d_rofs = nullptr;
+    c.d_rcnt = nullptr;
+    c.d_rscan_tmp = nullptr;
+    c.rwaves = 0;
+    if (c.dcap && c.symmetric) {
+      const uint32_t W = c.k1_grid * kWpb;
+      std::vector<uint64_t> rows(W + 1, 0);
+      for (size_t r = 0; r + 1 < tab.size(); ++r) {
+        const KRange& R = tab[r];
+        if (R.kind >= static_cast<uint32_t>(kHeavyKind)) continue;
+        const uint64_t nrows = R.end - R.start, nt = (nrows + R.rpt - 1) / R.rpt;
+        for (uint64_t k = 0; k < nt; ++k) rows[(R.tile0 + k) % W] += std::min<uint64_t>(R.rpt, nrows - k * R.rpt);
+      }
+      uint64_t tot = 0;
+      for (uint32_t w = 0; w < W; ++w) {
+        const uint64_t x = rows[w];
+        rows[w] = tot;
+        tot += x;
+      }
+      rows[W] = tot;
+      c.rarea_cap = std::max<uint64_t>(tot, 1);
+      c.srec_cap = tot + nheavy + c.hubinfo.size() + 1;
+      PM_HIP_CHECK(hipMalloc(&c.d_rarea, c.rarea_cap * sizeof(uint4)));
+      PM_HIP_CHECK(hipMalloc(&c.d_srec, c.srec_cap * sizeof(uint4)));
+      PM_HIP_CHECK(hipMalloc(&c.d_rbase, (W + 1) * sizeof(uint64_t)));
+      PM_HIP_CHECK(hipMalloc(&c.d_rcnt, std::max<uint32_t>(W, 1) * sizeof(uint32_t)));
+      PM_HIP_CHECK(hipMalloc(&c.d_rofs, (W + 1) * sizeof(uint64_t)));
+      PM_HIP_CHECK(hipMalloc(&c.d_hrec, std::max<uint64_t>(nheavy, 1) * sizeof(uint4)));
+      PM_HIP_CHECK(hipMemcpy(c.d_rbase, rows.data(), (W + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
+      rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> it(c.d_rcnt, Widen());
+      PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, c.rscan_tmp_bytes, it, c.d_rofs, uint64_t(0), size_t(W),
+                                           rocprim::plus<uint64_t>(), c.stream));
+      PM_HIP_CHECK(hipMalloc(&c.d_rscan_tmp, std::max<size_t>(c.rscan_tmp_bytes, 1)));
+      c.rwaves = W;
+    }
+  }
   if (c.d_hubinfo) (void)hipFree(c.d_hubinfo);
   if (c.d_moff) (void)hipFree(c.d_moff);
   if (c.d_hubpart) (void)hipFree(c.d_hubpart);
@@ -1687,9 +1762,25 @@ void build_tiling(Ctx& c) {
 }
 
 static K1Out k1_out(Ctx& c, unsigned grid) {
-  return K1Out{c.d_tst,   c.d_tpub[c.cur], c.d_mcol,  c.d_mlen, c.d_malive, c.d_tcnt,
-               c.d_tstart, c.d_tcode,      c.k1_dense ? reinterpret_cast<unsigned long long*>(c.d_s0rec) : nullptr, c.dbase,
-               c.dcap / (uint64_t(std::max(grid, 1u)) * kWpb)};
+  // records: dense M on the grid the record slices were sized for
+  const bool rec = c.k1_dense && c.d_rarea && grid * kWpb == c.rwaves;
+  c.k1_records = rec;
+  K1Out o{};
+  o.tst = c.d_tst;
+  o.tpub = c.d_tpub[c.cur];
+  o.mcol = c.d_mcol;
+  o.mlen = c.d_mlen;
+  o.malive = c.d_malive;
+  o.tcnt = c.d_tcnt;
+  o.tstart = c.d_tstart;
+  o.tcode = c.d_tcode;
+  o.rarea = rec ? c.d_rarea : nullptr;
+  o.rbase = c.d_rbase;
+  o.rcnt = c.d_rcnt;
+  o.hrec = rec ? c.d_hrec : nullptr;
+  o.dbase = c.dbase;
+  o.dslice = c.k1_dense ? c.dcap / (uint64_t(std::max(grid, 1u)) * kWpb) : 0;
+  return o;
 }
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
@@ -1744,6 +1835,38 @@ void lcc_first_set_dense(Ctx& c) {
 
 void lcc_first_prepare(Ctx& c) {
   if (c.nheavy) PM_HIP_CHECK(hipMemsetAsync(c.d_hscr, 0, 3 * size_t(c.nheavy) * sizeof(uint32_t), c.stream));
+  if (c.nheavy && c.d_hrec) PM_HIP_CHECK(hipMemsetAsync(c.d_hrec, 0, size_t(c.nheavy) * sizeof(uint4), c.stream));
+}
+
+// slist from the superstep-0 records (dense mode): one wave per record slice copies its records to
+// srec[rofs[w] ..] and their positions to slist; the heavy survivors follow (k_slist_heavy).
+__global__ void k_slist_from_records(const uint4* __restrict__ rarea, const uint64_t* __restrict__ rbase,
+                                     const uint32_t* __restrict__ rcnt, const uint64_t* __restrict__ rofs,
+                                     uint32_t W, uint4* __restrict__ srec, uint32_t* __restrict__ slist,
+                                     uint32_t* __restrict__ nS) {
+  const int lane = lane_id();
+  const uint64_t nw = uint64_t(gridDim.x) * kWpb;
+  for (uint64_t w = blockIdx.x * uint64_t(kWpb) + threadIdx.x / kWave; w < W; w += nw) {
+    const uint32_t n = rcnt[w];
+    const uint64_t src = rbase[w], dst = rofs[w];
+    for (uint32_t i = lane; i < n; i += kWave) {
+      const uint4 r = rarea[src + i];
+      srec[dst + i] = r;
+      slist[dst + i] = r.x;
+    }
+    if (w == W - 1 && lane == 0) *nS = static_cast<uint32_t>(dst + n);
+  }
+}
+
+__global__ void k_slist_heavy(const uint4* __restrict__ hrec, uint32_t nheavy, const uint16_t* __restrict__ tst,
+                              uint4* __restrict__ srec, uint32_t* __restrict__ slist, uint32_t* __restrict__ nS) {
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nheavy; h += gridDim.x * blockDim.x) {
+    const uint4 r = hrec[h];
+    if (!r.w) continue;
+    const uint32_t i = atomicAdd(nS, 1u);
+    srec[i] = make_uint4(r.x, tst[r.x], kNone, 0u);  // T_pub = T_state after superstep 0
+    slist[i] = r.x;
+  }
 }
 
 void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) {
@@ -1764,6 +1887,21 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
   launch_lcc_first_kernel(c, 0, grid, d_slot);
   if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
   reduce_into(c, grid, d_slot);
+  c.smask_valid = false;
+  if (c.k1_records) {
+    // slist = the records of the waves' slices (wave order), then the heavy survivors
+    rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> rit(c.d_rcnt, Widen());
+    size_t tb = c.rscan_tmp_bytes;
+    PM_HIP_CHECK(rocprim::exclusive_scan(c.d_rscan_tmp, tb, rit, c.d_rofs, uint64_t(0), size_t(c.rwaves),
+                                         rocprim::plus<uint64_t>(), c.stream));
+    hipLaunchKernelGGL(k_slist_from_records, dim3(grid_for(c.rwaves, kWpb, 8192)), dim3(kBlock), 0, c.stream,
+                       c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.rwaves, c.d_srec, c.d_slist, c.d_nS);
+    if (c.nheavy)
+      hipLaunchKernelGGL(k_slist_heavy, dim3(grid_for(c.nheavy, kBlock, 1024)), dim3(kBlock), 0, c.stream, c.d_hrec,
+                         c.nheavy, c.d_tst, c.d_srec, c.d_slist, c.d_nS);
+    PM_HIP_CHECK(hipGetLastError());
+    return;
+  }
   // slist = survivors in label-major row order (tiles are in position order)
   rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> it(c.d_tcnt, Widen());
   size_t tmp = c.scan_tmp_bytes;
@@ -1813,11 +1951,10 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
-                     c.diag_step,
-                     first_after_ss0 && c.k1_dense ? reinterpret_cast<const unsigned long long*>(c.d_s0rec) : nullptr,
-                     c.dbase);
+                     c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase);
   PM_HIP_CHECK(hipGetLastError());
   c.k1_dense = false;  // every M row of S is in its padded row from here on
+  c.k1_records = false;
   reduce_into(c, grid, d_slot);
   c.cur ^= 1;
   c.smask_cur ^= 1;

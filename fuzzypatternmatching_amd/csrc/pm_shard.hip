@@ -278,13 +278,13 @@ __global__ void k_count_to_u64(const uint32_t* __restrict__ n, uint64_t* __restr
 // (its code 3 means "gather T_pub"), position | T_pub << 32 | code << 62.
 __global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
                              const uint32_t* __restrict__ tcode, const uint16_t* __restrict__ tpub,
-                             const unsigned long long* __restrict__ rec, int wide, uint32_t* __restrict__ out32,
+                             const uint4* __restrict__ srec, int wide, uint32_t* __restrict__ out32,
                              unsigned long long* __restrict__ out64) {
   const uint64_t n = *nSp;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t p = slist[i];
     const uint32_t code = (tcode[p >> 4] >> ((p & 15u) << 1)) & 3u;
-    const uint16_t T = rec ? static_cast<uint16_t>(rec[p]) : tpub[p];  // dense superstep 0: T_pub in the record
+    const uint16_t T = srec ? static_cast<uint16_t>(srec[i].y) : tpub[p];  // superstep-0 records: T_pub there
     if (wide) out64[i] = p | (static_cast<unsigned long long>(T) << 32) | (static_cast<unsigned long long>(code) << 62);
     else out32[i] = p | (code << 30);
   }
@@ -293,7 +293,7 @@ __global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t*
 // The other shards' code records into this shard's 2-bit codes (and T_pub).
 __global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned long long* __restrict__ in64,
                                uint64_t maxS, uint32_t G, uint32_t me, XCounts x, uint32_t* __restrict__ tcode,
-                               uint16_t* __restrict__ tpub, unsigned long long* __restrict__ rec) {
+                               uint16_t* __restrict__ tpub) {
   const uint64_t total = uint64_t(G) * maxS;
   for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t g = static_cast<uint32_t>(j / maxS);
@@ -303,9 +303,7 @@ __global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned
       const unsigned long long r = in64[j];
       p = static_cast<uint32_t>(r & 0x3FFFFFFFull);
       code = static_cast<uint32_t>(r >> 62);
-      // where the next superstep's gathers look up a code-3 T_pub (k_lcc_step tpub_of)
-      if (rec) rec[p] = (r >> 32) & 0xFFFFull;
-      else tpub[p] = static_cast<uint16_t>(r >> 32);
+      tpub[p] = static_cast<uint16_t>(r >> 32);  // (the next superstep's code-3 gathers, k_lcc_step tpub_of)
     } else {
       p = in32[j] & 0x3FFFFFFFu;
       code = in32[j] >> 30;
@@ -468,7 +466,7 @@ struct HubFinishArgs {
   uint32_t* mlen;
   uint32_t* malive;
   uint32_t* tcode;
-  unsigned long long* rec;            // dense superstep-0 M in use: the hub's record (its row is not dense)
+  uint4* srec;                        // superstep-0 records in use: the hub's record beside its slist entry
   uint32_t* mcol;
   uint32_t* slist;
   uint32_t* nS;
@@ -507,8 +505,9 @@ __global__ void k_hub_finish(HubFinishArgs a) {
         a.mlen[p] = static_cast<uint32_t>(cnt);
         a.malive[p] = static_cast<uint32_t>(cnt);
         atomicOr(&a.tcode[p >> 4], tpub_code(T, tu) << ((p & 15u) << 1));
-        if (a.rec) a.rec[p] = T | (static_cast<unsigned long long>(kNone) << 32);
-        a.slist[atomicAdd(a.nS, 1u)] = p;
+        const uint32_t at = atomicAdd(a.nS, 1u);
+        a.slist[at] = p;
+        if (a.srec) a.srec[at] = make_uint4(p, T, kNone, 0u);  // its M in the hub area (m_off), not dense
         const uint32_t r = a.nranks <= 1 ? 0u : j % a.nranks;  // owner rule of a delegate
         atomicAdd(&a.slot[r], 1ull);
         atomicAdd(&a.slot[a.P + r], static_cast<unsigned long long>(cnt));
@@ -631,7 +630,7 @@ void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
   a.mlen = c.d_mlen;
   a.malive = c.d_malive;
   a.tcode = c.d_tcode;
-  a.rec = c.k1_dense ? reinterpret_cast<unsigned long long*>(c.d_s0rec) : nullptr;
+  a.srec = c.k1_records ? c.d_srec : nullptr;
   a.mcol = c.d_mcol;
   a.slist = c.d_slist;
   a.nS = c.d_nS;
@@ -656,18 +655,17 @@ void shard_codes_after_first(Ctx& c) {
   const size_t rb = c.xcode_wide ? 8 : 4;
   auto* send = grow<char>(c.d_xsend, c.xsend_cap, maxS * rb);
   auto* recv = grow<char>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxS * rb);
-  auto* rec = c.k1_dense ? reinterpret_cast<unsigned long long*>(c.d_s0rec) : nullptr;
   hipLaunchKernelGGL(k_pack_codes, dim3(xgrid(c.nS_host)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tcode,
-                     c.d_tpub[c.cur], rec, c.xcode_wide ? 1 : 0, reinterpret_cast<uint32_t*>(send),
-                     reinterpret_cast<unsigned long long*>(send));
+                     c.d_tpub[c.cur], c.k1_records ? c.d_srec : nullptr, c.xcode_wide ? 1 : 0,
+                     reinterpret_cast<uint32_t*>(send), reinterpret_cast<unsigned long long*>(send));
   c.comm->allgather(send, recv, maxS * rb, c.stream);
   XCounts x{};
   for (uint32_t g = 0; g < G; ++g) x.n[g] = n[g];
   hipLaunchKernelGGL(k_unpack_codes, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream,
                      c.xcode_wide ? nullptr : reinterpret_cast<const uint32_t*>(recv),
                      c.xcode_wide ? reinterpret_cast<const unsigned long long*>(recv) : nullptr, maxS, G, c.shard, x,
-                     c.d_tcode, c.d_tpub[c.cur], rec);
-  c.xcode_in_tpub = c.xcode_wide && !rec;
+                     c.d_tcode, c.d_tpub[c.cur]);
+  c.xcode_in_tpub = c.xcode_wide;
   PM_HIP_CHECK(hipGetLastError());
 }
 
