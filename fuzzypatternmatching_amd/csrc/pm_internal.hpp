@@ -143,6 +143,14 @@ static constexpr uint32_t kNoHub = 0xFFFFFFFFu;
 static constexpr int kSub = 8;                      // 64-slot sub-tiles per tile
 static constexpr uint32_t kTileEntries = 64 * kSub; // 512
 static constexpr uint32_t kHeavyDeg = kTileEntries; // heavy rows: segments of this many entries
+// Rows per light tile at most (LDS per-row staging of k_lcc_first; G = 1 tiles hold 256 rows)
+static constexpr uint32_t kTileRows = 256;
+// Superstep-0 tile descriptor (d_ttab, one u64 per tile): bits [0, 36) first slot of the tile, [36, 45)
+// slots of its rows (rows * g; 0: heavy tile, loads nothing), [45, 57) KRange index
+static constexpr int kTtabRemShift = 36, kTtabRangeShift = 45;
+// Consecutive tiles a superstep-0 wave takes at a time (tile t goes to wave (t / kTileBlock) % W): the
+// tiles of a block share their range, whose fields then hit in the scalar cache
+static constexpr uint32_t kTileBlock = 4;
 // Light rows fit in one tile with room for the 16-B alignment shift of its
 // loads (a light tile holds at most kTileEntries - 4 slots).
 static constexpr uint32_t kLightMax = 480;
@@ -242,6 +250,7 @@ struct Ctx {
   // superstep-0 tiling for the current labels and pattern
   std::vector<KRange> ktab;
   KRange* d_ktab = nullptr;
+  uint64_t* d_ttab = nullptr;     // superstep-0 tile descriptors (kTtab*Shift)
   uint32_t ntiles = 0;
   bool k1_wide = false;           // some range has more than four relevant label runs
   HSeg* d_hseg = nullptr;

@@ -329,107 +329,82 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return (uint64_t(hi) << 32) | lo;
 }
 
-// Uniform description of one superstep-0 tile, resolved from the KRange table.
-struct K1Desc {
-  uint64_t qbase;  // first slot of the run
-  uint32_t start;  // first row position of the run
-  uint32_t nrows;  // rows of the run
-  uint32_t rel;    // tile index inside the run
-  uint32_t kind;   // light degree class or kHeavyKind
-  uint32_t g;      // light: slots per row
-  uint32_t rpt;    // light: rows per tile
-  uint32_t rdiv;   // light: row of a slot = (slot * rdiv) >> 19
-  uint32_t r;      // KRange index
-};
+// A superstep-0 tile from its descriptor word (d_ttab): first slot, slots of its rows (0: a heavy tile),
+// KRange index.  The table is read through the constant address space (scalar loads).
+typedef __attribute__((address_space(4))) const uint64_t* TTab;
+__device__ __forceinline__ uint64_t ttab_slot(uint64_t w) { return w & ((1ull << kTtabRemShift) - 1); }
+__device__ __forceinline__ uint32_t ttab_rem(uint64_t w) {
+  return static_cast<uint32_t>(w >> kTtabRemShift) & ((1u << (kTtabRangeShift - kTtabRemShift)) - 1);
+}
+__device__ __forceinline__ uint32_t ttab_range(uint64_t w) { return static_cast<uint32_t>(w >> kTtabRangeShift); }
 
-// Advances the wave's range cursor r to the range holding tile t (tiles are
-// visited in increasing order by each wave) and returns the tile's description.
-__device__ __forceinline__ K1Desc k1_desc(KTab kt, uint32_t& r, uint32_t t) {
-  // (r and t are wave-uniform: pinned to SGPRs, or the search runs on vector loads)
-  r = __builtin_amdgcn_readfirstlane(r);
-  t = __builtin_amdgcn_readfirstlane(t);
-  while (kt[r + 1].tile0 <= t) r = __builtin_amdgcn_readfirstlane(r + 1);
-  K1Desc d;
-  d.r = r;
-  d.kind = kt[r].kind;
-  d.g = kt[r].g;
-  d.rpt = kt[r].rpt;
-  d.rdiv = kt[r].rdiv;
-  d.start = kt[r].start;
-  d.nrows = kt[r].end - d.start;
-  d.rel = t - kt[r].tile0;
-  d.qbase = kt[r].qbase;
-  return d;
+// The tile after t of a wave that takes kTileBlock consecutive tiles out of every W * kTileBlock.
+__device__ __forceinline__ uint32_t k1_next(uint32_t t, uint32_t W) {
+  const uint32_t n = t + 1;
+  return __builtin_amdgcn_readfirstlane((n % kTileBlock) ? n : n + (W - 1) * kTileBlock);
 }
 
-// Pins a loop-carried descriptor to scalar registers (the compiler otherwise
-// keeps it in VGPRs and turns every range-table read into a vector load).
-__device__ __forceinline__ void k1_uniform(K1Desc& d) {
-  d.r = __builtin_amdgcn_readfirstlane(d.r);
-  d.kind = __builtin_amdgcn_readfirstlane(d.kind);
-  d.g = __builtin_amdgcn_readfirstlane(d.g);
-  d.rpt = __builtin_amdgcn_readfirstlane(d.rpt);
-  d.rdiv = __builtin_amdgcn_readfirstlane(d.rdiv);
-  d.start = __builtin_amdgcn_readfirstlane(d.start);
-  d.nrows = __builtin_amdgcn_readfirstlane(d.nrows);
-  d.rel = __builtin_amdgcn_readfirstlane(d.rel);
-  d.qbase = uniform64(d.qbase);
-}
-
-// The rpt * g slots of a light tile (kNone outside them) in two 16-B loads per
-// lane, issued before any use: load k, component c of lane l holds the slot
-// at 256 k + 4 l + c of the 16-B aligned window that starts s = base & 3
-// slots before the tile (rpt * g <= kTileEntries - 4, so the window covers
-// the tile).  Lanes whose four slots all lie outside the tile load nothing;
-// a heavy tile or a tile past the end loads nothing at all.
+// The slots of a light tile in two 16-B loads per lane: load k, component c
+// of lane l holds the slot at 256 k + 4 l + c of the 16-B aligned window that
+// starts s = base & 3 slots before the tile (rpt * g <= kTileEntries - 4, so
+// the window covers the tile).  Buffer loads through a descriptor that ends at
+// the tile (lanes past it read 0, a heavy tile or a tile past the end reads
+// nothing): the lane offsets are loop-invariant and no slot is masked here.
+// Window slots outside the tile (the s slots before it, the tail after it) are
+// phase A contributors like any other; their tile-relative slot falls outside
+// [0, rows * g) and phase B drops them.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t k1_load(uint32_t (&v)[kSub], const K1Desc& d, const uint32_t* __restrict__ colp,
-                                            bool valid) {
-  const int lane = lane_id();
-  const bool light = valid && d.kind < static_cast<uint32_t>(kHeavyKind);
-  // slots of the tile inside the run, in 32-bit row arithmetic (rows < 2^30)
-  const uint32_t r0 = d.rel * d.rpt;
-  const uint32_t rows = light && d.nrows > r0 ? min(d.nrows - r0, d.rpt) : 0u;
-  const uint32_t rem = rows * d.g;
-  const uint64_t b = rem ? d.qbase + uint64_t(r0) * d.g : 0;
+__device__ __forceinline__ uint32_t k1_load(uint32_t (&v)[kSub], uint64_t w, const uint32_t* __restrict__ colp,
+                                            uint32_t voff) {
+  const uint32_t rem = ttab_rem(w);
+  const uint64_t b = rem ? ttab_slot(w) : 0;
   const uint32_t s = static_cast<uint32_t>(b) & 3u;
-  const u32x4* tp = reinterpret_cast<const u32x4*>(colp + (b - s));
+  const uint64_t wbase = uniform64(reinterpret_cast<uint64_t>(colp + (b - s)));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(wbase), 0, static_cast<int>(__builtin_amdgcn_readfirstlane(rem ? (rem + s) * 4u : 0u)),
+      0x00020000);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const uint32_t o = static_cast<uint32_t>(k * 256 + 4 * lane);  // window offset of component 0
-    u32x4 w = {kNone, kNone, kNone, kNone};
-    if (o + 3 >= s && o < rem + s) w = __builtin_nontemporal_load(tp + k * kWave + lane);
+    // aux 2: nontemporal (the adjacency is read once per superstep 0)
+    const u32x4 x = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(voff) + k * 1024, 0, 2));
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[4 * k + c] = (o + c >= s && o + c < rem + s) ? w[c] : kNone;
+    for (int c = 0; c < 4; ++c) v[4 * k + c] = x[c];
   }
   return s;
 }
 
 // Per-wave LDS staging of a light tile: the tile's contributing entries in
-// slot order (neighbour position, row inside the tile), which become M rows
+// slot order (neighbour position, slot relative to the tile start: outside
+// [0, rows * g) for the window slots around the tile), which become M rows
 // once the verify has decided which rows survive, and per-row accumulators:
 // TN (two rows per word, zero between tiles) and the row's first / last + 1
 // list index (valid while its TN is non-zero).
 struct K1Stage {
   uint32_t lx[kTileEntries];
-  uint16_t lrow[kTileEntries];
-  uint16_t hd[kTileEntries], tl[kTileEntries];
-  uint32_t tn[kTileEntries / 2];
-  unsigned long long sm[kSub];  // survivor bits of the tile's rows
+  uint16_t lrel[kTileEntries];
+  uint16_t hd[kTileRows], tl[kTileRows];
+  uint32_t tn[kTileRows / 2];
+  unsigned long long sm[kTileRows / kWave];  // survivor bits of the tile's rows
 };
+// 4.6 KB per wave: eight 4-wave blocks (8 waves per SIMD) fit the CU's 160 KB of LDS with the block's
+// other shared arrays
+static_assert(sizeof(K1Stage) * kWpb + 2 * kMaxRanks * 8 + kWpb * 6 * 8 + 32 + 3 * 16 * 4 <= 160 * 1024 / 8,
+              "k_lcc_first LDS exceeds 8 blocks per CU");
 
-// Phase A of a light tile: appends the tile's contributing slots (neighbour
-// position in an admitted run, first occurrence in its row) to the wave's
-// staging list in slot order and returns their number (wave-uniform).  NR
-// merged-run compares (unused runs have length 0); NR = 0: the full label
+// Phase A of a light tile: appends the tile window's contributing slots
+// (neighbour position in an admitted run, first occurrence in its row) to the
+// wave's staging list in slot order and returns their number (wave-uniform).
+// NR merged-run compares (unused runs have length 0); NR = 0: the full label
 // test (more than four runs).  Per 16-B load: the compares of its four
 // components land in 64-bit lane masks; a component's left neighbour is the
 // previous component of the same lane (component 0: lane - 1's component 3),
 // the row starts come from the range's masks for the tile's shift s, and a
 // lane's contributors are written in component order after those of the lower
-// lanes (prefix = sum of four masked popcounts), which keeps slot order.
+// lanes (prefix = sum of four masked popcounts), which keeps slot order.  The
+// lane masks drive exec directly (inverse ballot); rel = window slot - s.
 template <int NR, bool WIDE>
-__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R, uint32_t s, uint32_t rdiv,
+__device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R, uint32_t s,
                                                const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
                                                uint16_t nm, K1Stage& st) {
   const int lane = lane_id();
@@ -458,23 +433,25 @@ __device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R
           // (p != x0) as integer carry arithmetic: a bool here would be widened on the VALU
           ne_m = (ne_m & ~1ull) | ((uint64_t(p ^ x0) + 0xFFFFFFFFull) >> 32);
         }
-        // k = 0: lane 0's component 0 is either outside the tile or its first slot (a row start)
+        // k = 0: lane 0's component 0 is either before the tile or its first slot (a row start)
       }
       C[c] = in_m & (R->rs[s][4 * k + c] | ne_m);
     }
     const uint64_t any = C[0] | C[1] | C[2] | C[3];
     if (any) {
-      if ((any >> lane) & 1ull) {
+      if (__builtin_amdgcn_inverse_ballot_w64(any)) {
         uint32_t idx = nlist;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           idx += __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(C[c] >> 32),
                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(C[c]), 0));
+        // window slot relative to the tile start (wraps below 0: outside the tile)
+        const uint32_t rel0 = static_cast<uint32_t>(k * 256 + 4 * lane) - s;
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if ((C[c] >> lane) & 1ull) {
+          if (__builtin_amdgcn_inverse_ballot_w64(C[c])) {
             st.lx[idx] = v[4 * k + c];
-            st.lrow[idx] = static_cast<uint16_t>(((static_cast<uint32_t>(k * 256 + 4 * lane + c) - s) * rdiv) >> 19);
+            st.lrel[idx] = static_cast<uint16_t>(rel0 + c);
             ++idx;
           }
       }
@@ -494,10 +471,12 @@ struct K1Pend {
   uint32_t ustart;         // position of the tile's first row
   uint32_t g;              // slots per row
   uint32_t nlist;          // staged contributors
-  uint32_t ngroups;        // 64-row groups with verified rows (0: none)
+  uint32_t g0, g1;         // 64-row groups [g0, g1) that hold verified rows (g1 = 0: none)
   uint32_t any;            // survivors of the tile
   uint32_t tile;           // tile index
   uint32_t tu;             // template bits of the tile's label
+  uint32_t rem;            // slots of the tile's rows (rows * g)
+  uint32_t rdiv;           // row of a tile slot = (slot * rdiv) >> 19
 };
 
 __device__ __forceinline__ void k1_pend_uniform(K1Pend& p) {
@@ -506,98 +485,122 @@ __device__ __forceinline__ void k1_pend_uniform(K1Pend& p) {
   p.ustart = __builtin_amdgcn_readfirstlane(p.ustart);
   p.g = __builtin_amdgcn_readfirstlane(p.g);
   p.nlist = __builtin_amdgcn_readfirstlane(p.nlist);
-  p.ngroups = __builtin_amdgcn_readfirstlane(p.ngroups);
+  p.g0 = __builtin_amdgcn_readfirstlane(p.g0);
+  p.g1 = __builtin_amdgcn_readfirstlane(p.g1);
   p.any = __builtin_amdgcn_readfirstlane(p.any);
   p.tile = __builtin_amdgcn_readfirstlane(p.tile);
   p.tu = __builtin_amdgcn_readfirstlane(p.tu);
+  p.rem = __builtin_amdgcn_readfirstlane(p.rem);
+  p.rdiv = __builtin_amdgcn_readfirstlane(p.rdiv);
 }
 
-// Light tile (G = d.g slots per row, d.rpt = (kTileEntries - 4) / G whole rows).
+// Row of a staged entry of a tile (kNoRow: a window slot outside the tile's rows).
+static constexpr uint32_t kNoRow = 0xFFFFu;
+__device__ __forceinline__ uint32_t k1_row(uint32_t rel, uint32_t rem, uint32_t rdiv) {
+  return rel < rem ? (__umul24(rel, rdiv) >> 19) : kNoRow;
+}
+
+// Light tile: rem = rows * g slots from slot qb of rows of g slots (R->rpt = min((kTileEntries - 4) / g,
+// kTileRows) rows per tile), the first at position ustart.
 // Phase A, per 16-B load, all in wave masks: a lane's neighbour can contribute
 // iff its position lies in one of the range's relevant label runs (one
 // compare per run, the masks OR-ed on the scalar unit) and it is the first
 // occurrence in its row (row start, or differs from its left neighbour);
 // only the contributing lanes (a few percent of the slots) are appended to
 // the LDS staging list.  Phase B: row TN / first and last list index from the
-// list (B1), one lane per row verifies and leaves T_state in the row's half
+// list (B1, entries outside the tile's rows dropped), one lane per row of the
+// groups that hold listed rows verifies and leaves T_state in the row's half
 // word (B2); the stores (state, survivor mask, M) wait in LDS for k1_flush.
 template <int MODE, bool WIDE>
-__device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, const K1Desc& d, KTab R,
+__device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, uint64_t qb, uint32_t rem,
+                                                uint32_t ustart, uint32_t g, uint32_t rpt, uint32_t rdiv, KTab R,
                                                 uint16_t tu, uint16_t nm, const RelRuns& rel_runs,
                                                 const uint32_t* s_runs, int nruns, const KeepArgs& keep,
                                                 const uint16_t* s_adj, const OwnerArgs& oa, BlockAcc& acc,
                                                 unsigned long long* s_hist, unsigned long long* tm, uint32_t tile,
                                                 K1Stage& st) {
   const int lane = lane_id();
-  const uint32_t g = d.g, rpt = d.rpt;
-  const uint32_t row0 = d.rel * rpt;
-  K1Pend p{tm, d.qbase + uint64_t(row0) * g, d.start + row0, g, 0u, 0u, 0u, tile, tu};
+  K1Pend p{tm, qb, ustart, g, 0u, 0u, 0u, 0u, tile, tu, rem, rdiv};
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
   if (WIDE || rel_runs.nadm > 4)
-    nlist = k1_phase_a<0, WIDE>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<0, WIDE>(v, R, s, rel_runs, s_runs, nruns, nm, st);
   else if (rel_runs.nadm <= 1)
-    nlist = k1_phase_a<1, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<1, false>(v, R, s, rel_runs, s_runs, nruns, nm, st);
   else if (rel_runs.nadm == 2)
-    nlist = k1_phase_a<2, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<2, false>(v, R, s, rel_runs, s_runs, nruns, nm, st);
   else
-    nlist = k1_phase_a<4, false>(v, R, s, d.rdiv, rel_runs, s_runs, nruns, nm, st);
+    nlist = k1_phase_a<4, false>(v, R, s, rel_runs, s_runs, nruns, nm, st);
   if ((MODE & 16) || nlist == 0) return p;  // MODE 16 (diagnostic): phase A only
   __builtin_amdgcn_wave_barrier();
   // phase B1 over the list: a row's entries are consecutive (slot order), so
   // its first entry records the row's first list index and its last entry the
-  // end; TN is OR-ed into the row's half word
+  // end; TN is OR-ed into the row's half word.  The lowest and highest listed
+  // rows bound the groups B2 visits.
+  uint32_t rlo = kNoRow, rhi = 0;
 #pragma unroll 1
   for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
+    uint32_t row = kNoRow;
     if (i < nlist) {
       const uint32_t x = st.lx[i];
-      const uint32_t row = st.lrow[i];
-      const uint32_t prow = i ? st.lrow[i - 1] : 0xFFFFu;
-      const uint32_t nrow = i + 1 < nlist ? st.lrow[i + 1] : 0xFFFFu;
-      if (row != prow) st.hd[row] = static_cast<uint16_t>(i);
-      if (row != nrow) st.tl[row] = static_cast<uint16_t>(i + 1);
-      atomicOr(&st.tn[row >> 1], static_cast<uint32_t>(tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm)
-                                     << ((row & 1u) << 4));
+      row = k1_row(st.lrel[i], rem, rdiv);
+      if (row != kNoRow) {
+        const uint32_t prow = i ? k1_row(st.lrel[i - 1], rem, rdiv) : kNoRow;
+        const uint32_t nrow = i + 1 < nlist ? k1_row(st.lrel[i + 1], rem, rdiv) : kNoRow;
+        if (row != prow) st.hd[row] = static_cast<uint16_t>(i);
+        if (row != nrow) st.tl[row] = static_cast<uint16_t>(i + 1);
+        atomicOr(&st.tn[row >> 1], static_cast<uint32_t>(tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm)
+                                       << ((row & 1u) << 4));
+      }
+    }
+    // listed rows are increasing along the list: the chunk's first / last valid lanes hold its extremes
+    const uint64_t vm = __builtin_amdgcn_ballot_w64(row != kNoRow);
+    if (vm) {
+      const uint32_t a = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), __builtin_ctzll(vm)));
+      const uint32_t z = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), 63 - __builtin_clzll(vm)));
+      rlo = min(rlo, a);
+      rhi = max(rhi, z);
     }
   }
   __builtin_amdgcn_wave_barrier();
+  if (rlo == kNoRow) return p;  // only window slots outside the tile's rows
   if (MODE & 32) {  // diagnostic: phase A + B1 only
     for (uint32_t r = lane; r < rpt; r += 2 * kWave) st.tn[r >> 1] = 0;
     return p;
   }
-  // phase B2, one lane per row of the tile: verify the rows with contributors;
-  // a row's half word then holds its T_state (0: not in S)
+  // phase B2, one lane per row of the groups [g0, g1) that hold listed rows: verify the rows with
+  // contributors; a row's half word then holds its T_state (0: not in S)
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
+  const uint32_t g0 = rlo / kWave, g1 = rhi / kWave + 1;
   uint32_t any = 0;
 #pragma unroll 1
-  for (uint32_t r0 = 0; r0 < rpt; r0 += kWave) {
-    const uint32_t row = r0 + lane;
+  for (uint32_t gi = g0; gi < g1; ++gi) {
+    const uint32_t row = gi * kWave + lane;
     uint16_t T = 0;
-    if (row < rpt) {
+    if (row <= rhi) {
       const uint16_t TN = tn16[row];
       if (TN) {
-        if (row0 + row < d.nrows) {
-          const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
-          T = keep_fast(tu, TN, keep, s_adj);
-          if (!T) {
-            acc.removed = 1;
-          } else if (oa.nranks <= 1) {
-            acc.vs += 1;
-            acc.es += cnt;
-          } else {
-            acc_owner(s_hist, oa, d.start + row0 + row, cnt);
-          }
+        const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
+        T = keep_fast(tu, TN, keep, s_adj);
+        if (!T) {
+          acc.removed = 1;
+        } else if (oa.nranks <= 1) {
+          acc.vs += 1;
+          acc.es += cnt;
+        } else {
+          acc_owner(s_hist, oa, ustart + row, cnt);
         }
         tn16[row] = T;
       }
     }
     const uint64_t b = __builtin_amdgcn_ballot_w64(T != 0);
-    if (lane == 0) st.sm[r0 / kWave] = b;
+    if (lane == 0) st.sm[gi] = b;
     any += static_cast<uint32_t>(__builtin_popcountll(b));
   }
   p.nlist = nlist;
-  p.ngroups = (rpt + kWave - 1) / kWave;
+  p.g0 = g0;
+  p.g1 = g1;
   p.any = any;
   return p;
 }
@@ -621,7 +624,8 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
     return;
   }
   // the mask words that hold survivors (the slist build stops at the tile's count)
-  if (!(MODE & 64) && !o.rarea && static_cast<uint32_t>(lane) < p.ngroups) p.tm[lane] = st.sm[lane];  // bit r = row r
+  if (!(MODE & 64) && !o.rarea && static_cast<uint32_t>(lane) < p.g1)
+    p.tm[lane] = static_cast<uint32_t>(lane) >= p.g0 ? st.sm[lane] : 0ull;  // bit r = row r
   // dense M: the tile's whole contributor list is appended to the wave's own
   // slice of the region (coalesced; a cursor in scalar registers, no atomics:
   // one counter shared by the grid serialised 2.5 M atomics and cost 20 ms),
@@ -632,7 +636,7 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
   if (dense) dcur += p.nlist;
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
 #pragma unroll 1
-  for (uint32_t gi = 0; gi < p.ngroups; ++gi) {
+  for (uint32_t gi = p.g0; gi < p.g1; ++gi) {
     const uint64_t m = uniform64(st.sm[gi]);
     if (!m) continue;
     const uint64_t rslot = rcur + __builtin_popcountll(m & ((1ull << lane) - 1));
@@ -682,8 +686,8 @@ __device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stag
   for (uint32_t i0 = 0; i0 < p.nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
     if (i < p.nlist) {
-      const uint32_t row = st.lrow[i];
-      if ((st.sm[row / kWave] >> (row % kWave)) & 1ull)
+      const uint32_t row = k1_row(st.lrel[i], p.rem, p.rdiv);
+      if (row != kNoRow && ((st.sm[row / kWave] >> (row % kWave)) & 1ull))  // (listed rows lie in [g0, g1))
         *reinterpret_cast<uint32_t*>(mtile + ((row * p.g + (i - st.hd[row])) << 2)) = st.lx[i] | kAlive;
     }
   }
@@ -760,9 +764,9 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
 // and the label test (checksum), bit4 stops light tiles after phase A, bit5
 // after phase B1.  WIDE: some range has more than four
 // relevant label runs (tbits_rel scans them all).
-template <int MODE, bool WIDE = false, int WMIN = 6>
+template <int MODE, bool WIDE = false, int WMIN = 8>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8))) void k_lcc_first(
-    const KRange* __restrict__ ktab, uint32_t nr, uint32_t ntiles, const HSeg* __restrict__ hseg,
+    const KRange* __restrict__ ktab, const uint64_t* __restrict__ ttab, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
     K1Out o, uint32_t* __restrict__ hscr, uint32_t nheavy, uint32_t nhseg, unsigned long long* __restrict__ tmask,
     Partials pp) {
@@ -782,42 +786,51 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform
   K1Stage& st = s_stage[wid];
-  for (int i = threadIdx.x % kWave; i < static_cast<int>(kTileEntries / 2); i += kWave) st.tn[i] = 0;
+  for (int i = threadIdx.x % kWave; i < static_cast<int>(kTileRows / 2); i += kWave) st.tn[i] = 0;
   __syncthreads();
   BlockAcc acc;
-  const uint32_t W = gridDim.x * kWpb;
+  // (wave-uniform: left to the compiler the grid stride lands in a VGPR, the next-tile test becomes a
+  // divergent branch and every loop-carried tile field a VGPR copied and re-read each iteration)
+  const uint32_t W = __builtin_amdgcn_readfirstlane(gridDim.x * kWpb);
   const int nruns = lr.n;
-  uint32_t r = 0;
-  uint32_t t = blockIdx.x * kWpb + wid;
-  // the next tile's slots are in flight while the current one is processed
+  const TTab tt = (TTab)ttab;
+  const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWpb + wid);
+  // tiles t = (j W + gw) kTileBlock + i; descriptors read one tile ahead of the loads they address, the
+  // slots of the next tile in flight while the current one is processed
+  uint32_t t = gw * kTileBlock;
+  uint32_t tn = k1_next(t, W);
+  uint64_t wcur = t < ntiles ? tt[t] : 0ull, wnx = tn < ntiles ? tt[tn] : 0ull;
   uint32_t vc[kSub], vn[kSub];
-  K1Desc cur{};
-  if (t < ntiles) cur = k1_desc(kt, r, t);
-  uint32_t sc = k1_load(vc, cur, colp, t < ntiles);
+  const uint32_t voff = 16u * static_cast<uint32_t>(lane_id());  // byte offset of the lane's 16 B in a load
+  uint32_t sc = k1_load(vc, wcur, colp, voff);
   K1Pend pend{};  // the previous light tile's stores
   // dense M: this wave's slice of the region
-  uint64_t dcur = uniform64((uint64_t(blockIdx.x) * kWpb + wid) * o.dslice);
+  uint64_t dcur = uniform64(uint64_t(gw) * o.dslice);
   const uint64_t dend = uniform64(dcur + o.dslice);
   // dense mode: this wave's record slice
-  const uint32_t gw = blockIdx.x * kWpb + wid;
   uint64_t rcur = o.rarea ? uniform64(o.rbase[gw]) : 0;
   while (t < ntiles) {
     t = __builtin_amdgcn_readfirstlane(t);
-    const uint32_t tn = t + W;
+    tn = __builtin_amdgcn_readfirstlane(tn);
+    wcur = uniform64(wcur);
+    wnx = uniform64(wnx);
+    // this tile's slots (loaded a whole tile ago) and the stores before them are complete here, ahead
+    // of the new stores and loads: the vector memory counter retires in issue order, so a wait at the
+    // first use would also wait for the stores issued below
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     // the previous tile's stores go out ahead of the next tile's loads
     k1_pend_uniform(pend);
     dcur = uniform64(dcur);
     rcur = uniform64(rcur);
     k1_flush<MODE>(pend, o, st, dcur, dend, rcur);
     pend.tm = nullptr;
-    K1Desc nxt{};
-    if (tn < ntiles) nxt = k1_desc(kt, r, tn);
-    const uint32_t sn = k1_load(vn, nxt, colp, tn < ntiles);
-    k1_uniform(cur);
+    const uint32_t sn = k1_load(vn, wnx, colp, voff);
+    const uint32_t tnn = k1_next(tn, W);
+    const uint64_t wnn = tnn < ntiles ? tt[tnn] : 0ull;
     sc = __builtin_amdgcn_readfirstlane(sc);
-    const KTab R = kt + cur.r;
-    unsigned long long* tm = tmask + uint64_t(t) * kSub;
-    if (cur.kind < static_cast<uint32_t>(kHeavyKind)) {
+    const uint32_t rem = ttab_rem(wcur);
+    if (rem) {  // a light tile (heavy tiles: the loop below)
+      const KTab R = kt + ttab_range(wcur);
       const uint16_t tu = R->tu;
       const uint16_t nm = R->nm;
       const RelRuns rel_runs = load_rel(R);
@@ -826,12 +839,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
         for (int q = 0; q < kSub; ++q) acc.vs += vc[q] ^ tbits_rel<WIDE>(vc[q], rel_runs, s_runs, nruns);
       } else if (!(MODE & 2)) {
         const KeepArgs keep = load_keep(R);
-        pend = k1_light_tile<MODE, WIDE>(vc, sc, cur, R, tu, nm, rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist,
-                                         tm, t, st);
+        const uint32_t rpt = R->rpt;
+        const uint32_t ustart = R->start + (t - R->tile0) * rpt;
+        unsigned long long* tm = tmask + uint64_t(t) * kSub;
+        pend = k1_light_tile<MODE, WIDE>(vc, sc, ttab_slot(wcur), rem, ustart, R->g, rpt, R->rdiv, R, tu, nm,
+                                         rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist, tm, t, st);
       }
-    }  // heavy tiles: the loop below
+    }
     t = tn;
-    cur = nxt;
+    tn = tnn;
+    wcur = wnx;
+    wnx = wnn;
     sc = sn;
 #pragma unroll
     for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
@@ -1524,6 +1542,7 @@ void build_tiling(Ctx& c) {
   }
   std::vector<KRange> tab;
   std::vector<HSeg> hs;
+  std::vector<uint64_t> ttab;  // tile descriptors (kTtabRemShift / kTtabRangeShift)
   uint32_t tiles = 0, nheavy = 0;
   c.ss0_trav = 0;
   c.ss0_rows = 0;
@@ -1586,7 +1605,7 @@ void build_tiling(Ctx& c) {
       R.kind = static_cast<uint32_t>(kind);
       if (kind < kHeavyKind) {
         R.g = kind_slots(static_cast<uint32_t>(kind));
-        R.rpt = (kTileEntries - 4) / R.g;
+        R.rpt = std::min<uint32_t>((kTileEntries - 4) / R.g, kTileRows);
         R.rdiv = ((1u << 19) + R.g - 1) / R.g;
         for (uint32_t sh = 0; sh < 4; ++sh)
           for (uint32_t sl = 0; sl < R.rpt * R.g; sl += R.g) {  // tile slot sl sits at load offset sl + sh
@@ -1648,7 +1667,20 @@ void build_tiling(Ctx& c) {
         }
         nt = hs.size() - R.aux;
       }
-      if (uint64_t(tiles) + nt >= 0xFFFFFFFFull) throw std::runtime_error("superstep-0 tiling exceeds 2^32 tiles");
+      if (uint64_t(tiles) + nt >= 0xFFFFFFFFull - 2ull * kPartGridMax * kWpb * kTileBlock)
+        throw std::runtime_error("superstep-0 tiling exceeds 2^32 tiles");
+      const uint64_t rfield = uint64_t(tab.size()) << kTtabRangeShift;
+      if (tab.size() >= (1u << (64 - kTtabRangeShift - 7))) throw std::runtime_error("internal: tile range index");
+      for (uint64_t k = 0; k < nt; ++k) {
+        if (kind >= kHeavyKind) {  // heavy segment tile: loads nothing in the light loop
+          ttab.push_back(rfield);
+          continue;
+        }
+        const uint64_t rows = std::min<uint64_t>(R.rpt, (b - a) - k * R.rpt);
+        const uint64_t qb = R.qbase + k * R.rpt * R.g;
+        if (qb >> kTtabRemShift) throw std::runtime_error("superstep-0 tile slot exceeds 2^36");
+        ttab.push_back(qb | ((rows * R.g) << kTtabRemShift) | rfield);
+      }
       tiles += static_cast<uint32_t>(nt);
       tab.push_back(R);
     }
@@ -1671,6 +1703,8 @@ void build_tiling(Ctx& c) {
   c.nheavy = nheavy;
   c.nhseg = static_cast<uint32_t>(hs.size());
   if (c.d_ktab) (void)hipFree(c.d_ktab);
+  if (c.d_ttab) (void)hipFree(c.d_ttab);
+  c.d_ttab = nullptr;
   if (c.d_hseg) (void)hipFree(c.d_hseg);
   if (c.d_hscr) (void)hipFree(c.d_hscr);
   if (c.d_tmask) (void)hipFree(c.d_tmask);
@@ -1686,6 +1720,9 @@ void build_tiling(Ctx& c) {
   c.d_scan_tmp = nullptr;
   PM_HIP_CHECK(hipMalloc(&c.d_ktab, tab.size() * sizeof(KRange)));
   PM_HIP_CHECK(hipMemcpy(c.d_ktab, tab.data(), tab.size() * sizeof(KRange), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMalloc(&c.d_ttab, std::max<size_t>(1, ttab.size()) * sizeof(uint64_t)));
+  if (!ttab.empty())
+    PM_HIP_CHECK(hipMemcpy(c.d_ttab, ttab.data(), ttab.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   PM_HIP_CHECK(hipMalloc(&c.d_hseg, std::max<size_t>(1, hs.size()) * sizeof(HSeg)));
   if (!hs.empty()) PM_HIP_CHECK(hipMemcpy(c.d_hseg, hs.data(), hs.size() * sizeof(HSeg), hipMemcpyHostToDevice));
   PM_HIP_CHECK(hipMalloc(&c.d_hscr, std::max<size_t>(1, 3 * size_t(nheavy)) * sizeof(uint32_t)));
@@ -1698,7 +1735,7 @@ void build_tiling(Ctx& c) {
   PM_HIP_CHECK(hipMalloc(&c.d_scan_tmp, std::max<size_t>(1, c.scan_tmp_bytes)));
   c.k1_grid = lcc_first_grid(c);
   // record slices of the superstep-0 waves (dense mode): each wave's bound is the rows of the light tiles
-  // it visits (tiles t, t + W, ... of a persistent grid of W waves)
+  // it visits (tile t goes to wave (t / kTileBlock) % W of a persistent grid of W waves)
   {
     void* ptrs[] = {c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.d_hrec, c.d_srec, c.d_rscan_tmp};
     for (void* q : ptrs)
@@ -1715,7 +1752,8 @@ void build_tiling(Ctx& c) {
         const KRange& R = tab[r];
         if (R.kind >= static_cast<uint32_t>(kHeavyKind)) continue;
         const uint64_t nrows = R.end - R.start, nt = (nrows + R.rpt - 1) / R.rpt;
-        for (uint64_t k = 0; k < nt; ++k) rows[(R.tile0 + k) % W] += std::min<uint64_t>(R.rpt, nrows - k * R.rpt);
+        for (uint64_t k = 0; k < nt; ++k)
+          rows[((R.tile0 + k) / kTileBlock) % W] += std::min<uint64_t>(R.rpt, nrows - k * R.rpt);
       }
       uint64_t tot = 0;
       for (uint32_t w = 0; w < W; ++w) {
@@ -1786,8 +1824,7 @@ static K1Out k1_out(Ctx& c, unsigned grid) {
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
   if (c.ntiles == 0) return;
 #define PM_K1_ARGS                                                                                                    \
-  dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab,                                    \
-      static_cast<uint32_t>(c.ktab.size() - 1), c.ntiles, c.d_hseg,                                                  \
+  dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab, c.d_ttab, c.ntiles, c.d_hseg,                                                  \
       c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c, grid), c.d_hscr, c.nheavy, c.nhseg,                         \
       reinterpret_cast<unsigned long long*>(c.d_tmask), partials(c, d_slot)
   switch (variant) {
