@@ -1644,22 +1644,24 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
 const char* pm_build_arch(void) { return "gfx950"; }
 
 // Diagnostics: times `reps` launches of the superstep-0 kernel on the current
-// labels (state is reset first).  variant < 256: diagnostic MODE of the
-// kernel on the default grid; variant >= 256: the product kernel on a grid of
-// `variant` blocks.
+// labels (state is reset first).  variant < 65536: diagnostic MODE of the
+// kernel on the default grid (dense M whenever light tiles run, as in the
+// product); variant >= 65536: the product kernel on a grid of variant - 65536
+// blocks.
 int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
   PM_API_BODY(ctx, {
     pm::reset_state(*ctx);
     hipEvent_t a, b;
     PM_HIP_CHECK(hipEventCreate(&a));
     PM_HIP_CHECK(hipEventCreate(&b));
-    const unsigned grid = variant >= 256 ? std::min<unsigned>(static_cast<unsigned>(variant), pm::kPartGridMax)
-                                         : ctx->k1_grid;
-    const int mode = variant >= 256 ? 0 : variant;
+    const unsigned grid = variant >= 65536 ? std::min<unsigned>(static_cast<unsigned>(variant - 65536), pm::kPartGridMax)
+                                           : ctx->k1_grid;
+    const int mode = variant >= 65536 ? 0 : variant;
+    const bool dense = !(mode & 2);
     pm::ensure_counts(*ctx, 1);
     pm::lcc_first_prepare(*ctx);
     // the product launch writes dense M when the search would
-    if (mode == 0 || mode == 5) pm::lcc_first_set_dense(*ctx);
+    if (dense) pm::lcc_first_set_dense(*ctx);
     pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);  // warm (partials not reduced)
     // each timed launch starts from cleared heavy-row tickets (the last segment of a heavy row runs its
     // verify), the memsets outside the events
@@ -1667,7 +1669,7 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     for (int i = 0; i < reps; ++i) {
       pm::lcc_first_prepare(*ctx);
       PM_HIP_CHECK(hipMemsetAsync(ctx->d_tcode, 0, ((ctx->n + 15) / 16 + 1) * sizeof(uint32_t), ctx->stream));
-      if (mode == 0 || mode == 5) pm::lcc_first_set_dense(*ctx);
+      if (dense) pm::lcc_first_set_dense(*ctx);
       PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
       pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);
       PM_HIP_CHECK(hipEventRecord(b, ctx->stream));

@@ -462,42 +462,22 @@ __device__ __forceinline__ uint32_t k1_phase_a(const uint32_t (&v)[kSub], KTab R
   return nlist;
 }
 
-// A light tile's global stores, issued at the top of the next iteration (no
-// store is issued between a tile's prefetch loads and their first use, so the
-// wait for those loads never waits for a store as well).
-struct K1Pend {
-  unsigned long long* tm;  // the tile's survivor mask words (null: nothing pending)
-  uint64_t mbase;          // first M slot of the tile
-  uint32_t ustart;         // position of the tile's first row
-  uint32_t g;              // slots per row
-  uint32_t nlist;          // staged contributors
-  uint32_t g0, g1;         // 64-row groups [g0, g1) that hold verified rows (g1 = 0: none)
-  uint32_t any;            // survivors of the tile
-  uint32_t tile;           // tile index
-  uint32_t tu;             // template bits of the tile's label
-  uint32_t rem;            // slots of the tile's rows (rows * g)
-  uint32_t rdiv;           // row of a tile slot = (slot * rdiv) >> 19
-};
-
-__device__ __forceinline__ void k1_pend_uniform(K1Pend& p) {
-  p.tm = reinterpret_cast<unsigned long long*>(uniform64(reinterpret_cast<uint64_t>(p.tm)));
-  p.mbase = uniform64(p.mbase);
-  p.ustart = __builtin_amdgcn_readfirstlane(p.ustart);
-  p.g = __builtin_amdgcn_readfirstlane(p.g);
-  p.nlist = __builtin_amdgcn_readfirstlane(p.nlist);
-  p.g0 = __builtin_amdgcn_readfirstlane(p.g0);
-  p.g1 = __builtin_amdgcn_readfirstlane(p.g1);
-  p.any = __builtin_amdgcn_readfirstlane(p.any);
-  p.tile = __builtin_amdgcn_readfirstlane(p.tile);
-  p.tu = __builtin_amdgcn_readfirstlane(p.tu);
-  p.rem = __builtin_amdgcn_readfirstlane(p.rem);
-  p.rdiv = __builtin_amdgcn_readfirstlane(p.rdiv);
-}
-
 // Row of a staged entry of a tile (kNoRow: a window slot outside the tile's rows).
 static constexpr uint32_t kNoRow = 0xFFFFu;
 __device__ __forceinline__ uint32_t k1_row(uint32_t rel, uint32_t rem, uint32_t rdiv) {
   return rel < rem ? (__umul24(rel, rdiv) >> 19) : kNoRow;
+}
+
+// Inclusive prefix sum over the wave's 64 lanes (DPP: four row shifts, then
+// the row-15 and row-31 broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xF, 0xF, true));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xF, 0xF, true));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xF, 0xF, true));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xF, 0xF, true));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xA, 0xF, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xC, 0xF, false));
+  return x;
 }
 
 // Light tile: rem = rows * g slots from slot qb of rows of g slots (R->rpt = min((kTileEntries - 4) / g,
@@ -507,20 +487,30 @@ __device__ __forceinline__ uint32_t k1_row(uint32_t rel, uint32_t rem, uint32_t 
 // compare per run, the masks OR-ed on the scalar unit) and it is the first
 // occurrence in its row (row start, or differs from its left neighbour);
 // only the contributing lanes (a few percent of the slots) are appended to
-// the LDS staging list.  Phase B: row TN / first and last list index from the
-// list (B1, entries outside the tile's rows dropped), one lane per row of the
-// groups that hold listed rows verifies and leaves T_state in the row's half
-// word (B2); the stores (state, survivor mask, M) wait in LDS for k1_flush.
+// the LDS staging list.  Phase B1: row TN / first and last list index from
+// the list (entries outside the tile's rows dropped).  Phase B2, one lane per
+// row of the groups that hold listed rows: verify, and the survivors' state
+// goes out at once.  Dense M (o.rarea): one 16-B record per survivor in the
+// wave's record slice {position, T_pub | |M| << 16, first M entry, 0}
+// (T_state = T_pub and the alive count = |M| are implied until the first later
+// superstep rewrites them) and the survivors' M entries compacted into the
+// wave's slice of the dense region (the records' first entries are the
+// exclusive prefix sums of |M| over the tile's survivors); otherwise
+// position-indexed state, survivor mask words, the tile's count, and M at the
+// start of each survivor's padded row; the 2-bit T_pub code OR-ed into tcode.
+// The stores are issued
+// in place: held back to the next iteration they cost more (the pending
+// state's registers) than the wait for them at its top.
 template <int MODE, bool WIDE>
-__device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, uint64_t qb, uint32_t rem,
-                                                uint32_t ustart, uint32_t g, uint32_t rpt, uint32_t rdiv, KTab R,
-                                                uint16_t tu, uint16_t nm, const RelRuns& rel_runs,
-                                                const uint32_t* s_runs, int nruns, const KeepArgs& keep,
-                                                const uint16_t* s_adj, const OwnerArgs& oa, BlockAcc& acc,
-                                                unsigned long long* s_hist, unsigned long long* tm, uint32_t tile,
-                                                K1Stage& st) {
+__device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_t s, uint64_t qb, uint32_t rem,
+                                              uint32_t ustart, uint32_t rows, uint32_t g, uint32_t rpt,
+                                              uint32_t rdiv, KTab R, uint16_t tu, uint16_t nm,
+                                              const RelRuns& rel_runs, const uint32_t* s_runs, int nruns,
+                                              const KeepArgs& keep, const uint16_t* s_adj, const OwnerArgs& oa,
+                                              BlockAcc& acc, unsigned long long* s_hist, unsigned long long* tm,
+                                              uint32_t tile, K1Stage& st, const K1Out& o, uint64_t& dcur,
+                                              uint64_t dend, uint64_t& rcur) {
   const int lane = lane_id();
-  K1Pend p{tm, qb, ustart, g, 0u, 0u, 0u, 0u, tile, tu, rem, rdiv};
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
   if (WIDE || rel_runs.nadm > 4)
@@ -531,7 +521,17 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
     nlist = k1_phase_a<2, false>(v, R, s, rel_runs, s_runs, nruns, nm, st);
   else
     nlist = k1_phase_a<4, false>(v, R, s, rel_runs, s_runs, nruns, nm, st);
-  if ((MODE & 16) || nlist == 0) return p;  // MODE 16 (diagnostic): phase A only
+  nlist = __builtin_amdgcn_readfirstlane(nlist);
+  if (MODE & 16) return;  // diagnostic: phase A only
+  // position-indexed mode: the slist build reads every tile's count
+  const bool counts = !o.rarea && !(MODE & 128);
+  if (nlist == 0) {
+    if (counts && lane == 0) {
+      o.tcnt[tile] = 0u;
+      o.tstart[tile] = ustart;
+    }
+    return;
+  }
   __builtin_amdgcn_wave_barrier();
   // phase B1 over the list: a row's entries are consecutive (slot order), so
   // its first entry records the row's first list index and its last entry the
@@ -564,24 +564,34 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
     }
   }
   __builtin_amdgcn_wave_barrier();
-  if (rlo == kNoRow) return p;  // only window slots outside the tile's rows
+  if (rlo == kNoRow) {  // only window slots outside the tile's rows
+    if (counts && lane == 0) {
+      o.tcnt[tile] = 0u;
+      o.tstart[tile] = ustart;
+    }
+    return;
+  }
   if (MODE & 32) {  // diagnostic: phase A + B1 only
     for (uint32_t r = lane; r < rpt; r += 2 * kWave) st.tn[r >> 1] = 0;
-    return p;
+    return;
   }
-  // phase B2, one lane per row of the groups [g0, g1) that hold listed rows: verify the rows with
-  // contributors; a row's half word then holds its T_state (0: not in S)
+  // phase B2 over the groups [g0, g1) that hold listed rows
   uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
   const uint32_t g0 = rlo / kWave, g1 = rhi / kWave + 1;
+  // dense M when the tile's list fits the rest of the wave's slice (the survivors' entries are a part of it)
+  const bool dense = o.rarea && dcur + nlist <= dend;
+  const uint64_t dpos = dcur;
+  uint32_t mrun = 0;  // survivors' M entries of the groups before this one
   uint32_t any = 0;
 #pragma unroll 1
   for (uint32_t gi = g0; gi < g1; ++gi) {
     const uint32_t row = gi * kWave + lane;
     uint16_t T = 0;
+    uint32_t cnt = 0;
     if (row <= rhi) {
       const uint16_t TN = tn16[row];
       if (TN) {
-        const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
+        cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
         T = keep_fast(tu, TN, keep, s_adj);
         if (!T) {
           acc.removed = 1;
@@ -591,106 +601,82 @@ __device__ __forceinline__ K1Pend k1_light_tile(const uint32_t (&v)[kSub], uint3
         } else {
           acc_owner(s_hist, oa, ustart + row, cnt);
         }
-        tn16[row] = T;
+        tn16[row] = 0;  // (TN words are zero between tiles)
       }
     }
-    const uint64_t b = __builtin_amdgcn_ballot_w64(T != 0);
+    const bool surv = T != 0;
+    const uint64_t b = __builtin_amdgcn_ballot_w64(surv);
     if (lane == 0) st.sm[gi] = b;
+    if (!b) continue;
     any += static_cast<uint32_t>(__builtin_popcountll(b));
-  }
-  p.nlist = nlist;
-  p.g0 = g0;
-  p.g1 = g1;
-  p.any = any;
-  return p;
-}
-
-// The pending stores of a light tile: survivor mask words, T_state / T_pub /
-// |M| of the survivors (consecutive positions: coalesced), M[u] of the
-// survivors in slot order at the start of u's padded row; leaves the tile's
-// TN words zero.
-template <int MODE>
-__device__ __forceinline__ void k1_flush(const K1Pend& p, const K1Out& o, K1Stage& st, uint64_t& dcur,
-                                         uint64_t dend, uint64_t& rcur) {
-  const int lane = lane_id();
-  if (!p.tm) return;
-  if (lane == 0 && !o.rarea) {  // (dense mode: the slist comes from the records)
-    o.tcnt[p.tile] = p.any;
-    o.tstart[p.tile] = p.ustart;
-  }
-  if (!p.any) {
-    // no survivor: the half words of verified rows are already 0; the slist build reads no mask word of a
-    // tile without survivors
-    return;
-  }
-  // the mask words that hold survivors (the slist build stops at the tile's count)
-  if (!(MODE & 64) && !o.rarea && static_cast<uint32_t>(lane) < p.g1)
-    p.tm[lane] = static_cast<uint32_t>(lane) >= p.g0 ? st.sm[lane] : 0ull;  // bit r = row r
-  // dense M: the tile's whole contributor list is appended to the wave's own
-  // slice of the region (coalesced; a cursor in scalar registers, no atomics:
-  // one counter shared by the grid serialised 2.5 M atomics and cost 20 ms),
-  // survivor u's M starts at list index hd[row] of it; a tile that no longer
-  // fits the slice keeps the padded-row layout
-  const uint64_t dpos = dcur;
-  const bool dense = o.rarea && dcur + p.nlist <= dend;
-  if (dense) dcur += p.nlist;
-  uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
-#pragma unroll 1
-  for (uint32_t gi = p.g0; gi < p.g1; ++gi) {
-    const uint64_t m = uniform64(st.sm[gi]);
-    if (!m) continue;
-    const uint64_t rslot = rcur + __builtin_popcountll(m & ((1ull << lane) - 1));
-    if (o.rarea) rcur = uniform64(rcur + __builtin_popcountll(m));
-    if ((m >> lane) & 1ull) {
-      const uint32_t row = gi * kWave + lane;
-      const uint16_t T = tn16[row];
-      const uint32_t cnt = static_cast<uint32_t>(st.tl[row]) - st.hd[row];
-      tn16[row] = 0;
+    // the survivors' first M entries in the tile's compacted M: exclusive prefix of |M| over them
+    const uint32_t c = surv ? cnt : 0u;
+    const uint32_t incl = wave_incl_sum(c);
+    if (surv) {
+      const uint32_t code = tpub_code(T, tu);
       if (!(MODE & 128)) {
         // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
-        const uint32_t u = p.ustart + row, b2 = u * 2u, b4 = u * 4u;
-        // dense mode: one 16-B record in the wave's slice (consecutive survivors: coalesced) instead of
-        // position-indexed stores that land in partial cache lines; T_state (= T_pub) and the alive
-        // count (= |M|) are implied: the first later superstep, the only reader before they are
-        // rewritten, takes them from the record.  A tile outside the M region: its state arrays, and a
-        // record without a first entry.  A label of more than two template vertices keeps its
-        // position-indexed T_pub (the next superstep's code-3 gathers).
-        const uint32_t code = tpub_code(T, p.tu);
+        const uint32_t u = ustart + row, b2 = u * 2u, b4 = u * 4u;
+        if (!(MODE & 512)) atomicOr(&o.tcode[u >> 4], code << ((u & 15u) << 1));
         if (o.rarea) {
           if (!dense) {
             *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
             *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
             *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
           }
+          // a label of more than two template vertices keeps its position-indexed T_pub (the next
+          // superstep's code-3 gathers)
           if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
-          o.rarea[rslot] = make_uint4(u, T | (cnt << 16), dense ? static_cast<uint32_t>(dpos + st.hd[row]) : kNone, 0u);
+          const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0));
+          o.rarea[rslot] =
+              make_uint4(u, T | (cnt << 16), dense ? static_cast<uint32_t>(dpos + mrun + incl - c) : kNone, 0u);
         } else {
           *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
           *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
           *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = cnt;
           *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
         }
-        atomicOr(&o.tcode[u >> 4], code << ((u & 15u) << 1));
       }
+      if (!dense) st.hd[row] = static_cast<uint16_t>(mrun + incl - c);  // (the padded M copy below)
+    }
+    if (o.rarea) rcur = uniform64(rcur + __builtin_popcountll(b));
+    mrun += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), kWave - 1));
+  }
+  if (counts) {  // survivor mask words (bit r = row r) up to the last group with listed rows; the count
+    if (static_cast<uint32_t>(lane) < g1) tm[lane] = static_cast<uint32_t>(lane) >= g0 ? st.sm[lane] : 0ull;
+    if (lane == 0) {
+      o.tcnt[tile] = any;
+      o.tstart[tile] = ustart;
     }
   }
+  if (!any) return;
   if (MODE & 129) return;  // diagnostics: without the M stores
-  if (dense) {
-    uint32_t* const dm = o.mcol + o.dbase + dpos;
+  // the survivors' entries in list order: entry i is the kidx-th kept one, and the kidx - hd[r]-th of its
+  // row r (hd: the row's first entry in the compacted M)
+  uint32_t* const dm = o.mcol + o.dbase + dpos;
+  char* const mtile = reinterpret_cast<char*>(o.mcol + qb);  // 32-bit in-tile offsets
+  uint32_t base = 0;
 #pragma unroll 1
-    for (uint32_t i = lane; i < p.nlist; i += kWave) dm[i] = st.lx[i] | kAlive;
-    return;
-  }
-  char* const mtile = reinterpret_cast<char*>(o.mcol + p.mbase);  // 32-bit in-tile offsets
-#pragma unroll 1
-  for (uint32_t i0 = 0; i0 < p.nlist; i0 += kWave) {
+  for (uint32_t i0 = 0; i0 < nlist; i0 += kWave) {
     const uint32_t i = i0 + lane;
-    if (i < p.nlist) {
-      const uint32_t row = k1_row(st.lrel[i], p.rem, p.rdiv);
-      if (row != kNoRow && ((st.sm[row / kWave] >> (row % kWave)) & 1ull))  // (listed rows lie in [g0, g1))
-        *reinterpret_cast<uint32_t*>(mtile + ((row * p.g + (i - st.hd[row])) << 2)) = st.lx[i] | kAlive;
+    bool kept = false;
+    uint32_t row = kNoRow;
+    if (i < nlist) {
+      row = k1_row(st.lrel[i], rem, rdiv);
+      kept = row != kNoRow && ((st.sm[row / kWave] >> (row % kWave)) & 1ull);  // (listed rows lie in [g0, g1))
     }
+    const uint64_t kb = __builtin_amdgcn_ballot_w64(kept);
+    if (kept) {
+      const uint32_t kidx = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(kb >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(kb), 0));
+      const uint32_t x = st.lx[i] | kAlive;
+      if (dense) dm[kidx] = x;
+      else *reinterpret_cast<uint32_t*>(mtile + ((row * g + (kidx - st.hd[row])) << 2)) = x;
+    }
+    base += static_cast<uint32_t>(__builtin_popcountll(kb));
   }
+  if (dense) dcur = uniform64(dcur + mrun);
 }
 
 // Heavy rows (above kHeavyDeg): one kHeavyDeg segment per tile, uncompacted M;
@@ -759,7 +745,7 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
   return acc;
 }
 
-// MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores,
+// MODE (diagnostic builds only, 0 in the product): bit0 drops the M stores, bit9 the T_pub code atomics,
 // bit1 skips light tiles, bit2 skips heavy tiles, bit3 keeps only the loads
 // and the label test (checksum), bit4 stops light tiles after phase A, bit5
 // after phase B1.  WIDE: some range has more than four
@@ -803,7 +789,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
   uint32_t vc[kSub], vn[kSub];
   const uint32_t voff = 16u * static_cast<uint32_t>(lane_id());  // byte offset of the lane's 16 B in a load
   uint32_t sc = k1_load(vc, wcur, colp, voff);
-  K1Pend pend{};  // the previous light tile's stores
   // dense M: this wave's slice of the region
   uint64_t dcur = uniform64(uint64_t(gw) * o.dslice);
   const uint64_t dend = uniform64(dcur + o.dslice);
@@ -814,16 +799,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
     tn = __builtin_amdgcn_readfirstlane(tn);
     wcur = uniform64(wcur);
     wnx = uniform64(wnx);
-    // this tile's slots (loaded a whole tile ago) and the stores before them are complete here, ahead
-    // of the new stores and loads: the vector memory counter retires in issue order, so a wait at the
-    // first use would also wait for the stores issued below
+    // this tile's slots (requested a whole tile ago) and the previous tile's stores are complete here,
+    // ahead of the next tile's loads: the vector memory counter retires in issue order, so a wait at
+    // the first use would also wait for the stores this tile issues
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    // the previous tile's stores go out ahead of the next tile's loads
-    k1_pend_uniform(pend);
     dcur = uniform64(dcur);
     rcur = uniform64(rcur);
-    k1_flush<MODE>(pend, o, st, dcur, dend, rcur);
-    pend.tm = nullptr;
     const uint32_t sn = k1_load(vn, wnx, colp, voff);
     const uint32_t tnn = k1_next(tn, W);
     const uint64_t wnn = tnn < ntiles ? tt[tnn] : 0ull;
@@ -841,9 +822,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
         const KeepArgs keep = load_keep(R);
         const uint32_t rpt = R->rpt;
         const uint32_t ustart = R->start + (t - R->tile0) * rpt;
-        unsigned long long* tm = tmask + uint64_t(t) * kSub;
-        pend = k1_light_tile<MODE, WIDE>(vc, sc, ttab_slot(wcur), rem, ustart, R->g, rpt, R->rdiv, R, tu, nm,
-                                         rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist, tm, t, st);
+        const uint32_t rows = min(rpt, R->end - ustart);
+        k1_light_tile<MODE, WIDE>(vc, sc, ttab_slot(wcur), rem, ustart, rows, R->g, rpt, R->rdiv, R, tu, nm,
+                                  rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist, tmask + uint64_t(t) * kSub, t,
+                                  st, o, dcur, dend, rcur);
       }
     }
     t = tn;
@@ -854,10 +836,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
 #pragma unroll
     for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
   }
-  k1_pend_uniform(pend);
-  dcur = uniform64(dcur);
   rcur = uniform64(rcur);
-  k1_flush<MODE>(pend, o, st, dcur, dend, rcur);
   if (o.rarea && lane_id() == 0) o.rcnt[gw] = static_cast<uint32_t>(rcur - o.rbase[gw]);
   // heavy rows, one segment per wave at a time (a separate loop: no slot
   // buffers live, so the light loop's register budget is its own)
@@ -1843,6 +1822,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 32: hipLaunchKernelGGL(k_lcc_first<32>, PM_K1_ARGS); break;
     case 80: hipLaunchKernelGGL(k_lcc_first<80>, PM_K1_ARGS); break;
     case 128: hipLaunchKernelGGL(k_lcc_first<128>, PM_K1_ARGS); break;
+    case 512: hipLaunchKernelGGL(k_lcc_first<512>, PM_K1_ARGS); break;
     case 5: hipLaunchKernelGGL((k_lcc_first<0, false, 5>), PM_K1_ARGS); break;  // 5 waves/SIMD, no spills
 #endif
     default: throw std::runtime_error("unknown superstep-0 kernel variant (ablation variants: lib/libpm_diag.so)");

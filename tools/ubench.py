@@ -1,9 +1,9 @@
 """Superstep-0 kernel timing: diagnostic variants / grid sizes (one process, interleaved rounds).
 
 usage: ubench.py SCALE [P_GEN] [variant,variant,...]
-  variant < 256: diagnostic MODE (pm_kernels.hip k_lcc_first: 0 product, 1 no M stores,
+  variant < 65536: diagnostic MODE (pm_kernels.hip k_lcc_first: 0 product, 1 no M stores,
   8 loads + label test only, 2 skip light tiles, 4 skip heavy tiles, 16 phase A only,
-  32 phases A + B1); >= 256: product kernel on a grid of that many blocks.  The graph is generated on the GPU.
+  32 phases A + B1, 512 no T_pub code atomics); >= 65536: product kernel on a grid of variant - 65536 blocks.  The graph is generated on the GPU.
 """
 import ctypes
 import os
