@@ -267,6 +267,29 @@ def main():
                "edges": oe,
                "gpu_value_same_sample": round(ge / gsec, 1),
                "gpu_over_cpu_same_sample": round(ge / gsec / (oe / secs[1]), 1)}
+        # BASELINE.json configs[0] (C1): R-MAT S=21, P_gen=4, the reference's CPU-runnable case with 4 MPI
+        # ranks: the oracle as 4 emulated ranks on 4 threads, the GPU search on the same input beside it
+        g1 = pm.rmat_graph(21, 4, device=0)
+        r1 = [oracle.run(g1.off, g1.col, pattern_dir, None, nranks=4, max_iterations=args.max_iterations, threads=4)
+              for _ in range(3)]
+        s1 = sorted(r["seconds"] for r in r1)
+        m1 = pm.PatternMatcher(g1, pattern_dir, device=0)
+        for _ in range(2):
+            m1.run_beta("", args.max_iterations)
+        t1 = time.perf_counter()
+        q1 = [m1.run_beta("", args.max_iterations) for _ in range(10)]
+        gs1 = (time.perf_counter() - t1) / 10
+        m1.close()
+        e1 = edges_of(r1[0])
+        if (e1, r1[0]["final_vertices"], r1[0]["final_edges"]) != (edges_of(q1[-1]), q1[-1]["final_vertices"],
+                                                                   q1[-1]["final_edges"]):
+            invalid.append(f"C1 S=21: oracle edges {e1} |S| {r1[0]['final_vertices']} != GPU {edges_of(q1[-1])} "
+                           f"{q1[-1]['final_vertices']}")
+        cpu["c1_config"] = {"value": round(e1 / s1[1], 1), "unit": "edges/s", "cores": 4, "ranks": 4,
+                            "seconds": [round(x, 4) for x in s1], "edges": e1,
+                            "what": "BASELINE configs[0]: R-MAT S=21, P_gen=4, rmat_log2_tree_pattern, the oracle as 4 "
+                                    "ranks on 4 host threads (median of 3)",
+                            "gpu_value_same_input": round(edges_of(q1[-1]) / gs1, 1)}
         if os.path.exists(fx_path):
             ot = json.load(open(fx_path)).get("oracle_timing")
             if ot:

@@ -150,7 +150,10 @@ static constexpr uint32_t kTileRows = 256;
 static constexpr int kTtabRemShift = 36, kTtabRangeShift = 45;
 // Consecutive tiles a superstep-0 wave takes at a time (tile t goes to wave (t / kTileBlock) % W): the
 // tiles of a block share their range, whose fields then hit in the scalar cache
-static constexpr uint32_t kTileBlock = 4;
+#ifndef PM_TILE_BLOCK
+#define PM_TILE_BLOCK 4
+#endif
+static constexpr uint32_t kTileBlock = PM_TILE_BLOCK;
 // Light rows fit in one tile with room for the 16-B alignment shift of its
 // loads (a light tile holds at most kTileEntries - 4 slots).
 static constexpr uint32_t kLightMax = 480;
