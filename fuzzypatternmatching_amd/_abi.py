@@ -110,6 +110,8 @@ SIGNATURES = [
     ("pm_pattern_summary", ctypes.c_int, [c_char_p, c_char_p, c_u64]),
     ("pm_debug_time_lcc_first", ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     ("pm_debug_layout_stats", ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
+    ("pm_write_rmat_text", ctypes.c_int, [c_u64, c_u64, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(c_u64)]),
+    ("pm_write_label_text", ctypes.c_int, [c_vp, c_u64, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(c_u64)]),
     ("pm_debug_copy_gbs", ctypes.c_int, [ctypes.c_int, c_u64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     ("pm_debug_rccl_selftest", ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_int]),
     ("pm_build_arch", c_char_p, []),

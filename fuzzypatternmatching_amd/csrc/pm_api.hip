@@ -358,19 +358,23 @@ static void relayout(Ctx& c) {
   c.live_hint = ~0ull;
 }
 
-static void reset_state(Ctx& c) {
+// defer: the fills stay queued for the search's first launch (flush_zero batches them into one)
+static void reset_state(Ctx& c, bool defer = false) {
   if (c.tpub_clean && c.lcc_started) {
-    launch_clear_tpub(c);  // nonzero T_pub only at (every shard's) slist entries
-  } else if (!c.tpub_clean) {
-    PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[0], 0, c.n * sizeof(uint16_t), c.stream));
-    PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[1], 0, c.n * sizeof(uint16_t), c.stream));
+    c.clear_pending = true;  // nonzero T_pub only at (every shard's) slist entries; d_nS zeroed after the clear
+  } else {
+    if (!c.tpub_clean) {
+      PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[0], 0, c.n * sizeof(uint16_t), c.stream));
+      PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[1], 0, c.n * sizeof(uint16_t), c.stream));
+    }
+    zero_later(c, c.d_nS, sizeof(uint32_t));
   }
   c.tpub_clean = true;
   c.lines_prelaunched = false;  // (a failed search may leave one behind; the stream has run it)
   // d_tsm needs no reset: only sources are read, and selecting a source resets its entry
   c.smask_valid = false;
-  PM_HIP_CHECK(hipMemsetAsync(c.d_nS, 0, sizeof(uint32_t), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(c.d_flags, 0, 4 * sizeof(uint32_t), c.stream));
+  zero_later(c, c.d_flags, 4 * sizeof(uint32_t));
+  if (!defer) flush_zero(c);
   c.cur = 0;
   c.nS_host = 0;
   c.lcc_started = false;
@@ -423,7 +427,10 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     c.events.push_back(e);
   }
   std::vector<hipEvent_t>& ev = c.events;  // [0..D] superstep bounds, [D+1], [D+2] superstep-0 kernel
-  PM_HIP_CHECK(hipMemsetAsync(c.d_counts, 0, D * W * sizeof(uint64_t), c.stream));  // kernels add into the slots
+  zero_later(c, c.d_counts, D * W * sizeof(uint64_t));  // kernels add into the slots
+  // the search's reset fills go with superstep 0's own (one launch, before the call's timing event)
+  if (init_step) queue_lcc_first_fills(c);
+  flush_zero(c);
   PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
   bool k_timed = false;
   for (uint64_t ss = 0; ss < D; ++ss) {
@@ -643,7 +650,7 @@ static void write_lines(const std::string& path, const std::vector<std::string>&
 static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations, pm_run_stats* st) {
   const Pattern& P = c.pattern;
   const bool files = !out_dir.empty();
-  reset_state(c);
+  reset_state(c, true);  // flushed with superstep 0's fills
   DriverFiles f;
   f.vcount.assign(c.nranks, {});
   f.ecount.assign(c.nranks, {});
@@ -1642,6 +1649,126 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
 }
 
 const char* pm_build_arch(void) { return "gfx950"; }
+
+}  // extern "C"
+
+namespace {
+
+// Decimal text of x at p (no terminator); returns the end.
+inline char* put_u64(char* p, uint64_t x) {
+  char tmp[20];
+  int k = 0;
+  do {
+    tmp[k++] = static_cast<char>('0' + x % 10);
+    x /= 10;
+  } while (x);
+  while (k) *p++ = tmp[--k];
+  return p;
+}
+
+// Lines "a[i] b[i]\n" (b == nullptr: "i a[i]\n") for i in [0, n), formatted by host threads into
+// per-chunk buffers and written in order to f.
+uint64_t write_pairs_text(std::FILE* f, const uint64_t* a, const uint64_t* b, uint64_t n, uint64_t id0) {
+  const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  constexpr uint64_t kChunk = 1ull << 22;  // lines per chunk (<= 42 bytes each)
+  uint64_t total = 0;
+  std::vector<std::vector<char>> buf(T, std::vector<char>(kChunk * 42));
+  std::vector<uint64_t> len(T);
+  for (uint64_t c0 = 0; c0 < n; c0 += kChunk * T) {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const uint64_t b0 = c0 + t * kChunk, e0 = std::min(n, b0 + kChunk);
+        char* p = buf[t].data();
+        for (uint64_t i = b0; i < e0; ++i) {
+          p = put_u64(p, b ? a[i] : id0 + i);
+          *p++ = ' ';
+          p = put_u64(p, b ? b[i] : a[i]);
+          *p++ = '\n';
+        }
+        len[t] = b0 < e0 ? static_cast<uint64_t>(p - buf[t].data()) : 0;
+      });
+    for (auto& x : th) x.join();
+    for (unsigned t = 0; t < T; ++t) {
+      if (len[t] && std::fwrite(buf[t].data(), 1, len[t], f) != len[t]) throw std::runtime_error("text write failed");
+      total += len[t];
+    }
+  }
+  return total;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pm_write_rmat_text(uint64_t scale, uint64_t p_gen, int device, const char* base, uint64_t* bytes_out) {
+  hipStream_t s = nullptr;
+  uint64_t* d_keys = nullptr;
+  try {
+    if (!base || !p_gen || scale == 0 || scale > 32) throw std::runtime_error("pm_write_rmat_text: bad arguments");
+    pm::require_gfx950(device);
+    PM_HIP_CHECK(hipSetDevice(device));
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const pm::RmatPlan plan = pm::rmat_plan(scale, p_gen);
+    PM_HIP_CHECK(hipMalloc(&d_keys, std::max<uint64_t>(2 * plan.per_rank, 1) * sizeof(uint64_t)));
+    std::vector<uint64_t> keys(2 * plan.per_rank), u(plan.per_rank), v(plan.per_rank);
+    const uint64_t mask = (uint64_t(1) << scale) - 1;
+    uint64_t total = 0;
+    for (uint64_t r = 0; r < p_gen; ++r) {
+      pm::rmat_keys_device(plan, {r}, d_keys, s);  // keys 2k = (u << S | v), 2k + 1 = (v << S | u)
+      PM_HIP_CHECK(hipMemcpy(keys.data(), d_keys, keys.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      for (uint64_t k = 0; k < plan.per_rank; ++k) {
+        u[k] = keys[2 * k] >> scale;
+        v[k] = keys[2 * k] & mask;
+      }
+      const std::string path = std::string(base) + "." + std::to_string(r);
+      std::FILE* f = std::fopen(path.c_str(), "wb");
+      if (!f) throw std::runtime_error("cannot write " + path);
+      try {
+        total += write_pairs_text(f, u.data(), v.data(), plan.per_rank, 0);
+      } catch (...) {
+        std::fclose(f);
+        throw;
+      }
+      if (std::fclose(f) != 0) throw std::runtime_error("cannot close " + path);
+    }
+    (void)hipFree(d_keys);
+    (void)hipStreamDestroy(s);
+    if (bytes_out) *bytes_out = total;
+    return 0;
+  } catch (const std::exception& e) {
+    if (d_keys) (void)hipFree(d_keys);
+    if (s) (void)hipStreamDestroy(s);
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pm_write_label_text(const uint64_t* labels, uint64_t n, const char* prefix, uint32_t nfiles, uint64_t* bytes_out) {
+  try {
+    if (!labels || !prefix || !nfiles) throw std::runtime_error("pm_write_label_text: bad arguments");
+    uint64_t total = 0;
+    const uint64_t per = (n + nfiles - 1) / nfiles;
+    for (uint32_t i = 0; i < nfiles; ++i) {
+      const uint64_t b = std::min<uint64_t>(n, uint64_t(i) * per), e = std::min<uint64_t>(n, b + per);
+      const std::string path = std::string(prefix) + "." + std::to_string(i);
+      std::FILE* f = std::fopen(path.c_str(), "wb");
+      if (!f) throw std::runtime_error("cannot write " + path);
+      try {
+        total += write_pairs_text(f, labels + b, nullptr, e - b, b);
+      } catch (...) {
+        std::fclose(f);
+        throw;
+      }
+      if (std::fclose(f) != 0) throw std::runtime_error("cannot close " + path);
+    }
+    if (bytes_out) *bytes_out = total;
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
 
 // Diagnostics: times `reps` launches of the superstep-0 kernel on the current
 // labels (state is reset first).  variant < 65536: diagnostic MODE of the

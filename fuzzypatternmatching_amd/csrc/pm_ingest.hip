@@ -11,8 +11,10 @@
 //   * numbers follow num_get in the "C" locale: white space skipped, optional sign ('-' negates
 //     modulo 2^64, as strtoull), decimal digits, overflow -> ULLONG_MAX and failure.
 //
-// MI355X design: the files are streamed through one pinned staging buffer in
-// pieces of <= 256 MiB that end at a newline; per piece, one thread per
+// MI355X design: the files are streamed through two pinned staging buffers in
+// pieces of <= 256 MiB that end at a newline (a helper thread pages the next
+// piece in, split over several copy threads, while the device parses the
+// current one); per piece, one thread per
 // 32-byte window owns the lines that START in its window (a line start is a
 // byte after '\n'), parses them in place and, after an exclusive scan of the
 // per-window counts (rocPRIM), writes its edges at its own offset: the key
@@ -34,11 +36,14 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <iostream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pm_ingest.hpp"
@@ -111,7 +116,7 @@ class TextPieces {
         if (!nl) throw std::runtime_error("ingest: a text line is longer than the upload piece");
         take = static_cast<uint64_t>(static_cast<const char*>(nl) - s) + 1;
       }
-      std::memcpy(dst, s, take);
+      par_copy(dst, s, take);
       pos_ += take;
       if (dst[take - 1] != '\n') dst[take++] = '\n';
       return take;
@@ -119,6 +124,24 @@ class TextPieces {
   }
 
  private:
+  // page-in + copy of a piece split over kCopyThreads threads (one thread copies a mapped file at a few GB/s)
+  static void par_copy(char* dst, const char* src, uint64_t n) {
+    constexpr unsigned kCopyThreads = 8;
+    constexpr uint64_t kMinChunk = 8ull << 20;
+    const unsigned t = static_cast<unsigned>(std::min<uint64_t>(kCopyThreads, (n + kMinChunk - 1) / kMinChunk));
+    if (t <= 1) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    const uint64_t chunk = (n + t - 1) / t;
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < t; ++i) {
+      const uint64_t b = i * chunk, e = std::min(n, b + chunk);
+      if (b < e) th.emplace_back([=] { std::memcpy(dst + b, src + b, e - b); });
+    }
+    std::memcpy(dst, src, std::min(n, chunk));
+    for (auto& x : th) x.join();
+  }
   bool open(const std::string& path) {
     const int fd = ::open(path.c_str(), O_RDONLY);
     if (fd < 0) {
@@ -148,6 +171,57 @@ class TextPieces {
   size_t fi_ = 0;
   const char* map_ = nullptr;
   uint64_t len_ = 0, pos_ = 0;
+};
+
+// Double-buffered staging: pieces alternate between two pinned buffers; the
+// next piece is filled on a helper thread while the device works on the
+// current one.  A buffer is refilled only after the upload that read it has
+// completed (its event).
+class PieceFeeder {
+ public:
+  PieceFeeder(TextPieces& pieces, uint64_t cap) : pieces_(pieces), cap_(cap), a_(cap), b_(cap) {
+    for (auto& e : ev_) PM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    fill(0);
+  }
+  ~PieceFeeder() {
+    if (worker_.joinable()) worker_.join();
+    for (auto& e : ev_) (void)hipEventDestroy(e);
+  }
+  // the current piece (its length; 0 at the end) and its pinned bytes
+  uint64_t wait() {
+    if (worker_.joinable()) worker_.join();
+    if (err_) std::rethrow_exception(err_);
+    return len_[cur_];
+  }
+  const char* data() const { return cur_ ? b_.p : a_.p; }
+  // enqueues the current piece's upload on s, then starts filling the other buffer with the next piece
+  void upload(void* d_dst, hipStream_t s) {
+    PM_HIP_CHECK(hipMemcpyAsync(d_dst, data(), len_[cur_], hipMemcpyHostToDevice, s));
+    PM_HIP_CHECK(hipEventRecord(ev_[cur_], s));
+    cur_ ^= 1;
+    fill(cur_);
+  }
+
+ private:
+  void fill(int i) {
+    worker_ = std::thread([this, i] {
+      try {
+        PM_HIP_CHECK(hipEventSynchronize(ev_[i]));  // the upload that last read buffer i is done
+        len_[i] = pieces_.next(i ? b_.p : a_.p, cap_);
+      } catch (...) {
+        err_ = std::current_exception();
+        len_[i] = 0;
+      }
+    });
+  }
+  TextPieces& pieces_;
+  uint64_t cap_;
+  PinnedBuf a_, b_;
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  uint64_t len_[2] = {0, 0};
+  int cur_ = 0;
+  std::thread worker_;
+  std::exception_ptr err_;
 };
 
 __device__ __forceinline__ bool is_space(uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
@@ -358,7 +432,7 @@ IngestCsr ingest_edges_device(const std::vector<std::string>& files, bool undire
   TextPieces pieces(files);
   const uint64_t total = pieces.total_bytes();
   const uint64_t piece = piece_bytes();
-  PinnedBuf stage(piece);
+  PinnedBuf tail(64);
   Buf text, cnt, pos, scan_tmp, stat, kf;
   uint8_t* d_text = text.alloc<uint8_t>(piece);
   const uint64_t nw_max = (piece + kWin - 1) / kWin;
@@ -373,12 +447,14 @@ IngestCsr ingest_edges_device(const std::vector<std::string>& files, bool undire
   // forward keys (src << 32 | dst), grown on demand (a line of an edge takes >= 4 bytes)
   uint64_t cap = std::max<uint64_t>(total / 12, 1 << 16), used = 0;
   uint64_t* d_kf = kf.alloc<uint64_t>(cap);
-  uint32_t* h_tail = reinterpret_cast<uint32_t*>(stage.p);  // reused after each piece is on the device
+  uint32_t* h_tail = reinterpret_cast<uint32_t*>(tail.p);
+  PieceFeeder feed(pieces, piece);
   for (;;) {
-    const uint64_t L = pieces.next(stage.p, piece);
+    const uint64_t L = feed.wait();
     if (!L) break;
     out.bytes += L;
-    PM_HIP_CHECK(hipMemcpyAsync(d_text, stage.p, L, hipMemcpyHostToDevice, stream));
+    // (the previous piece's kernels have completed: the stream was synchronised after them)
+    feed.upload(d_text, stream);
     const uint64_t nw = (L + kWin - 1) / kWin;
     hipLaunchKernelGGL(k_count_edges, dim3(grid_for(nw, kThreads, 1u << 30)), dim3(kThreads), 0, stream, d_text, L,
                        nw, d_cnt);
@@ -403,7 +479,7 @@ IngestCsr ingest_edges_device(const std::vector<std::string>& files, bool undire
                        nw, d_pos, d_kf + used, d_stat);
     PM_HIP_CHECK(hipGetLastError());
     used += c;
-    PM_HIP_CHECK(hipStreamSynchronize(stream));  // the staging buffer is refilled next
+    PM_HIP_CHECK(hipStreamSynchronize(stream));  // d_text is overwritten by the next upload
   }
   unsigned long long hs[4];
   PM_HIP_CHECK(hipMemcpy(hs, d_stat, sizeof(hs), hipMemcpyDeviceToHost));
@@ -455,17 +531,17 @@ void labels_from_files_device(const std::vector<std::string>& files, uint64_t n,
                               hipStream_t stream) {
   TextPieces pieces(files);
   const uint64_t piece = piece_bytes();
-  PinnedBuf stage(piece);
   Buf text, win;
   uint8_t* d_text = text.alloc<uint8_t>(piece);
   auto* d_win = win.alloc<unsigned long long>(n);
   PM_HIP_CHECK(hipMemsetAsync(d_win, 0, std::max<uint64_t>(n, 1) * sizeof(unsigned long long), stream));
   PM_HIP_CHECK(hipMemsetAsync(d_labels, 0, std::max<uint64_t>(n, 1) * sizeof(uint64_t), stream));
   uint64_t ord0 = 0;
+  PieceFeeder feed(pieces, piece);
   for (;;) {
-    const uint64_t L = pieces.next(stage.p, piece);
+    const uint64_t L = feed.wait();
     if (!L) break;
-    PM_HIP_CHECK(hipMemcpyAsync(d_text, stage.p, L, hipMemcpyHostToDevice, stream));
+    feed.upload(d_text, stream);
     const uint64_t nw = (L + kWin - 1) / kWin;
     for (int pass = 0; pass < 2; ++pass) {
       hipLaunchKernelGGL(k_label_lines, dim3(grid_for(nw, kThreads, 1u << 30)), dim3(kThreads), 0, stream, d_text,
@@ -473,7 +549,7 @@ void labels_from_files_device(const std::vector<std::string>& files, uint64_t n,
       PM_HIP_CHECK(hipGetLastError());
     }
     ord0 += L;
-    PM_HIP_CHECK(hipStreamSynchronize(stream));  // the staging buffer is refilled next
+    PM_HIP_CHECK(hipStreamSynchronize(stream));  // d_text is overwritten by the next upload
   }
 }
 

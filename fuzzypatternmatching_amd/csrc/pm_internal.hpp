@@ -386,6 +386,16 @@ struct Ctx {
   size_t counts_slots = 0;
 
   Arena arena;
+  // zero fills and the T_pub clear of a search's start, batched into one launch (flush_zero)
+  struct ZeroRange {
+    void* p;
+    uint64_t bytes;
+  };
+  ZeroRange zq[8];
+  int nzq = 0;
+  bool clear_pending = false;
+  bool k1_fills_queued = false;    // queue_lcc_first_fills ran for the next superstep-0 launch      // T_pub at the slist entries, then d_nS (flush_zero)
+  uint32_t* d_zticket = nullptr;   // last-block ticket of k_zero_batch (zero between launches)
   std::vector<hipEvent_t> events;  // LCC call timing, created once
   uint32_t nS_host = 0;     // size of d_slist (host copy, valid after superstep 0)
   bool lcc_started = false; // superstep 0 of the first call done
@@ -460,6 +470,12 @@ void launch_compact_slist(Ctx& c);  // keeps the live entries of the last supers
 // Zero T_pub (both buffers) at the slist entries of the last search (every
 // nonzero T_pub entry is one of them, plus the other shards' when sharded).
 void launch_clear_tpub(Ctx& c);
+// Deferred zero fill of `bytes` (a multiple of 4, 4-aligned) at p: the queued fills, and a pending T_pub clear
+// (clear_pending: T_pub at the slist entries, then d_nS = 0), go out as ONE launch in flush_zero -- each
+// hipMemsetAsync is a dispatch of its own, several microseconds apart on the stream.
+void zero_later(Ctx& c, void* p, uint64_t bytes);
+void queue_lcc_first_fills(Ctx& c);
+void flush_zero(Ctx& c);
 size_t slist_scan_tmp_bytes(uint64_t words);
 static constexpr unsigned kPartGridMax = 2048;
 

@@ -1886,8 +1886,18 @@ __global__ void k_slist_heavy(const uint4* __restrict__ hrec, uint32_t nheavy, c
   }
 }
 
+// heavy-row scratch, heavy records and the 2-bit codes of a superstep-0 launch (queued with the search's reset)
+void queue_lcc_first_fills(Ctx& c) {
+  if (c.ntiles == 0) return;
+  if (c.nheavy) zero_later(c, c.d_hscr, 3 * size_t(c.nheavy) * sizeof(uint32_t));
+  if (c.nheavy && c.d_hrec) zero_later(c, c.d_hrec, size_t(c.nheavy) * sizeof(uint4));
+  zero_later(c, c.d_tcode, ((c.n + 15) / 16 + 1) * sizeof(uint32_t));
+  c.k1_fills_queued = true;
+}
+
 void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) {
   if (c.ntiles == 0) {
+    flush_zero(c);
     if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
     if (ev1) PM_HIP_CHECK(hipEventRecord(ev1, c.stream));
     PM_HIP_CHECK(hipMemsetAsync(d_slot, 0, slot_words(c) * sizeof(uint64_t), c.stream));
@@ -1896,8 +1906,9 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
     return;
   }
   const unsigned grid = c.k1_grid;
-  lcc_first_prepare(c);
-  PM_HIP_CHECK(hipMemsetAsync(c.d_tcode, 0, ((c.n + 15) / 16 + 1) * sizeof(uint32_t), c.stream));
+  if (!c.k1_fills_queued) queue_lcc_first_fills(c);
+  flush_zero(c);
+  c.k1_fills_queued = false;
   lcc_first_set_dense(c);
   c.slist_compacted = false;
   if (ev0) PM_HIP_CHECK(hipEventRecord(ev0, c.stream));
@@ -2062,6 +2073,87 @@ void launch_compact_slist(Ctx& c) {
   std::swap(c.d_nS, c.d_nS2);
   c.smask_valid = false;  // every entry of the new list is live
   c.slist_compacted = true;
+}
+
+// Batched zero fills (16-B stores in the aligned middle of each range) and the T_pub clear at the slist
+// entries; the block that finishes last zeroes *np (read by every block's clear) and re-arms the ticket.
+struct ZeroBatch {
+  uint32_t* p[8];
+  uint64_t words[8];
+  int n;
+  const uint32_t* list;
+  uint32_t* np;
+  uint64_t cap;
+  uint16_t* t0;
+  uint16_t* t1;
+  uint32_t* ticket;
+};
+
+__global__ __launch_bounds__(kBlock) void k_zero_batch(ZeroBatch b) {
+  const uint64_t tid = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  const uint64_t nt = uint64_t(gridDim.x) * blockDim.x;
+  for (int r = 0; r < b.n; ++r) {
+    uint32_t* p = b.p[r];
+    const uint64_t w = b.words[r];
+    const uint64_t head = min<uint64_t>(w, ((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4);
+    const uint64_t nv = (w - head) / 4;
+    if (tid < head) p[tid] = 0u;
+    uint4* v = reinterpret_cast<uint4*>(p + head);
+    for (uint64_t i = tid; i < nv; i += nt) v[i] = make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t tail = head + nv * 4;
+    if (tail + tid < w) p[tail + tid] = 0u;
+  }
+  if (!b.list) return;
+  const uint64_t n = min(static_cast<uint64_t>(*b.np), b.cap);
+  for (uint64_t i = tid; i < n; i += nt) {
+    const uint32_t q = b.list[i];
+    b.t0[q] = 0;
+    b.t1[q] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(b.ticket, 1u) == gridDim.x - 1) {
+      *b.np = 0u;
+      *b.ticket = 0u;
+    }
+  }
+}
+
+void zero_later(Ctx& c, void* p, uint64_t bytes) {
+  if (!bytes) return;
+  if ((bytes & 3) || (reinterpret_cast<uintptr_t>(p) & 3)) throw std::runtime_error("internal: unaligned zero fill");
+  if (c.nzq == 8) flush_zero(c);
+  c.zq[c.nzq++] = Ctx::ZeroRange{p, bytes};
+}
+
+void flush_zero(Ctx& c) {
+  if (!c.nzq && !c.clear_pending) return;
+  ZeroBatch b{};
+  uint64_t most = 0;
+  for (int r = 0; r < c.nzq; ++r) {
+    b.p[r] = static_cast<uint32_t*>(c.zq[r].p);
+    b.words[r] = c.zq[r].bytes / 4;
+    most = std::max(most, b.words[r] / 4);
+  }
+  b.n = c.nzq;
+  if (c.clear_pending) {
+    if (!c.d_zticket) {
+      PM_HIP_CHECK(hipMalloc(&c.d_zticket, sizeof(uint32_t)));
+      PM_HIP_CHECK(hipMemsetAsync(c.d_zticket, 0, sizeof(uint32_t), c.stream));
+    }
+    b.list = c.d_slist;
+    b.np = c.d_nS;
+    b.cap = c.nS_host;
+    b.t0 = c.d_tpub[0];
+    b.t1 = c.d_tpub[1];
+    b.ticket = c.d_zticket;
+    most = std::max<uint64_t>(most, c.nS_host);
+  }
+  hipLaunchKernelGGL(k_zero_batch, dim3(grid_for(most, kBlock, 2048)), dim3(kBlock), 0, c.stream, b);
+  PM_HIP_CHECK(hipGetLastError());
+  c.nzq = 0;
+  c.clear_pending = false;
 }
 
 __global__ void k_clear_tpub(const uint32_t* __restrict__ list, const uint32_t* __restrict__ np, uint64_t cap,

@@ -786,7 +786,7 @@ static void ensure_hash(Ctx& c, uint64_t want) {
 }
 
 void free_line_buffers(Ctx& c) {
-  void* ptrs[] = {c.d_lstats, c.d_hkey, c.d_hval, c.d_front, c.d_gbar, c.d_ldesc};
+  void* ptrs[] = {c.d_hkey, c.d_hval, c.d_front, c.d_gbar, c.d_ldesc};  // (d_lstats lives in d_gbar)
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   c.d_lstats = nullptr;
@@ -831,10 +831,15 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     if (stride > 18) throw std::runtime_error("NLC line longer than 16 positions");
   }
   upload_lines(c);
+  // one buffer: grid barrier state | 64 control words (lines done, kept-walk counter, ...) | LineStats per
+  // line -- the control words and the stats are cleared by one fill and read back by one copy
+  static_assert(((kGbarWords + 64) * sizeof(unsigned)) % alignof(LineStats) == 0, "LineStats alignment");
+  static_assert(sizeof(LineStats) % sizeof(unsigned) == 0, "LineStats size");
   if (!c.d_lstats) {
-    c.d_lstats = dmalloc<LineStats>(std::max<size_t>(nl_all, 1));
-    c.d_gbar = dmalloc<unsigned>(kGbarWords + 64);
-    PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, (kGbarWords + 64) * sizeof(unsigned), c.stream));
+    const size_t words = kGbarWords + 64 + std::max<size_t>(nl_all, 1) * (sizeof(LineStats) / sizeof(unsigned));
+    c.d_gbar = dmalloc<unsigned>(words);
+    PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, words * sizeof(unsigned), c.stream));
+    c.d_lstats = reinterpret_cast<LineStats*>(c.d_gbar + kGbarWords + 64);
   }
   if (!c.line_grid) {
     int per_cu = 0;
@@ -849,8 +854,8 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   ensure_hash(c, std::max<uint64_t>(1ull << 16, 4 * c.ss0_rows));
   unsigned* d_done = c.d_gbar + kGbarWords;                                   // [0] lines done
   auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
-  PM_HIP_CHECK(hipMemsetAsync(c.d_lstats + pl0, 0, (nl - pl0) * sizeof(LineStats), c.stream));
-  PM_HIP_CHECK(hipMemsetAsync(d_done, 0, 64 * sizeof(unsigned), c.stream));
+  const size_t ctl_bytes = 64 * sizeof(unsigned) + nl * sizeof(LineStats);  // control words + stats of lines < nl
+  PM_HIP_CHECK(hipMemsetAsync(d_done, 0, ctl_bytes, c.stream));
   LineKernelArgs a{};
   a.offp = m_off(c);
   a.mcol = m_col(c);
@@ -903,10 +908,9 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args,
                                             0, c.stream));
   c.probe("lines launched");
-  // read-back through pinned memory: [done | kept slots | line stats]
+  // read-back through pinned memory, one copy: [done | . | kept slots | ... (64 words) | line stats]
   static_assert(sizeof(LineStats) % 8 == 0, "LineStats is read back as u64 words");
-  const size_t sw = sizeof(LineStats) / 8;
-  const size_t words = 2 + (nl - pl0) * sw;
+  const size_t words = ctl_bytes / 8;
   if (c.h_pin_lines_words < words) {
     if (c.h_pin_lines) (void)hipHostFree(c.h_pin_lines);
     c.h_pin_lines = nullptr;
@@ -915,10 +919,7 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     c.h_pin_lines_words = w;
   }
   uint64_t* pin = c.h_pin_lines;
-  PM_HIP_CHECK(hipMemcpyAsync(pin, d_done, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipMemcpyAsync(pin + 1, d_kept_ctr, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipMemcpyAsync(pin + 2, c.d_lstats + pl0, (nl - pl0) * sizeof(LineStats), hipMemcpyDeviceToHost,
-                              c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(pin, d_done, ctl_bytes, hipMemcpyDeviceToHost, c.stream));
   kept_out = a.kept;
   return nl;
 }
@@ -948,7 +949,8 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("lines synced");
   std::vector<LineStats> hs(nl - pl0);
-  std::memcpy(hs.data(), pin + 2, hs.size() * sizeof(LineStats));
+  std::memcpy(hs.data(), reinterpret_cast<const char*>(pin) + 64 * sizeof(unsigned) + pl0 * sizeof(LineStats),
+              hs.size() * sizeof(LineStats));
   const unsigned done = static_cast<unsigned>(pin[0] & 0xFFFFFFFFull);
   const unsigned long long kept_slots = pin[1];
   std::vector<uint32_t> kept;

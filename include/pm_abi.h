@@ -223,6 +223,13 @@ int pm_write_graph(const char* base, uint64_t n, const uint64_t* off, const uint
 int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n, int* symmetric,
                   uint32_t* nranks, uint64_t* hub_threshold);
 
+/* Test-input writers (config C5 at size: a text edge list and -v label files too large for Python).
+ * pm_write_rmat_text: the undirected R-MAT edge stream of every generator rank r < p_gen, generated on
+ * `device` and written as "u v" lines to <base>.<r> (formatted on host threads); bytes_out: text bytes.
+ * pm_write_label_text: "v labels[v]" lines for v < n, split into nfiles files <prefix>.<i>. */
+int pm_write_rmat_text(uint64_t scale, uint64_t p_gen, int device, const char* base, uint64_t* bytes_out);
+int pm_write_label_text(const uint64_t* labels, uint64_t n, const char* prefix, uint32_t nfiles, uint64_t* bytes_out);
+
 /* Parsed pattern directory as JSON text (host only; loader check). */
 int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen);
 
