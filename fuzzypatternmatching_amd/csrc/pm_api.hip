@@ -692,8 +692,10 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     c.live_hint = 0;
     for (auto x : loc_vc) c.live_hint += x;
     for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
-      f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
-      add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
+      if (files) {  // (result-file lines are built only when they are written)
+        f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
+        add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
+      }
       if (phase_times) {
         uint64_t sv = 0, se = 0;
         for (auto x : lo.vcount[ss]) sv += x;
@@ -732,7 +734,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     }
     record_lcc(lo, itr);
     nf = nf || lo.not_finished;
-    f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lp)));
+    if (files) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lp)));
     init_step = false;
     if (itr == 0) nf = true;  // forced token passing (beta.cpp:686-688)
     if (nf) {
@@ -809,8 +811,10 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           s.nlcc_edges += tr.edges;
         }
         if (deleted) nf = true;
-        f.superstep.push_back(std::to_string(itr) + ", TP, " + std::to_string(pl) + ", " + fmt_double(since(t_tp)));
-        add_count_lines(c, f, itr, "TP", pl, vc, ec, tr.edges);
+        if (files) {
+          f.superstep.push_back(std::to_string(itr) + ", TP, " + std::to_string(pl) + ", " + fmt_double(since(t_tp)));
+          add_count_lines(c, f, itr, "TP", pl, vc, ec, tr.edges);
+        }
         totals(vc, ec);
         cur_vc = vc;
         cur_ec = ec;
@@ -819,13 +823,13 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           LccOut li = lcc_call(c, false);
           record_lcc(li, itr);
           nf = nf || li.not_finished;
-          f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lpi)));
+          if (files) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lpi)));
         }
       }
     } else {
       nf = false;
     }
-    f.iteration.push_back(std::to_string(itr) + ", " + fmt_double(since(t_itr)));
+    if (files) f.iteration.push_back(std::to_string(itr) + ", " + fmt_double(since(t_itr)));
     ++itr;
   } while (nf);
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
@@ -1795,7 +1799,7 @@ int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
     float total = 0.f;
     for (int i = 0; i < reps; ++i) {
       pm::lcc_first_prepare(*ctx);
-      PM_HIP_CHECK(hipMemsetAsync(ctx->d_tcode, 0, ((ctx->n + 15) / 16 + 1) * sizeof(uint32_t), ctx->stream));
+      PM_HIP_CHECK(hipMemsetAsync(ctx->d_tcode, 0, pm::tcode_words(ctx->lr) * sizeof(uint32_t), ctx->stream));
       if (dense) pm::lcc_first_set_dense(*ctx);
       PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
       pm::launch_lcc_first_kernel(*ctx, mode, grid, ctx->d_counts);

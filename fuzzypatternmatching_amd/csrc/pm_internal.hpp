@@ -40,8 +40,10 @@ struct OwnerArgs {
 // a vertex at position p carries template bits tu[l] iff lo[l] <= p < hi[l].
 struct LabelRuns {
   uint32_t lo[16], len[16];
+  uint32_t cd[16];  // code index of position p in run l: p + cd[l] (the runs packed one after the other)
   uint16_t tu[16];
   int32_t n;
+  uint32_t ncode;   // positions in the runs (code indices 0 .. ncode-1)
 };
 
 // NLC line constants for the token-passing kernels.
@@ -121,6 +123,7 @@ struct KRange {
   uint16_t kbit[4];
   uint32_t kneed[4];
   uint32_t nkeep;
+  uint32_t cdelta;  // code index of a row of the range: position + cdelta (LabelRuns::cd of its label)
 };
 struct HSeg {
   uint32_t row;    // row position
@@ -191,6 +194,17 @@ __host__ __device__ inline uint32_t tpub_code(uint32_t T, uint32_t tu) {
   if (rest & (rest - 1)) return T ? 3u : 0u;
   return ((T & tu & (0u - tu)) ? 1u : 0u) | ((T & rest) ? 2u : 0u);
 }
+
+// The 2-bit T_pub codes are indexed by position inside the pattern's label runs (the runs packed one after
+// the other): only such positions are ever coded (members of S) or gathered (M entries), and at S=28 the
+// array is 22 MB instead of 64 MB for the first later superstep's 31 M random gathers.
+__host__ __device__ inline uint32_t code_index(uint32_t p, const LabelRuns& lr) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (int l = 0; l < lr.n; ++l)
+    if (p - lr.lo[l] < lr.len[l]) c = p + lr.cd[l];
+  return c;
+}
+__host__ __device__ inline uint64_t tcode_words(const LabelRuns& lr) { return (uint64_t(lr.ncode) + 15) / 16 + 1; }
 
 // Padded row length: the class length up to kLightMax, the degree above.
 __host__ __device__ inline uint64_t padded_degree(uint64_t d) {

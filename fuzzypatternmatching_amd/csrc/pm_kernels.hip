@@ -251,9 +251,10 @@ __device__ __forceinline__ uint16_t keep_fast(uint16_t tu, uint16_t TN, const Ke
 }
 
 // Verify of the row at position u by the calling lane; returns survivor.
-__device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t TN, uint32_t len, uint32_t cnt,
-                                              const uint16_t* adj, const KeepArgs& ka, const OwnerArgs& oa,
-                                              const K1Out& o, BlockAcc& acc, unsigned long long* s_hist) {
+__device__ __forceinline__ bool k1_finish_row(uint32_t u, uint32_t cdelta, uint16_t tu, uint16_t TN, uint32_t len,
+                                              uint32_t cnt, const uint16_t* adj, const KeepArgs& ka,
+                                              const OwnerArgs& oa, const K1Out& o, BlockAcc& acc,
+                                              unsigned long long* s_hist) {
   if (!TN) return false;
   const uint16_t T = keep_fast(tu, TN, ka, adj);
   if (!T) {
@@ -265,7 +266,8 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint16_t tu, uint16_t 
   *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.mlen) + b4) = len;
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.malive) + b4) = cnt;
-  atomicOr(&o.tcode[u >> 4], tpub_code(T, tu) << ((u & 15u) << 1));
+  const uint32_t ci = u + cdelta;
+  atomicOr(&o.tcode[ci >> 4], tpub_code(T, tu) << ((ci & 15u) << 1));
   // dense mode: T_pub in the record (a heavy row's M stays in its padded row: no first entry); a
   // label of more than two template vertices also keeps its position-indexed T_pub (code 3 gathers)
   if (!o.rarea || tpub_code(T, tu) == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
@@ -617,7 +619,10 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
       if (!(MODE & 128)) {
         // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
         const uint32_t u = ustart + row, b2 = u * 2u, b4 = u * 4u;
-        if (!(MODE & 512)) atomicOr(&o.tcode[u >> 4], code << ((u & 15u) << 1));
+        if (!(MODE & 512)) {
+          const uint32_t ci = u + R->cdelta;
+          atomicOr(&o.tcode[ci >> 4], code << ((ci & 15u) << 1));
+        }
         if (o.rarea) {
           if (!dense) {
             *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
@@ -730,7 +735,7 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
       __threadfence();
       const uint16_t TNall = static_cast<uint16_t>(atomicOr(&h_tn[hs.h], 0u));
       const uint32_t call = atomicAdd(&h_cnt[hs.h], 0u);
-      surv = k1_finish_row(hs.row, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
+      surv = k1_finish_row(hs.row, R->cdelta, tu, TNall, deg, call, s_adj, keep, oa, o, acc, s_hist);
       // dense mode: the heavy row's record (its M in the padded row); hrec was zeroed before the launch
       if (surv && o.hrec) o.hrec[hs.h] = make_uint4(hs.row, 0u, kNone, 1u);
     }
@@ -933,7 +938,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   __shared__ uint64_t s_beg[kWpb][kWave];  // flattened short rows (per wave)
   __shared__ uint32_t s_end[kWpb][kWave], s_tn[kWpb][kWave], s_cnt[kWpb][kWave];
   __shared__ uint16_t s_nm[kWpb][kWave];
-  __shared__ uint32_t s_rlo[16], s_rlen[16], s_rtu[16];
+  __shared__ uint32_t s_rlo[16], s_rlen[16], s_rtu[16], s_rcd[16];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   load_adj(s_adj, pa);
   if (threadIdx.x < 16) {
@@ -941,6 +946,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     s_rlo[l] = lr.lo[l];
     s_rlen[l] = l < lr.n ? lr.len[l] : 0u;
     s_rtu[l] = lr.tu[l];
+    s_rcd[l] = lr.cd[l];
   }
   __syncthreads();
   const int nruns = lr.n;
@@ -948,11 +954,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   // label's template bits from its run), the T_pub array otherwise
   auto tpub_of = [&](uint32_t p) -> uint16_t {
     if (!tcode) return tcur[p];
-    const uint32_t code = (tcode[p >> 4] >> ((p & 15u) << 1)) & 3u;
-    if (!code) return 0;
-    uint32_t tu = 0;
+    // the label's template bits and the code index from its run (an M entry lies in a template label's run)
+    uint32_t tu = 0, ci = 0;
     for (int l = 0; l < nruns; ++l)
-      if (p - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
+      if (p - s_rlo[l] < s_rlen[l]) {
+        tu = s_rtu[l];
+        ci = p + s_rcd[l];
+      }
+    const uint32_t code = (tcode[ci >> 4] >> ((ci & 15u) << 1)) & 3u;
+    if (!code) return 0;
     const uint32_t rest = tu & (tu - 1);
     if (rest & (rest - 1)) return tcur[p];
     return static_cast<uint16_t>(((code & 1u) ? (tu & (0u - tu)) : 0u) | ((code & 2u) ? rest : 0u));
@@ -1514,11 +1524,15 @@ void build_tiling(Ctx& c) {
   };
   c.lr = LabelRuns{};
   c.lr.n = nl;
+  uint32_t cb = 0;
   for (int l = 0; l < nl; ++l) {
     c.lr.lo[l] = static_cast<uint32_t>(bounds[l * kLB + 0]);
     c.lr.len[l] = static_cast<uint32_t>(bounds[l * kLB + kLB - 1] - bounds[l * kLB + 0]);
     c.lr.tu[l] = tus[l];
+    c.lr.cd[l] = cb - c.lr.lo[l];  // (mod 2^32)
+    cb += c.lr.len[l];
   }
+  c.lr.ncode = cb;
   std::vector<KRange> tab;
   std::vector<HSeg> hs;
   std::vector<uint64_t> ttab;  // tile descriptors (kTtabRemShift / kTtabRangeShift)
@@ -1581,6 +1595,7 @@ void build_tiling(Ctx& c) {
       R.end = static_cast<uint32_t>(b);
       R.tu = tu;
       R.nm = nm;
+      R.cdelta = c.lr.cd[l];
       R.kind = static_cast<uint32_t>(kind);
       if (kind < kHeavyKind) {
         R.g = kind_slots(static_cast<uint32_t>(kind));
@@ -1891,7 +1906,7 @@ void queue_lcc_first_fills(Ctx& c) {
   if (c.ntiles == 0) return;
   if (c.nheavy) zero_later(c, c.d_hscr, 3 * size_t(c.nheavy) * sizeof(uint32_t));
   if (c.nheavy && c.d_hrec) zero_later(c, c.d_hrec, size_t(c.nheavy) * sizeof(uint4));
-  zero_later(c, c.d_tcode, ((c.n + 15) / 16 + 1) * sizeof(uint32_t));
+  zero_later(c, c.d_tcode, tcode_words(c.lr) * sizeof(uint32_t));
   c.k1_fills_queued = true;
 }
 

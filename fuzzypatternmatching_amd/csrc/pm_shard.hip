@@ -278,12 +278,13 @@ __global__ void k_count_to_u64(const uint32_t* __restrict__ n, uint64_t* __restr
 // (its code 3 means "gather T_pub"), position | T_pub << 32 | code << 62.
 __global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
                              const uint32_t* __restrict__ tcode, const uint16_t* __restrict__ tpub,
-                             const uint4* __restrict__ srec, int wide, uint32_t* __restrict__ out32,
+                             const uint4* __restrict__ srec, int wide, LabelRuns lr, uint32_t* __restrict__ out32,
                              unsigned long long* __restrict__ out64) {
   const uint64_t n = *nSp;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t p = slist[i];
-    const uint32_t code = (tcode[p >> 4] >> ((p & 15u) << 1)) & 3u;
+    const uint32_t ci = code_index(p, lr);  // (a member of S: in its label's run)
+    const uint32_t code = (tcode[ci >> 4] >> ((ci & 15u) << 1)) & 3u;
     const uint16_t T = srec ? static_cast<uint16_t>(srec[i].y) : tpub[p];  // superstep-0 records: T_pub there
     if (wide) out64[i] = p | (static_cast<unsigned long long>(T) << 32) | (static_cast<unsigned long long>(code) << 62);
     else out32[i] = p | (code << 30);
@@ -292,8 +293,8 @@ __global__ void k_pack_codes(const uint32_t* __restrict__ slist, const uint32_t*
 
 // The other shards' code records into this shard's 2-bit codes (and T_pub).
 __global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned long long* __restrict__ in64,
-                               uint64_t maxS, uint32_t G, uint32_t me, XCounts x, uint32_t* __restrict__ tcode,
-                               uint16_t* __restrict__ tpub) {
+                               uint64_t maxS, uint32_t G, uint32_t me, XCounts x, LabelRuns lr,
+                               uint32_t* __restrict__ tcode, uint16_t* __restrict__ tpub) {
   const uint64_t total = uint64_t(G) * maxS;
   for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t g = static_cast<uint32_t>(j / maxS);
@@ -308,7 +309,8 @@ __global__ void k_unpack_codes(const uint32_t* __restrict__ in32, const unsigned
       p = in32[j] & 0x3FFFFFFFu;
       code = in32[j] >> 30;
     }
-    atomicOr(&tcode[p >> 4], code << ((p & 15u) << 1));
+    const uint32_t ci = code_index(p, lr);
+    atomicOr(&tcode[ci >> 4], code << ((ci & 15u) << 1));
   }
 }
 
@@ -504,7 +506,8 @@ __global__ void k_hub_finish(HubFinishArgs a) {
         a.tpub[p] = T;
         a.mlen[p] = static_cast<uint32_t>(cnt);
         a.malive[p] = static_cast<uint32_t>(cnt);
-        atomicOr(&a.tcode[p >> 4], tpub_code(T, tu) << ((p & 15u) << 1));
+        const uint32_t ci = code_index(p, a.lr);
+        atomicOr(&a.tcode[ci >> 4], tpub_code(T, tu) << ((ci & 15u) << 1));
         const uint32_t at = atomicAdd(a.nS, 1u);
         a.slist[at] = p;
         if (a.srec) a.srec[at] = make_uint4(p, T, kNone, 0u);  // its M in the hub area (m_off), not dense
@@ -656,7 +659,7 @@ void shard_codes_after_first(Ctx& c) {
   auto* send = grow<char>(c.d_xsend, c.xsend_cap, maxS * rb);
   auto* recv = grow<char>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxS * rb);
   hipLaunchKernelGGL(k_pack_codes, dim3(xgrid(c.nS_host)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tcode,
-                     c.d_tpub[c.cur], c.k1_records ? c.d_srec : nullptr, c.xcode_wide ? 1 : 0,
+                     c.d_tpub[c.cur], c.k1_records ? c.d_srec : nullptr, c.xcode_wide ? 1 : 0, c.lr,
                      reinterpret_cast<uint32_t*>(send), reinterpret_cast<unsigned long long*>(send));
   c.comm->allgather(send, recv, maxS * rb, c.stream);
   XCounts x{};
@@ -664,7 +667,7 @@ void shard_codes_after_first(Ctx& c) {
   hipLaunchKernelGGL(k_unpack_codes, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream,
                      c.xcode_wide ? nullptr : reinterpret_cast<const uint32_t*>(recv),
                      c.xcode_wide ? reinterpret_cast<const unsigned long long*>(recv) : nullptr, maxS, G, c.shard, x,
-                     c.d_tcode, c.d_tpub[c.cur]);
+                     c.lr, c.d_tcode, c.d_tpub[c.cur]);
   c.xcode_in_tpub = c.xcode_wide;
   PM_HIP_CHECK(hipGetLastError());
 }

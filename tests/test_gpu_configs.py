@@ -1,14 +1,17 @@
-"""GPU parity at the BASELINE.json configurations (SURVEY.md 8(d) C2, C3, C5;
-C4 on one GPU behind PM_BIG=1): every result file of the HIP path compared with
-the oracle (run on all host threads) on the same R-MAT input.
+"""GPU parity at the BASELINE.json configurations (SURVEY.md 8(d) C2, C3, C4 on
+one GPU, C5): every result file of the HIP path compared with the oracle (run on
+all host threads) on the same R-MAT input, or with the oracle's committed S=28
+result digest.
 
 C2: S=24, P_gen=4, tree, degree labels, 1 and 4 ranks of output attribution.
 C3: S=26, P_gen=4, 4-cycle pattern (NLCC token-passing stress).
 C5: ingested text edge list (-u 1) + explicit -v label files (hash32(v) % 64)
     through the CLIs at S=18 (text size), and hash labels through the library at
     S=22.
-C4': S=28, P_gen=8, tree on ONE GPU (PM_BIG=1: ~100 GB of host memory for the
-    oracle; the 8-GPU sharding of C4 is covered by tests/test_gpu_shards.py).
+C4': S=28, P_gen=8, tree on ONE GPU against tests/golden/rmat_s28_p8_tree.json
+    (the oracle needs ~100 GB of host memory there, so its result was made once:
+    tests/golden/make_rmat_fixture.py); the sharding of C4 is covered by
+    tests/test_gpu_shards.py.  C5 at S=27: tools/c5_at_size.py.
 """
 import os
 import subprocess

@@ -1,7 +1,11 @@
 """BASELINE config C5 at size on one GPU: an R-MAT text edge list of scale S (default 27, P_gen = 8 files,
 written from the GPU generator's stream), ingested on the GPU with -u 1 (ingest_edge_list.cpp:164-240,
-parallel_edge_list_reader.hpp:242-266), explicit -v label files (hash32(v ^ 5) % 64, vertex_data_db.hpp:137-257)
-parsed on the GPU, and the 4-cycle pattern searched with result files.  Checks:
+parallel_edge_list_reader.hpp:242-266), explicit -v label files (vertex_data_db.hpp:137-257) parsed on the GPU,
+and the pattern searched with result files.  Labels: --labels degree (default) writes the degree-log2 labels of
+the symmetrized graph as -v files; --labels hash writes hash32(v ^ 5) % alphabet.  (The hash-labelled 4-cycle's
+template-driven enumeration grows faster than the graph on R-MAT hubs -- 17 k walks at S=22 with alphabet 256,
+200 k with 128 -- and at S=27 exceeds both the oracle's host memory and the device walk arena, so the at-size
+run takes the tree pattern over explicit degree labels.)  Checks:
   * the ingested context's result directory equals the GPU-generated graph's (same labels) -- the text path
     builds the same graph;
   * with --oracle, both equal the oracle's result on the host CSR (16 threads; ~60 GB of host memory at S=27).
@@ -41,8 +45,9 @@ def main():
     ap.add_argument("--scale", type=int, default=27)
     ap.add_argument("--p-gen", type=int, default=8)
     ap.add_argument("--dir", default=None, help="text files (default: /dev/shm when it has room, else TMPDIR)")
-    ap.add_argument("--pattern", default="rmat_log2_cycle4_pattern")
-    ap.add_argument("--alphabet", type=int, default=64)
+    ap.add_argument("--pattern", default="rmat_log2_tree_pattern")
+    ap.add_argument("--labels", choices=["degree", "hash"], default="degree")
+    ap.add_argument("--alphabet", type=int, default=256)
     ap.add_argument("--nranks", type=int, default=8, help="output ranks of the result files")
     ap.add_argument("--oracle", action="store_true")
     ap.add_argument("--out", default=None)
@@ -57,8 +62,22 @@ def main():
         base_dir = "/dev/shm" if shm > 1.5 * need else tempfile.gettempdir()
     work = tempfile.mkdtemp(prefix="c5_", dir=base_dir)
     res = {"config": "C5 at size", "scale": args.scale, "p_gen": args.p_gen, "pattern": args.pattern,
-           "labels": f"hash32(v ^ 5) % {args.alphabet}, -v files", "text_dir": base_dir}
+           "labels": ("degree-log2 labels of the symmetrized graph" if args.labels == "degree" else
+                      f"hash32(v ^ 5) % {args.alphabet}") + ", as -v files", "text_dir": base_dir}
+    g = None
     try:
+        # 0. the graph's host CSR (the oracle's input; degree labels)
+        if args.labels == "degree" or args.oracle:
+            g = pm.rmat_graph(args.scale, args.p_gen, device=0)
+            log(f"host CSR: V={g.n} E={g.nnz}")
+        if args.labels == "degree":
+            deg = np.diff(g.off)
+            labels = np.zeros(n, np.uint64)
+            nz = deg > 0
+            labels[nz] = (np.floor(np.log2(deg[nz].astype(np.float64))) + 1).astype(np.uint64)  # bit_width
+            del deg, nz
+        else:
+            labels = pmtest.hash_labels(n, args.alphabet, salt=5)
         # 1. inputs
         t = time.time()
         nb = ctypes.c_uint64()
@@ -67,7 +86,6 @@ def main():
         files = [os.path.join(work, f"edges.{r}") for r in range(args.p_gen)]
         res["edge_text_bytes"] = nb.value
         log(f"edge text: {nb.value / 1e9:.2f} GB in {args.p_gen} files ({time.time() - t:.1f}s)")
-        labels = pmtest.hash_labels(n, args.alphabet, salt=5)
         lb = ctypes.c_uint64()
         if lib.pm_write_label_text(labels.ctypes.data, n, os.path.join(work, "lab").encode(), 4, ctypes.byref(lb)):
             raise pm._err()
@@ -115,8 +133,7 @@ def main():
         # 4. the oracle on the host CSR (full size)
         if args.oracle:
             import oracle
-            g = pm.rmat_graph(args.scale, args.p_gen, device=0)
-            log("host CSR ready; oracle ...")
+            log("oracle ...")
             t = time.time()
             out_o = os.path.join(work, "res_oracle")
             so = oracle.run(g.off, g.col, pattern, out_o, labels=labels, nranks=args.nranks, threads=16)
