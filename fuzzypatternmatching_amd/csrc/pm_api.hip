@@ -650,6 +650,8 @@ static void write_lines(const std::string& path, const std::vector<std::string>&
 static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations, pm_run_stats* st) {
   const Pattern& P = c.pattern;
   const bool files = !out_dir.empty();
+  static const bool build_lines_anyway = std::getenv("PM_BUILD_LINES") != nullptr;  // diagnostics (A/B)
+  const bool lines_on = files || build_lines_anyway;
   reset_state(c, true);  // flushed with superstep 0's fills
   DriverFiles f;
   f.vcount.assign(c.nranks, {});
@@ -692,7 +694,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     c.live_hint = 0;
     for (auto x : loc_vc) c.live_hint += x;
     for (size_t ss = 0; ss < lo.seconds.size(); ++ss) {
-      if (files) {  // (result-file lines are built only when they are written)
+      if (lines_on) {  // (result-file lines are built only when they are written)
         f.superstep.push_back(std::to_string(itr_) + ", LP, " + std::to_string(ss) + ", " + fmt_double(lo.seconds[ss]));
         add_count_lines(c, f, itr_, "LP", ss, lo.vcount[ss], lo.ecount[ss], lo.trav[ss]);
       }
@@ -734,7 +736,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     }
     record_lcc(lo, itr);
     nf = nf || lo.not_finished;
-    if (files) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lp)));
+    if (lines_on) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lp)));
     init_step = false;
     if (itr == 0) nf = true;  // forced token passing (beta.cpp:686-688)
     if (nf) {
@@ -811,7 +813,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           s.nlcc_edges += tr.edges;
         }
         if (deleted) nf = true;
-        if (files) {
+        if (lines_on) {
           f.superstep.push_back(std::to_string(itr) + ", TP, " + std::to_string(pl) + ", " + fmt_double(since(t_tp)));
           add_count_lines(c, f, itr, "TP", pl, vc, ec, tr.edges);
         }
@@ -823,13 +825,13 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           LccOut li = lcc_call(c, false);
           record_lcc(li, itr);
           nf = nf || li.not_finished;
-          if (files) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lpi)));
+          if (lines_on) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lpi)));
         }
       }
     } else {
       nf = false;
     }
-    if (files) f.iteration.push_back(std::to_string(itr) + ", " + fmt_double(since(t_itr)));
+    if (lines_on) f.iteration.push_back(std::to_string(itr) + ", " + fmt_double(since(t_itr)));
     ++itr;
   } while (nf);
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));

@@ -125,6 +125,7 @@ struct KRange {
   uint32_t nkeep;
   uint32_t cdelta;  // code index of a row of the range: position + cdelta (LabelRuns::cd of its label)
 };
+static_assert(sizeof(KRange) == 416, "KRange: cdelta fills the tail padding (scalar-load layout unchanged)");
 struct HSeg {
   uint32_t row;    // row position
   uint32_t seg;    // segment index inside the row

@@ -511,7 +511,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
                                               const KeepArgs& keep, const uint16_t* s_adj, const OwnerArgs& oa,
                                               BlockAcc& acc, unsigned long long* s_hist, unsigned long long* tm,
                                               uint32_t tile, K1Stage& st, const K1Out& o, uint64_t& dcur,
-                                              uint64_t dend, uint64_t& rcur) {
+                                              uint64_t dend, uint64_t& rcur, uint32_t cstart) {
   const int lane = lane_id();
   // admission compares specialised on the number of merged runs (wave-uniform)
   uint32_t nlist;
@@ -620,7 +620,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
         // 32-bit byte offsets (positions < 2^30): scalar base + vector offset stores
         const uint32_t u = ustart + row, b2 = u * 2u, b4 = u * 4u;
         if (!(MODE & 512)) {
-          const uint32_t ci = u + R->cdelta;
+          const uint32_t ci = cstart + row;  // code index of row 0 + row (wave-uniform base)
           atomicOr(&o.tcode[ci >> 4], code << ((ci & 15u) << 1));
         }
         if (o.rarea) {
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
         const uint32_t rows = min(rpt, R->end - ustart);
         k1_light_tile<MODE, WIDE>(vc, sc, ttab_slot(wcur), rem, ustart, rows, R->g, rpt, R->rdiv, R, tu, nm,
                                   rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist, tmask + uint64_t(t) * kSub, t,
-                                  st, o, dcur, dend, rcur);
+                                  st, o, dcur, dend, rcur, ustart + R->cdelta);
       }
     }
     t = tn;
@@ -938,6 +938,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
   __shared__ uint64_t s_beg[kWpb][kWave];  // flattened short rows (per wave)
   __shared__ uint32_t s_end[kWpb][kWave], s_tn[kWpb][kWave], s_cnt[kWpb][kWave];
   __shared__ uint16_t s_nm[kWpb][kWave];
+  __shared__ uint64_t s_dst[kWpb][kWave];  // dense survivors' padded row starts (flattened copy)
   __shared__ uint32_t s_rlo[16], s_rlen[16], s_rtu[16], s_rcd[16];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   load_adj(s_adj, pa);
@@ -1105,7 +1106,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
       }
     }
     bool survivor = false, removed = false, cleared = false;
-    if (srec) __threadfence_block();  // the entry updates of other lanes before the dense-row copies
+    uint32_t mv = 0;  // entries of this lane's dense survivor row to move to its padded row
     if (Tu) {
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
@@ -1113,10 +1114,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         tst[u] = T;
         tnxt[u] = T;
         malive[u] = cnt;
-        // dense M: the survivor's (updated) row moves to its padded row
+        // dense M: the survivor's (updated) row moves to its padded row (below, flattened over the wave)
         if (drow) {
           pb = offp[u];
-          for (uint32_t j = 0; j < len; ++j) mcol[pb + j] = mcol[beg + j];
+          mv = len;
           mlen[u] = len;
         }
       } else {
@@ -1142,6 +1143,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             cleared = true;
           }
         }
+      }
+    }
+    // the dense survivors' rows, concatenated over the wave: every lane moves every 64th entry, four in flight
+    // (a row per lane would wait out one load per entry)
+    {
+      const uint32_t incl2 = static_cast<uint32_t>(wave_incl_scan(mv));
+      const uint32_t total2 = static_cast<uint32_t>(__shfl(incl2, kWave - 1, kWave));
+      if (total2) {
+        __threadfence_block();  // the entry updates of other lanes before the copies read them
+        s_end[w][lane] = incl2;
+        s_beg[w][lane] = beg;
+        s_dst[w][lane] = pb;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t t0 = 0; t0 < total2; t0 += 4 * kWave) {
+          uint32_t x[4];
+          uint64_t d[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t t = t0 + q * kWave + lane;
+            d[q] = ~0ull;
+            if (t < total2) {
+              int lo = 0, hi = kWave - 1;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_end[w][mid] > t) hi = mid; else lo = mid + 1;
+              }
+              const uint32_t j = t - (lo ? s_end[w][lo - 1] : 0u);
+              x[q] = mcol[s_beg[w][lo] + j];
+              d[q] = s_dst[w][lo] + j;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (d[q] != ~0ull) mcol[d[q]] = x[q];
+        }
+        __builtin_amdgcn_wave_barrier();
       }
     }
     // live mask of the next superstep (S only shrinks); a vertex removed now
@@ -1533,6 +1570,10 @@ void build_tiling(Ctx& c) {
     cb += c.lr.len[l];
   }
   c.lr.ncode = cb;
+  if (std::getenv("PM_CODE_BY_POSITION")) {  // diagnostics: codes indexed by position (64 MB at S=28)
+    for (int l = 0; l < nl; ++l) c.lr.cd[l] = 0;
+    c.lr.ncode = static_cast<uint32_t>(c.n);
+  }
   std::vector<KRange> tab;
   std::vector<HSeg> hs;
   std::vector<uint64_t> ttab;  // tile descriptors (kTtabRemShift / kTtabRangeShift)
