@@ -535,6 +535,75 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
     return;
   }
   __builtin_amdgcn_wave_barrier();
+  // Dense mode with at most 64 contributors (the common case: ~20 per tile at S=28): phases B1, B2 and the
+  // M stores in registers, one contributor per lane in list order.  A row's contributors are consecutive
+  // lanes; its head lane (first lane of the row) verifies it with the row's TN (OR-ed in the row's LDS half
+  // word) and |M| = its run of lanes; the kept lanes (rows that survive) store their entries compacted.
+  if (MODE == 0 && o.rarea && nlist <= static_cast<uint32_t>(kWave) && dcur + nlist <= dend) {
+    const bool valid = static_cast<uint32_t>(lane) < nlist;
+    uint32_t x = 0, row = kNoRow;
+    if (valid) {
+      x = st.lx[lane];
+      row = k1_row(st.lrel[lane], rem, rdiv);
+    }
+    const bool inrow = row != kNoRow;
+    const uint32_t r1 = inrow ? row + 1u : 0u;  // (0: no row; lane 0 reads 0 from the shift)
+    const bool head = inrow && dpp_wave_shr1_z(r1) != r1;
+    const uint64_t im = __builtin_amdgcn_ballot_w64(inrow);
+    if (!im) return;  // only window slots outside the tile's rows
+    const uint64_t hm = __builtin_amdgcn_ballot_w64(head);
+    if (inrow)
+      atomicOr(&st.tn[row >> 1], static_cast<uint32_t>(tbits_rel<WIDE>(x, rel_runs, s_runs, nruns) & nm)
+                                     << ((row & 1u) << 4));
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* tn16 = reinterpret_cast<uint16_t*>(st.tn);
+    uint16_t T = 0;
+    uint32_t cnt = 0;
+    if (head) {
+      const uint16_t TN = tn16[row];
+      // the row's lanes run up to the next head or the first lane past the tile's rows
+      const uint64_t ends = (hm | ~im) & ~((2ull << lane) - 1ull);  // (lane 63: shift of 64 wraps to 0)
+      const uint32_t nxt = lane == kWave - 1 || !ends ? static_cast<uint32_t>(kWave)
+                                                      : static_cast<uint32_t>(__builtin_ctzll(ends));
+      cnt = nxt - static_cast<uint32_t>(lane);
+      if (TN) {  // (an admitted contributor always meets nm: TN != 0)
+        T = keep_fast(tu, TN, keep, s_adj);
+        if (!T) {
+          acc.removed = 1;
+        } else if (oa.nranks <= 1) {
+          acc.vs += 1;
+          acc.es += cnt;
+        } else {
+          acc_owner(s_hist, oa, ustart + row, cnt);
+        }
+        tn16[row] = 0;  // (TN words are zero between tiles)
+      }
+    }
+    const uint64_t sb = __builtin_amdgcn_ballot_w64(T != 0);
+    if (!sb) return;
+    // a lane is kept iff the head of its row (the highest head lane at or below it) survives
+    const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t hb = hm & upto;
+    const bool kept = inrow && hb && ((sb >> (63 - __builtin_clzll(hb))) & 1ull);
+    const uint64_t kb = __builtin_amdgcn_ballot_w64(kept);
+    const uint32_t kidx = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(kb >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(kb), 0));
+    if (kept) o.mcol[o.dbase + dcur + kidx] = x | kAlive;
+    if (T) {
+      const uint32_t u = ustart + row;
+      const uint32_t code = tpub_code(T, tu);
+      const uint32_t ci = cstart + row;
+      atomicOr(&o.tcode[ci >> 4], code << ((ci & 15u) << 1));
+      if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + u * 2u) = T;
+      const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(sb >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(sb), 0));
+      // the head's kidx: the kept entries before its row (consecutive lanes) = its first dense entry
+      o.rarea[rslot] = make_uint4(u, T | (cnt << 16), static_cast<uint32_t>(dcur + kidx), 0u);
+    }
+    rcur = uniform64(rcur + __builtin_popcountll(sb));
+    dcur = uniform64(dcur + __builtin_popcountll(kb));
+    return;
+  }
   // phase B1 over the list: a row's entries are consecutive (slot order), so
   // its first entry records the row's first list index and its last entry the
   // end; TN is OR-ed into the row's half word.  The lowest and highest listed
