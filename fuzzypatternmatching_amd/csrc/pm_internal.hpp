@@ -477,6 +477,7 @@ unsigned lcc_first_grid(const Ctx& c);
 // first_after_ss0: the superstep right after superstep 0 of the first call
 // (T_pub is still superstep 0's output: neighbours' T_pub from the 2-bit codes)
 void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false);
+void ensure_slist2(Ctx& c);
 // Push form of a later superstep (send + verify launches): directed inputs and
 // LCC calls after the first (M may be asymmetric there).
 void launch_lcc_push(Ctx& c, uint64_t* d_slot);

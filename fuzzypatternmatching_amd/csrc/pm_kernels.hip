@@ -482,6 +482,15 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
   return x;
 }
 
+// A dense superstep-0 record: {position, T_pub | |M| << 16 | (row start >> 32) << 25, first dense M entry,
+// row start (low 32 bits)} -- |M| <= 480 (light rows) fits 9 bits; the padded row start (the slot of the row,
+// where the first later superstep moves a survivor's M) rides along so that superstep needs no offp load.  A
+// start at or above 127 * 2^32 codes 127: load offp.
+__device__ __forceinline__ uint4 k1_record(uint32_t u, uint32_t T, uint32_t cnt, uint32_t first, uint64_t start) {
+  const uint32_t hi = static_cast<uint32_t>(min<uint64_t>(start >> 32, 127));
+  return make_uint4(u, T | (cnt << 16) | (hi << 25), first, static_cast<uint32_t>(start));
+}
+
 // Light tile: rem = rows * g slots from slot qb of rows of g slots (R->rpt = min((kTileEntries - 4) / g,
 // kTileRows) rows per tile), the first at position ustart.
 // Phase A, per 16-B load, all in wave masks: a lane's neighbour can contribute
@@ -598,7 +607,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
       const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(sb >> 32),
                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(sb), 0));
       // the head's kidx: the kept entries before its row (consecutive lanes) = its first dense entry
-      o.rarea[rslot] = make_uint4(u, T | (cnt << 16), static_cast<uint32_t>(dcur + kidx), 0u);
+      o.rarea[rslot] = k1_record(u, T, cnt, static_cast<uint32_t>(dcur + kidx), qb + uint64_t(row) * g);
     }
     rcur = uniform64(rcur + __builtin_popcountll(sb));
     dcur = uniform64(dcur + __builtin_popcountll(kb));
@@ -703,8 +712,8 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
           if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
           const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0));
-          o.rarea[rslot] =
-              make_uint4(u, T | (cnt << 16), dense ? static_cast<uint32_t>(dpos + mrun + incl - c) : kNone, 0u);
+          o.rarea[rslot] = k1_record(u, T, cnt, dense ? static_cast<uint32_t>(dpos + mrun + incl - c) : kNone,
+                                     qb + uint64_t(row) * g);
         } else {
           *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tst) + b2) = T;
           *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
@@ -1047,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     const uint64_t i = chunk * kWave + lane;
     uint32_t u = kNone;
     uint16_t Tu = 0, nm = 0, Ts = 0;
-    uint64_t beg = 0, pb = 0;
+    uint64_t beg = 0, pb = 0, pstart = ~0ull;  // pstart: a dense record's padded row start (k1_record)
     uint32_t len = 0, alive0 = 0;
     bool drow = false;  // M read from the dense superstep-0 region
     if (i < nS && ((live >> lane) & 1ull)) {
@@ -1059,7 +1068,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         u = r.x;
         Tu = static_cast<uint16_t>(r.y);
         dm = r.z;
-        l = dm != kNone ? r.y >> 16 : mlen[u];
+        l = dm != kNone ? (r.y >> 16) & 0x1FFu : mlen[u];
+        if (dm != kNone && (r.y >> 25) < 127u) pstart = (uint64_t(r.y >> 25) << 32) | r.w;
       } else {
         u = slist[i];
         Tu = tcur[u];
@@ -1185,7 +1195,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         malive[u] = cnt;
         // dense M: the survivor's (updated) row moves to its padded row (below, flattened over the wave)
         if (drow) {
-          pb = offp[u];
+          pb = pstart != ~0ull ? pstart : offp[u];
           mv = len;
           mlen[u] = len;
         }
@@ -2091,6 +2101,12 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
   c.smask_valid = false;  // the pull kernel's live masks are not maintained here
 }
 
+void ensure_slist2(Ctx& c) {
+  if (c.d_slist2) return;
+  PM_HIP_CHECK(hipMalloc(&c.d_slist2, std::max<uint64_t>(c.n, 1) * sizeof(uint32_t)));
+  PM_HIP_CHECK(hipMalloc(&c.d_nS2, sizeof(uint32_t)));
+}
+
 void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   // first later superstep (every slist entry live): one chunk per wave, the
@@ -2162,6 +2178,7 @@ __global__ void k_live_write(const uint32_t* __restrict__ slist, const unsigned 
 }
 
 void launch_compact_slist(Ctx& c) {
+  ensure_slist2(c);
   const uint64_t cap = (uint64_t(c.nS_host) + kWave - 1) / kWave;  // nS_host: upper bound of the device count
   if (!cap || !c.smask_valid) return;
   if (c.ccap < cap) {
@@ -2177,10 +2194,6 @@ void launch_compact_slist(Ctx& c) {
                                          rocprim::plus<uint32_t>(), c.stream));
     PM_HIP_CHECK(hipMalloc(&c.d_ctmp, std::max<size_t>(c.ctmp_bytes, 1)));
     c.ccap = words;
-  }
-  if (!c.d_slist2) {
-    PM_HIP_CHECK(hipMalloc(&c.d_slist2, std::max<uint64_t>(c.n, 1) * sizeof(uint32_t)));
-    PM_HIP_CHECK(hipMalloc(&c.d_nS2, sizeof(uint32_t)));
   }
   const auto* mask = reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur]);
   // the keep masks replace the superstep's live masks (that buffer is rewritten by the next superstep)
@@ -2212,6 +2225,7 @@ struct ZeroBatch {
   uint16_t* t0;
   uint16_t* t1;
   uint32_t* ticket;
+  uint32_t cblocks;  // blocks that clear (their last one zeroes *np): few, so the ticket atomics do not queue
 };
 
 __global__ __launch_bounds__(kBlock) void k_zero_batch(ZeroBatch b) {
@@ -2228,9 +2242,9 @@ __global__ __launch_bounds__(kBlock) void k_zero_batch(ZeroBatch b) {
     const uint64_t tail = head + nv * 4;
     if (tail + tid < w) p[tail + tid] = 0u;
   }
-  if (!b.list) return;
+  if (!b.list || blockIdx.x >= b.cblocks) return;
   const uint64_t n = min(static_cast<uint64_t>(*b.np), b.cap);
-  for (uint64_t i = tid; i < n; i += nt) {
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(b.cblocks) * blockDim.x) {
     const uint32_t q = b.list[i];
     b.t0[q] = 0;
     b.t1[q] = 0;
@@ -2238,7 +2252,7 @@ __global__ __launch_bounds__(kBlock) void k_zero_batch(ZeroBatch b) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    if (atomicAdd(b.ticket, 1u) == gridDim.x - 1) {
+    if (atomicAdd(b.ticket, 1u) == b.cblocks - 1) {
       *b.np = 0u;
       *b.ticket = 0u;
     }
@@ -2275,7 +2289,9 @@ void flush_zero(Ctx& c) {
     b.ticket = c.d_zticket;
     most = std::max<uint64_t>(most, c.nS_host);
   }
-  hipLaunchKernelGGL(k_zero_batch, dim3(grid_for(most, kBlock, 2048)), dim3(kBlock), 0, c.stream, b);
+  const unsigned grid = grid_for(most, kBlock, 2048);
+  b.cblocks = std::min<unsigned>(grid, grid_for(b.cap, 16 * kBlock, 2048));  // ~16 entries per thread
+  hipLaunchKernelGGL(k_zero_batch, dim3(grid), dim3(kBlock), 0, c.stream, b);
   PM_HIP_CHECK(hipGetLastError());
   c.nzq = 0;
   c.clear_pending = false;
