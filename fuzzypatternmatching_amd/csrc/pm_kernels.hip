@@ -1003,7 +1003,10 @@ __device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
   return x;
 }
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_lcc_step(
+#ifndef PM_STEP_WAVES
+#define PM_STEP_WAVES 6  // waves per SIMD the register budget of k_lcc_step is sized for
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_WAVES, 8))) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
     uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,

@@ -1,4 +1,5 @@
 """CPU tests of the product's host side: C-ABI library, loaders, generator, graph files."""
+import ctypes
 import os
 import re
 
@@ -123,3 +124,25 @@ def test_gpu_ingest_without_gpu_fails_loudly(tmp_path):
         pm.ingest_edge_list_gpu([str(f)], False)
     with pytest.raises(pm.PMError, match="no HIP device|not gfx950"):
         pm.edge_list_matcher([str(f)], os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern"))
+
+
+def test_label_text_writer_roundtrips_through_the_host_loader(tmp_path):
+    # pm_write_label_text (C5-at-size inputs): "v label" lines split over files <prefix>.<i>, read back by the
+    # -v host parse rules (vertex_data_db.hpp:176-185: iss >> vid >> label per line)
+    lib = _abi.load()
+    labels = pmtest.hash_labels(1000, 64, salt=5)
+    labels[7] = 2 ** 40 + 3  # wide labels survive the text form
+    nb = ctypes.c_uint64()
+    assert lib.pm_write_label_text(labels.ctypes.data, labels.shape[0], str(tmp_path / "lab").encode(), 3,
+                                   ctypes.byref(nb)) == 0
+    back = np.zeros_like(labels)
+    total = 0
+    for i in range(3):
+        txt = open(tmp_path / f"lab.{i}").read()
+        total += len(txt)
+        for line in txt.splitlines():
+            v, lab = line.split()
+            back[int(v)] = int(lab)
+    assert total == nb.value
+    assert np.array_equal(back, labels)
+    assert lib.pm_write_rmat_text(20, 4, 0, str(tmp_path / "e").encode(), ctypes.byref(nb)) != 0  # no GPU here
