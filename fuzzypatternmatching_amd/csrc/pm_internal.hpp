@@ -221,6 +221,7 @@ struct LineStats {
   unsigned int overflow, single;  // single: finished by block 0 alone
   unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
+  unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)
 };
 
 // One NLC line as seen by the fused line kernel (pm_lines.hip).

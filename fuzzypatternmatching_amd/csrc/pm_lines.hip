@@ -743,8 +743,37 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
   build_active(a);
   if (blockIdx.x == 0 && threadIdx.x == 0) kst[1] = __builtin_amdgcn_s_memrealtime();
   tree_barrier(a.gbar);
+  // Source census of every line of the launch on the state as it stands (select_source's test, counted only):
+  // a line that finds no source changes nothing, so the census stays exact up to the first line that has
+  // sources, and the lines before it are skipped without their selection pass and two grid barriers each.
+  {
+    const GridIdx g = grid_idx();
+    const uint64_t nact = ld_dev(a.nact);
+    for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
+      const LineArgs& la = a.lines[pl].la;
+      const bool tds = a.lines[pl].tds != 0;
+      uint64_t cnt = 0;
+      for (uint64_t i0 = g.gw * kWave; i0 < nact; i0 += g.nw * kWave) {
+        const uint64_t i = i0 + lane_id();
+        if (i < nact) {
+          const uint16_t T = a.tpub[ld_dev(&a.act[i])];
+          bool ok = T && pos_ok(T, 0, la);
+          if (ok && !tds && !la.VC && !((T >> la.ilast) & 1u)) ok = false;
+          cnt += ok ? 1u : 0u;
+        }
+      }
+      wave_add(&a.st[pl].census, cnt);
+    }
+    tree_barrier(a.gbar);
+  }
+  bool fresh = true;  // no line of this launch has changed the state yet
   for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
     const LineDesc& d = a.lines[pl];
+    if (fresh && ld_dev(&a.st[pl].census) == 0) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) *a.done = static_cast<unsigned>(pl + 1);
+      continue;
+    }
+    fresh = false;
     LineKernelArgs b = a;
     b.la = &d.la;
     b.i0 = d.i0;
