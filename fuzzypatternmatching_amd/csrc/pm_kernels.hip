@@ -1993,23 +1993,39 @@ void lcc_first_prepare(Ctx& c) {
   if (c.nheavy && c.d_hrec) PM_HIP_CHECK(hipMemsetAsync(c.d_hrec, 0, size_t(c.nheavy) * sizeof(uint4), c.stream));
 }
 
-// slist from the superstep-0 records (dense mode): one wave per record slice copies its records to
-// srec[rofs[w] ..] and their positions to slist; the heavy survivors follow (k_slist_heavy).
+// slist from the superstep-0 records (dense mode): the records of the waves' slices, concatenated in wave
+// order, copied to srec and their positions to slist; the heavy survivors follow (k_slist_heavy).  Every wave
+// copies an equal share of the output (a multiple of 64 records), its first slice found by a binary search of
+// the slice offsets: one wave per slice would wait for the largest slice.
 __global__ void k_slist_from_records(const uint4* __restrict__ rarea, const uint64_t* __restrict__ rbase,
                                      const uint32_t* __restrict__ rcnt, const uint64_t* __restrict__ rofs,
                                      uint32_t W, uint4* __restrict__ srec, uint32_t* __restrict__ slist,
                                      uint32_t* __restrict__ nS) {
   const int lane = lane_id();
+  const uint64_t total = rofs[W - 1] + rcnt[W - 1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *nS = static_cast<uint32_t>(total);
   const uint64_t nw = uint64_t(gridDim.x) * kWpb;
-  for (uint64_t w = blockIdx.x * uint64_t(kWpb) + threadIdx.x / kWave; w < W; w += nw) {
-    const uint32_t n = rcnt[w];
-    const uint64_t src = rbase[w], dst = rofs[w];
-    for (uint32_t i = lane; i < n; i += kWave) {
-      const uint4 r = rarea[src + i];
-      srec[dst + i] = r;
-      slist[dst + i] = r.x;
+  const uint64_t w = blockIdx.x * uint64_t(kWpb) + threadIdx.x / kWave;
+  const uint64_t per = ((total + nw - 1) / nw + kWave - 1) / kWave * kWave;
+  const uint64_t o0 = w * per, o1 = min(total, o0 + per);
+  if (o0 >= o1) return;
+  // the slice holding output o0: the last slice starting at or before it (empty slices share offsets)
+  uint32_t lo = 0, hi = W - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (rofs[mid] <= o0) lo = mid;
+    else hi = mid - 1;
+  }
+  uint32_t sl = lo;
+  uint64_t send = sl + 1 < W ? rofs[sl + 1] : total;  // end of the lane's current slice
+  for (uint64_t i = o0 + lane; i < o1; i += kWave) {
+    while (i >= send) {
+      ++sl;
+      send = sl + 1 < W ? rofs[sl + 1] : total;
     }
-    if (w == W - 1 && lane == 0) *nS = static_cast<uint32_t>(dst + n);
+    const uint4 r = rarea[rbase[sl] + (i - rofs[sl])];
+    srec[i] = r;
+    slist[i] = r.x;
   }
 }
 
