@@ -358,6 +358,7 @@ struct Ctx {
   // (members of S plus vertices removed in that superstep): later passes
   // skip dead chunks without touching them
   uint64_t* d_smask[2] = {nullptr, nullptr};
+  uint64_t* d_kmask = nullptr;  // survivors per 64-entry chunk of the last pull superstep (the compaction's keep)
   int smask_cur = 0;
   bool smask_valid = false;       // false right after superstep 0 (all entries live)
   uint32_t* d_flags = nullptr;    // [0] not_finished, [1] asymmetric edge state, [2] deleted

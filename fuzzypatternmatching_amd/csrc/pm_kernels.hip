@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
     uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
-    const uint4* __restrict__ srec, uint64_t dbase) {
+    const uint4* __restrict__ srec, uint64_t dbase, unsigned long long* __restrict__ keep_out) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1268,6 +1268,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
     // T_pub buffer (it is dropped once it arrives with T_pub = 0)
     const uint64_t lm = __ballot(survivor || (removed && !cleared));
     if (lane == 0) mask_out[chunk] = lm;
+    // keep_out: the survivors (T_pub just written != 0), the list compaction's keep mask
+    const uint64_t km = __ballot(survivor);
+    if (keep_out && lane == 0) keep_out[chunk] = km;
     acc.trav += alive0;
     acc.removed |= removed;
     acc.asym |= asym;
@@ -1293,7 +1296,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
     for (uint64_t k0 = uint64_t(blockIdx.x) * kWpb + w; k0 < nchunks; k0 += W * kWave) {
       const uint64_t ch = k0 + uint64_t(lane) * W;
       const uint64_t lm = ch < nchunks ? mask_in[ch] : 0ull;
-      if (ch < nchunks && !lm) mask_out[ch] = 0;
+      if (ch < nchunks && !lm) {
+        mask_out[ch] = 0;
+        if (keep_out) keep_out[ch] = 0;
+      }
       uint64_t bal = __ballot(lm != 0);
       while (bal) {
         const int j = __ffsll(static_cast<long long>(bal)) - 1;
@@ -2127,6 +2133,7 @@ void ensure_slist2(Ctx& c) {
 }
 
 void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
+  if (!c.d_kmask) PM_HIP_CHECK(hipMalloc(&c.d_kmask, ((c.n + 63) / 64 + 1) * sizeof(uint64_t)));
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   // first later superstep (every slist entry live): one chunk per wave, the
   // latency-bound rows need waves in flight; afterwards few chunks are live
@@ -2139,7 +2146,8 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
-                     c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase);
+                     c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,
+                     reinterpret_cast<unsigned long long*>(c.d_kmask));
   PM_HIP_CHECK(hipGetLastError());
   c.k1_dense = false;  // every M row of S is in its padded row from here on
   c.k1_records = false;
@@ -2181,6 +2189,25 @@ __global__ void k_live_keep(const uint32_t* __restrict__ slist, const unsigned l
   }
 }
 
+// The same from the superstep's own keep mask (k_lcc_step keep_out): no T_pub gather; the slist entries are
+// read only for live entries that were not kept (removed now: the buffer the superstep read is cleared).
+// One lane per chunk.
+__global__ void k_live_keep_masks(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ mask,
+                                  const unsigned long long* __restrict__ keep, const uint32_t* __restrict__ nSp,
+                                  uint64_t cap, uint16_t* __restrict__ told, uint32_t* __restrict__ cnt) {
+  const uint64_t nch = min(cap, (static_cast<uint64_t>(*nSp) + kWave - 1) / kWave);
+  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < nch; c += uint64_t(gridDim.x) * blockDim.x) {
+    const unsigned long long k = keep[c];
+    cnt[c] = static_cast<uint32_t>(__builtin_popcountll(k));
+    unsigned long long gone = mask[c] & ~k;
+    while (gone) {
+      const int b = __builtin_ctzll(gone);
+      gone &= gone - 1;
+      told[slist[c * kWave + b]] = 0;
+    }
+  }
+}
+
 __global__ void k_live_write(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ kmask,
                              const uint32_t* __restrict__ nSp, const uint32_t* __restrict__ cnt,
                              const uint32_t* __restrict__ base, uint32_t* __restrict__ out,
@@ -2215,11 +2242,12 @@ void launch_compact_slist(Ctx& c) {
     c.ccap = words;
   }
   const auto* mask = reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur]);
-  // the keep masks replace the superstep's live masks (that buffer is rewritten by the next superstep)
-  auto* kmask = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
-  // after launch_lcc_step: tpub[cur] was just written, tpub[cur ^ 1] was read
-  hipLaunchKernelGGL(k_live_keep, dim3(grid_for(cap * kWave, kBlock, 2048)), dim3(kBlock), 0, c.stream, c.d_slist,
-                     mask, c.d_nS, cap, c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], kmask, c.d_ccnt);
+  // the pull superstep wrote its survivors per chunk (d_kmask): the keep masks; the T_pub buffer it read is
+  // cleared at its live entries that were not kept (after launch_lcc_step: tpub[cur] was just written,
+  // tpub[cur ^ 1] was read)
+  auto* kmask = reinterpret_cast<unsigned long long*>(c.d_kmask);
+  hipLaunchKernelGGL(k_live_keep_masks, dim3(grid_for(cap, kBlock, 2048)), dim3(kBlock), 0, c.stream, c.d_slist,
+                     mask, kmask, c.d_nS, cap, c.d_tpub[c.cur ^ 1], c.d_ccnt);
   size_t tb = c.ctmp_bytes;
   PM_HIP_CHECK(rocprim::exclusive_scan(c.d_ctmp, tb, c.d_ccnt, c.d_cbase, 0u, size_t(cap), rocprim::plus<uint32_t>(),
                                        c.stream));
