@@ -329,6 +329,14 @@ class PatternMatcher:
         self._check(_lib().pm_run_beta(self._ctx, result_dir.encode(), max_iterations, ctypes.byref(st)))
         return st.as_dict()
 
+    def tpub_census(self, deferred_reset=False):
+        """(nonzero T_pub entries of buffer 0, of buffer 1, positions nonzero in either buffer outside the
+        current slist) -- diagnostics of the invariant the search-start clear relies on
+        (pm_debug_tpub_census); deferred_reset=True first runs a search start's reset."""
+        out = np.zeros(3, np.uint64)
+        self._check(_lib().pm_debug_tpub_census(self._ctx, int(bool(deferred_reset)), out.ctypes.data))
+        return tuple(int(x) for x in out)
+
     def export_state(self):
         """Returns (tpub[n] u16, mdeg[n] u32, nbrs u32) of the current state map."""
         n = self.graph.n

@@ -71,7 +71,7 @@ class RunStats(ctypes.Structure):
     _fields_ = [
         ("iterations", c_u64),
         ("terminated", c_u32),
-        ("reserved", c_u32),
+        ("hubs", c_u32),
         ("lcc_edges", c_u64),
         ("nlcc_edges", c_u64),
         ("tds_edges", c_u64),
@@ -82,6 +82,7 @@ class RunStats(ctypes.Structure):
         ("device_seconds", ctypes.c_double),
         ("lcc_first_kernel_ms", ctypes.c_double),
         ("lcc_first_bytes", c_u64),
+        ("tds_chunks", c_u64),
     ]
 
     def as_dict(self):
@@ -110,6 +111,7 @@ SIGNATURES = [
     ("pm_pattern_summary", ctypes.c_int, [c_char_p, c_char_p, c_u64]),
     ("pm_debug_time_lcc_first", ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     ("pm_debug_layout_stats", ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
+    ("pm_debug_tpub_census", ctypes.c_int, [c_vp, ctypes.c_int, c_vp]),
     ("pm_write_rmat_text", ctypes.c_int, [c_u64, c_u64, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(c_u64)]),
     ("pm_write_label_text", ctypes.c_int, [c_vp, c_u64, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(c_u64)]),
     ("pm_debug_copy_gbs", ctypes.c_int, [ctypes.c_int, c_u64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),

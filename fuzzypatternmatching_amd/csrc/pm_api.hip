@@ -258,8 +258,6 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
   c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
-  if (c->dcap) {
-  }
   c->d_mlen = dalloc<uint32_t>(c->n);
   c->d_malive = dalloc<uint32_t>(c->n);
   c->d_slist = dalloc<uint32_t>(c->n);
@@ -362,6 +360,7 @@ static void relayout(Ctx& c) {
 static void reset_state(Ctx& c, bool defer = false) {
   if (c.tpub_clean && c.lcc_started) {
     c.clear_pending = true;  // nonzero T_pub only at (every shard's) slist entries; d_nS zeroed after the clear
+    c.clear_cap = c.nS_host;
   } else {
     if (!c.tpub_clean) {
       PM_HIP_CHECK(hipMemsetAsync(c.d_tpub[0], 0, c.n * sizeof(uint16_t), c.stream));
@@ -395,6 +394,17 @@ struct LccOut {
   std::vector<uint64_t> loc_vc, loc_ec;
   uint64_t loc_surv = 0, loc_edges = 0;
 };
+
+void debug_point(Ctx& c, const char* where) {
+  static const int level = std::getenv("PM_DEBUG_SYNC") ? std::atoi(std::getenv("PM_DEBUG_SYNC")) : 0;
+  if (!level) return;
+  hipError_t e = hipStreamSynchronize(c.stream);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("device fault before debug point '") + where + "' (shard " +
+                             std::to_string(c.shard) + "): " + hipGetErrorString(e));
+  if (level >= 2) std::fprintf(stderr, "[pm dbg] shard %u: %s ok\n", c.shard, where);
+}
 
 // Pinned host staging of at least `words` u64 (read-backs of the driver loop).
 uint64_t* pinned(Ctx& c, size_t words) {
@@ -438,6 +448,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
       launch_lcc_first(c, slot, ev[D + 1], ev[D + 2]);
+      debug_point(c, "superstep 0");
       k_timed = true;
       // |slist| is read back with the counters at the end of the call; until
       // then later supersteps size their grids by its upper bound
@@ -446,8 +457,10 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       // sharded: the delegates' shares meet at their controllers; the survivors' codes of every shard
       // for the next superstep's pulls; a one-superstep pattern goes to the replica at once
       if (c.split_hubs) shard_hub_combine(c, slot);
+      debug_point(c, "delegate combine");
       if (D >= 2) shard_codes_after_first(c);
       else shard_replicate(c);
+      debug_point(c, "code exchange / replica");
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
       // pull form while M is known symmetric (the first call on a symmetric
@@ -459,10 +472,13 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         // entries inside the superstep, one counter reservation per 64-entry chunk, measured 1.2 ms slower
         // at S=28: 153 k atomics on one address serialise.)
         launch_lcc_step(c, slot, init_step && ss == 1);
+        debug_point(c, "pull superstep");
         if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
+        debug_point(c, "list compaction");
       }
       // sharded: after the first later superstep the state of S goes to the replica
       if (init_step && ss == 1) shard_replicate(c);
+      debug_point(c, "superstep end");
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
@@ -479,6 +495,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   }
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   if (c.prelaunch_lines) prelaunch_lines_fused(c);  // the device goes on with the lines while the host parses
+  debug_point(c, "counters + prelaunched lines");
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("lcc synced");
   std::vector<uint64_t> host(pin + 1 + D * W, pin + 1 + 2 * D * W);
@@ -650,6 +667,21 @@ static void write_lines(const std::string& path, const std::vector<std::string>&
   for (const auto& l : lines) f << l << "\n";
 }
 
+// Subgraph lines "[r], w0, ..., wk, [wk]" of kept TDS walks (positions, `stride` per walk), into the file of
+// the owner of the last vertex (tds_batch_1.hpp:739-743).
+static void add_walk_lines(const Ctx& c, std::vector<std::vector<std::string>>& files, const uint32_t* walks,
+                           uint64_t n, uint32_t stride) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t* w = walks + i * stride;
+    const uint32_t last = c.perm_host[w[stride - 1]];
+    const uint32_t r = owner_host(c, last);
+    std::string l = "[" + std::to_string(r) + "], ";
+    for (uint32_t p = 0; p < stride; ++p) l += std::to_string(c.perm_host[w[p]]) + ", ";
+    l += "[" + std::to_string(last) + "]";
+    files[r].push_back(std::move(l));
+  }
+}
+
 // run_pattern_matching_beta.cpp:539-1425
 static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations, pm_run_stats* st) {
   const Pattern& P = c.pattern;
@@ -789,7 +821,12 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         } else {
           // exact-count path (one launch + sync per position)
           if (pl >= 4) {  // beta.cpp:762-767
-            tr = run_tds_line(c, line, walks, stride);
+            // the kept walks become subgraph lines chunk by chunk (the chunked enumeration bounds the device
+            // memory, the lines are all the host keeps)
+            tr = run_tds_line(c, line, stride, [&](const uint32_t* w, uint64_t nk) {
+              if (lines_on) add_walk_lines(c, subgraphs[pl], w, nk, stride);
+            });
+            s.tds_chunks += c.last_tds_chunks;
           } else {
             tr = run_path_line(c, line);
           }
@@ -804,15 +841,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         if (pl >= 4) {
           s.tds_edges += tr.edges;
           s.walks = tr.walks;
-          for (uint64_t i = 0; i < walks.size() / std::max<uint32_t>(stride, 1); ++i) {
-            const uint32_t* w = walks.data() + i * stride;  // positions
-            const uint32_t last = c.perm_host[w[stride - 1]];
-            const uint32_t r = owner_host(c, last);
-            std::string l = "[" + std::to_string(r) + "], ";
-            for (uint32_t p = 0; p < stride; ++p) l += std::to_string(c.perm_host[w[p]]) + ", ";
-            l += "[" + std::to_string(last) + "]";
-            subgraphs[pl][r].push_back(std::move(l));
-          }
+          if (stride) add_walk_lines(c, subgraphs[pl], walks.data(), walks.size() / stride, stride);
         } else {
           s.nlcc_edges += tr.edges;
         }
@@ -857,6 +886,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   }
   s.iterations = itr;
   s.terminated = terminated ? 1 : 0;
+  s.hubs = static_cast<uint32_t>(c.hubs_host.size());
   s.seconds = secs;
   s.device_seconds = c.device_seconds;
   s.lcc_first_kernel_ms = c.lcc_first_ms;
@@ -1023,16 +1053,19 @@ int pm_tds(pm_ctx* ctx, uint32_t pl, pm_path_sink sink, void* user, pm_tp_stats*
     if (ctx->comm) throw std::runtime_error("pm_tds: sharded contexts run lines through pm_run_beta");
     if (pl >= ctx->pattern.lines.size()) throw std::runtime_error("NLC line index out of range");
     if (pl < 4) throw std::runtime_error("pm_tds: line index below 4 is a path / cycle line (pm_token_passing)");
-    std::vector<uint32_t> walks;
+    // kept walks reach the sink chunk by chunk, in the enumeration's order
     uint32_t stride = 0;
-    const pm::TpResult r = pm::run_tds_line(*ctx, ctx->pattern.lines[pl], walks, stride);
-    if (sink && stride) {
-      std::vector<uint32_t> ids(stride);
-      for (uint64_t i = 0; i < walks.size() / stride; ++i) {
-        for (uint32_t p = 0; p < stride; ++p) ids[p] = ctx->perm_host[walks[i * stride + p]];
-        sink(user, pm::owner_host(*ctx, ids[stride - 1]), ids.data(), stride);
-      }
-    }
+    std::vector<uint32_t> ids;
+    const pm::TpResult r = pm::run_tds_line(*ctx, ctx->pattern.lines[pl], stride,
+                                            [&](const uint32_t* w, uint64_t n) {
+                                              if (!sink) return;
+                                              ids.resize(stride);
+                                              for (uint64_t i = 0; i < n; ++i) {
+                                                for (uint32_t p = 0; p < stride; ++p)
+                                                  ids[p] = ctx->perm_host[w[i * stride + p]];
+                                                sink(user, pm::owner_host(*ctx, ids[stride - 1]), ids.data(), stride);
+                                              }
+                                            });
     if (out) {
       out->sources = r.sources;
       out->acked_sources = 0;
@@ -1842,6 +1875,34 @@ int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n) {
       st[2] += R.end - R.start;
     }
     for (uint64_t i = 0; i < n && i < 7; ++i) out[i] = st[i];
+  });
+}
+
+int pm_debug_tpub_census(pm_ctx* ctx, int deferred_reset, uint64_t* out) {
+  PM_API_BODY(ctx, {
+    if (!out) throw std::runtime_error("null output");
+    if (deferred_reset) {
+      pm::reset_state(*ctx, true);
+      pm::flush_zero(*ctx);
+    }
+    const uint64_t n = ctx->n;
+    std::vector<uint16_t> t0(n), t1(n);
+    uint32_t ns = 0;
+    PM_HIP_CHECK(hipMemcpyAsync(t0.data(), ctx->d_tpub[0], n * sizeof(uint16_t), hipMemcpyDeviceToHost, ctx->stream));
+    PM_HIP_CHECK(hipMemcpyAsync(t1.data(), ctx->d_tpub[1], n * sizeof(uint16_t), hipMemcpyDeviceToHost, ctx->stream));
+    PM_HIP_CHECK(hipMemcpyAsync(&ns, ctx->d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    std::vector<uint32_t> sl(ns);
+    if (ns) PM_HIP_CHECK(hipMemcpy(sl.data(), ctx->d_slist, ns * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<uint8_t> in(n, 0);
+    for (uint32_t p : sl)
+      if (p < n) in[p] = 1;
+    out[0] = out[1] = out[2] = 0;
+    for (uint64_t p = 0; p < n; ++p) {
+      out[0] += t0[p] != 0;
+      out[1] += t1[p] != 0;
+      out[2] += (t0[p] || t1[p]) && !in[p];
+    }
   });
 }
 

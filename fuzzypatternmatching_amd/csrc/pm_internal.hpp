@@ -6,6 +6,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -410,8 +411,10 @@ struct Ctx {
   };
   ZeroRange zq[8];
   int nzq = 0;
-  bool clear_pending = false;
-  bool k1_fills_queued = false;    // queue_lcc_first_fills ran for the next superstep-0 launch      // T_pub at the slist entries, then d_nS (flush_zero)
+  bool clear_pending = false;      // T_pub at the slist entries, then d_nS (flush_zero)
+  uint32_t clear_cap = 0;          // host bound of the slist the pending clear walks (saved at reset: nS_host is
+                                   // zeroed before the deferred flush)
+  bool k1_fills_queued = false;    // queue_lcc_first_fills ran for the next superstep-0 launch
   uint32_t* d_zticket = nullptr;   // last-block ticket of k_zero_batch (zero between launches)
   std::vector<hipEvent_t> events;  // LCC call timing, created once
   uint32_t nS_host = 0;     // size of d_slist (host copy, valid after superstep 0)
@@ -443,6 +446,7 @@ struct Ctx {
   uint64_t nsources = 0;
   std::vector<std::vector<std::string>> walk_lines;  // per rank, last TDS line
   uint64_t last_walks = 0;
+  uint64_t last_tds_chunks = 0;   // chunk launches of the last exact-path TDS line (unbatched: one per level)
 
   // timing of the fused superstep-0 kernel (for the roofline report)
   float lcc_first_ms = 0.f;
@@ -529,11 +533,19 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
 void prelaunch_lines_fused(Ctx& c);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
+// The same with the kept walks handed to `sink` chunk by chunk (positions, stride C+2 each) instead of
+// collected: the exact path's enumeration is depth-first over chunks of at most tds_walk_cap walks.
+using TdsSink = std::function<void(const uint32_t* walks, uint64_t n)>;
+TpResult run_tds_line(Ctx& c, const NlcLine& line, uint32_t& stride, const TdsSink& sink);
+uint64_t tds_walk_cap(const Ctx& c, int stride);  // walks per level chunk (arena room; PM_TDS_CAP caps it)
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line);
 
 LineArgs make_line_args(const Ctx& c, const NlcLine& line);
 
 uint64_t* pinned(Ctx& c, size_t words);  // pinned host staging (pm_api.hip)
+// PM_DEBUG_SYNC=1 (diagnostics): the stream is synchronised at each named point and a device fault is reported
+// with the point's name and the shard (=2: every point passed is also printed); no-op otherwise.
+void debug_point(Ctx& c, const char* where);
 
 // Shard exchanges (pm_shard.hip); no-ops without a communicator.
 // after superstep 0 (sharded, delegates): the shares' TN / counts all-gathered and OR-ed / summed, the

@@ -2330,11 +2330,11 @@ void flush_zero(Ctx& c) {
     }
     b.list = c.d_slist;
     b.np = c.d_nS;
-    b.cap = c.nS_host;
+    b.cap = c.clear_cap;
     b.t0 = c.d_tpub[0];
     b.t1 = c.d_tpub[1];
     b.ticket = c.d_zticket;
-    most = std::max<uint64_t>(most, c.nS_host);
+    most = std::max<uint64_t>(most, c.clear_cap);
   }
   const unsigned grid = grid_for(most, kBlock, 2048);
   b.cblocks = std::min<unsigned>(grid, grid_for(b.cap, 16 * kBlock, 2048));  // ~16 entries per thread
@@ -2597,12 +2597,12 @@ __global__ void k_tp_terminal_sv(const uint32_t* __restrict__ tu, const uint32_t
 }
 
 __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
-                           const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
+                           uint64_t obase0, const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
                            const uint32_t* __restrict__ mlen, int stride,
                            uint32_t* __restrict__ walks) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
-    uint64_t o = obase[i];
+    uint64_t o = obase[i] - obase0;
     const uint64_t b = offp[s], L = mlen[s];
     for (uint64_t e = b; e < b + L; ++e) {
       if (!(mcol[e] & kAlive)) continue;
@@ -2620,7 +2620,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
                              const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
                              const uint32_t* __restrict__ mcol,
                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive,
-                             uint32_t* __restrict__ cnt, const uint64_t* __restrict__ obase,
+                             uint32_t* __restrict__ cnt, const uint64_t* __restrict__ obase, uint64_t obase0,
                              uint32_t* __restrict__ wout, unsigned long long* __restrict__ trav) {
   uint64_t t = 0;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nw; i += uint64_t(gridDim.x) * blockDim.x) {
@@ -2630,7 +2630,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
     if (pos_ok(tpub[u], k, la) && enum_ok(w, k, u, la)) {
       const uint32_t s = w[0];
       const uint64_t b = offp[u], L = mlen[u];
-      uint64_t o = PASS ? obase[i] : 0;
+      uint64_t o = PASS ? obase[i] - obase0 : 0;
       for (uint64_t e = b; e < b + L; ++e) {
         if (!(mcol[e] & kAlive)) continue;
         const uint32_t nb = mcol[e] & kPosMask;
@@ -2947,14 +2947,108 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
   return res;
 }
 
-TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride_out) {
+// TDS line (tds_batch_1.hpp:976-1324) on the exact path: a depth-first enumeration over bounded chunks.  The
+// reference enumerates in source batches (the batch loop at :1181) so that a batch's tokens fit; here every
+// level of the walk tree is cut into chunks whose children number at most `cap` walks, and a chunk's whole
+// subtree is enumerated (down to the terminal, whose kept walks go to the sink) before the next chunk is
+// expanded.  Device memory is then bounded by (C + 1) levels of at most cap walks, whatever the total
+// frontier; a level's pass-0 count (and its traversed-edge counter) still covers the level's whole walk set,
+// and the kept walks come out in the order of the unbatched enumeration (lexicographic by the children's
+// indices), for every cap.  PM_TDS_CAP=<walks> forces a small cap (tests).
+namespace {
+struct TdsRun {
+  Ctx& c;
+  LineArgs la;
+  int C, stride;
+  uint64_t cap;
+  const uint16_t* tpub;
+  unsigned long long* d_trav;
+  TpResult& res;
+  const TdsSink& sink;
+  uint64_t chunks = 0, kept = 0;
+
+  // children of the walks at position k: count, scan, then chunk by chunk
+  void expand(int k, const uint32_t* walks, uint64_t nw) {
+    if (k > C) return terminal(walks, nw);
+    const size_t mark = c.arena.used;
+    auto* wc = arena_alloc<uint32_t>(c, nw);
+    hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
+                       stride, la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_malive, wc,
+                       static_cast<const uint64_t*>(nullptr), uint64_t(0), static_cast<uint32_t*>(nullptr), d_trav);
+    auto* wb = arena_alloc<uint64_t>(c, nw + 1);
+    const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
+    res.tokens += nnext;
+    if (nnext) {
+      std::vector<uint64_t> hb;  // host copy of the scan when the level is split
+      if (nnext > cap) {
+        hb.resize(nw + 1);
+        PM_HIP_CHECK(hipMemcpyAsync(hb.data(), wb, (nw + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+        PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+      }
+      for (uint64_t i0 = 0; i0 < nw;) {
+        uint64_t i1 = nw, b0 = 0, n = nnext;
+        if (!hb.empty()) {  // the longest run of walks whose children fit the cap (at least one walk)
+          b0 = hb[i0];
+          i1 = static_cast<uint64_t>(std::upper_bound(hb.begin() + i0 + 1, hb.end(), b0 + cap) - hb.begin()) - 1;
+          i1 = std::max(i1, i0 + 1);
+          n = hb[i1] - b0;
+        }
+        if (n) {
+          const size_t cm = c.arena.used;
+          auto* child = arena_alloc<uint32_t>(c, n * stride);
+          hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(i1 - i0, kBlock, 1024)), dim3(kBlock), 0, c.stream,
+                             walks + i0 * stride, i1 - i0, k, stride, la, tpub, m_off(c), m_col(c), c.d_mlen,
+                             c.d_malive, wc + i0, wb + i0, b0, child, d_trav);
+          PM_HIP_CHECK(hipGetLastError());
+          ++chunks;
+          expand(k + 1, child, n);
+          c.arena.used = cm;
+        }
+        i0 = i1;
+      }
+    }
+    c.arena.used = mark;
+  }
+
+  // terminal position C+1 (tds_batch_1.hpp:641-758): kept walks to the sink, in order
+  void terminal(const uint32_t* walks, uint64_t nw) {
+    if (!nw) return;
+    const size_t mark = c.arena.used;
+    auto* keep = arena_alloc<uint8_t>(c, nw);
+    hipLaunchKernelGGL(k_tds_terminal, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, stride,
+                       la, tpub, c.d_tsm, keep);
+    PM_HIP_CHECK(hipGetLastError());
+    std::vector<uint32_t> all(nw * stride), out;
+    std::vector<uint8_t> kp(nw);
+    PM_HIP_CHECK(hipMemcpyAsync(all.data(), walks, nw * stride * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipMemcpyAsync(kp.data(), keep, nw, hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    for (uint64_t i = 0; i < nw; ++i)
+      if (kp[i]) out.insert(out.end(), all.begin() + i * stride, all.begin() + (i + 1) * stride);
+    const uint64_t nk = out.size() / stride;
+    kept += nk;
+    if (nk) sink(out.data(), nk);
+    c.arena.used = mark;
+  }
+};
+}  // namespace
+
+uint64_t tds_walk_cap(const Ctx& c, int stride) {
+  // (C + 1) levels of at most cap walks: the walks (4 B per position), their child counts (4 B) and scan (8 B)
+  const uint64_t free_b = c.arena.cap > c.arena.used ? c.arena.cap - c.arena.used : 0;
+  uint64_t cap = free_b / (uint64_t(stride) * (4ull * stride + 16) * 5 / 4);
+  if (const char* e = std::getenv("PM_TDS_CAP")) cap = std::min<uint64_t>(cap, std::strtoull(e, nullptr, 10));
+  return std::max<uint64_t>(cap, 1);
+}
+
+TpResult run_tds_line(Ctx& c, const NlcLine& line, uint32_t& stride_out, const TdsSink& sink) {
   TpResult res;
   c.arena.reset();
   const LineArgs la = make_line_args(c, line);
   const int C = la.C;
   const int stride = C + 2;
   stride_out = static_cast<uint32_t>(stride);
-  walks_out.clear();
+  c.last_tds_chunks = 0;
   if (line.enumeration.size() < static_cast<size_t>(stride))
     throw std::runtime_error("pattern_non_local_constraint enumeration shorter than the TDS walk");
   auto* d_trav = arena_alloc<unsigned long long>(c, 1);
@@ -2963,54 +3057,55 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_
   ensure_sources(c, la, 1, line);
   res.sources = c.nsources;
   if (c.nsources == 0) return res;
-  const uint16_t* tpub = c.d_tpub[c.cur];
+  TdsRun run{c, la, C, stride, 0, c.d_tpub[c.cur], d_trav, res, sink};
+  // the sources' position-1 walks [s, w] (w alive in M[s]) in source batches of at most cap walks
   auto* cnt = arena_alloc<uint32_t>(c, c.nsources);
   auto* obase = arena_alloc<uint64_t>(c, c.nsources + 1);
   hipLaunchKernelGGL(k_row_alive, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
                      c.nsources, 1, 0, m_off(c), c.d_malive, cnt);
-  uint64_t nw = exclusive_scan_u32_to_u64(c, cnt, obase, c.nsources);
-  const uint64_t trav_init = nw;
-  auto* walks = arena_alloc<uint32_t>(c, nw * stride);
-  hipLaunchKernelGGL(k_tds_init, dim3(grid_for(c.nsources, kBlock, 4096)), dim3(kBlock), 0, c.stream, c.d_sources,
-                     c.nsources, obase, m_off(c), m_col(c), c.d_mlen, stride, walks);
-  PM_HIP_CHECK(hipGetLastError());
-  res.tokens += nw;
-  for (int k = 1; k <= C && nw > 0; ++k) {
-    auto* wc = arena_alloc<uint32_t>(c, nw);
-    hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                       stride, la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_malive, wc,
-                       static_cast<const uint64_t*>(nullptr), static_cast<uint32_t*>(nullptr), d_trav);
-    auto* wb = arena_alloc<uint64_t>(c, nw + 1);
-    const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
-    auto* wn = arena_alloc<uint32_t>(c, nnext * stride);
-    if (nnext) {
-      hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
-                         stride, la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_malive, wc, wb, wn, d_trav);
-      PM_HIP_CHECK(hipGetLastError());
-    }
-    walks = wn;
-    nw = nnext;
-    res.tokens += nw;
-  }
-  if (nw > 0) {
-    auto* keep = arena_alloc<uint8_t>(c, nw);
-    hipLaunchKernelGGL(k_tds_terminal, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, stride,
-                       la, tpub, c.d_tsm, keep);
-    PM_HIP_CHECK(hipGetLastError());
-    std::vector<uint32_t> all(nw * stride);
-    std::vector<uint8_t> kp(nw);
-    PM_HIP_CHECK(hipMemcpyAsync(all.data(), walks, nw * stride * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-    PM_HIP_CHECK(hipMemcpyAsync(kp.data(), keep, nw, hipMemcpyDeviceToHost, c.stream));
+  const uint64_t nw1 = exclusive_scan_u32_to_u64(c, cnt, obase, c.nsources);
+  const uint64_t trav_init = nw1;  // sources scan all of M[s]
+  res.tokens += nw1;
+  run.cap = tds_walk_cap(c, stride);
+  std::vector<uint64_t> hb;
+  if (nw1 > run.cap) {
+    hb.resize(c.nsources + 1);
+    PM_HIP_CHECK(hipMemcpyAsync(hb.data(), obase, hb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-    for (uint64_t i = 0; i < nw; ++i)
-      if (kp[i]) walks_out.insert(walks_out.end(), all.begin() + i * stride, all.begin() + (i + 1) * stride);
   }
-  res.walks = walks_out.size() / stride;
+  for (uint64_t i0 = 0; i0 < c.nsources;) {
+    uint64_t i1 = c.nsources, b0 = 0, n = nw1;
+    if (!hb.empty()) {
+      b0 = hb[i0];
+      i1 = static_cast<uint64_t>(std::upper_bound(hb.begin() + i0 + 1, hb.end(), b0 + run.cap) - hb.begin()) - 1;
+      i1 = std::max(i1, i0 + 1);
+      n = hb[i1] - b0;
+    }
+    if (n) {
+      const size_t mark = c.arena.used;
+      auto* walks = arena_alloc<uint32_t>(c, n * stride);
+      hipLaunchKernelGGL(k_tds_init, dim3(grid_for(i1 - i0, kBlock, 4096)), dim3(kBlock), 0, c.stream,
+                         c.d_sources + i0, i1 - i0, obase + i0, b0, m_off(c), m_col(c), c.d_mlen, stride, walks);
+      PM_HIP_CHECK(hipGetLastError());
+      ++run.chunks;
+      run.expand(1, walks, n);
+      c.arena.used = mark;
+    }
+    i0 = i1;
+  }
+  c.last_tds_chunks = run.chunks;
+  res.walks = run.kept;
   unsigned long long trav = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&trav, d_trav, sizeof(trav), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   res.edges = trav + trav_init;
   return res;
+}
+
+TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride_out) {
+  walks_out.clear();
+  return run_tds_line(c, line, stride_out,
+                      [&](const uint32_t* w, uint64_t n) { walks_out.insert(walks_out.end(), w, w + n * stride_out); });
 }
 
 uint32_t launch_post_tp(Ctx& c, const NlcLine& line) {

@@ -922,13 +922,17 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   a.kept_cap = room / 4;
   a.kept = static_cast<uint32_t*>(c.arena.get(a.kept_cap * sizeof(uint32_t)));
   a.wcap = (c.arena.cap - c.arena.used - 4096) / sizeof(uint32_t);
+  // PM_TDS_CAP (tests): the fused walk storage is bounded too, so that a larger enumeration overflows into the
+  // exact path's chunked enumeration
+  if (const char* e = std::getenv("PM_TDS_CAP")) a.wcap = std::min<uint64_t>(a.wcap, std::strtoull(e, nullptr, 10));
   a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
   void* args[] = {&a};
   c.probe("lines launch");
   // few state-map members: a smaller grid (dispatching the full one costs ~50 us
   // before the first grid barrier completes)
-  const unsigned grid = static_cast<unsigned>(
-      std::max<uint64_t>(16, std::min<uint64_t>(c.line_grid, (c.live_hint + 255) / 256)));
+  // (live_hint ~0: unknown after a relayout -- the full grid; the rounding must not wrap)
+  const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+      16, c.live_hint == ~0ull ? c.line_grid : std::min<uint64_t>(c.line_grid, c.live_hint / 256 + 1)));
   static const bool nocoop = std::getenv("PM_LINES_NOCOOP") && std::string(std::getenv("PM_LINES_NOCOOP")) == "1";
   if (nocoop)
     PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args, 0,
@@ -937,6 +941,7 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args,
                                             0, c.stream));
   c.probe("lines launched");
+  debug_point(c, "NLC line kernel");
   // read-back through pinned memory, one copy: [done | . | kept slots | ... (64 words) | line stats]
   static_assert(sizeof(LineStats) % 8 == 0, "LineStats is read back as u64 words");
   const size_t words = ctl_bytes / 8;

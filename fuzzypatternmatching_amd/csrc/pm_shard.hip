@@ -503,7 +503,10 @@ __global__ void k_hub_finish(HubFinishArgs a) {
         atomicAdd(&a.slot[2 * a.P + 2], 1ull);  // removed from S (not_finished)
       } else {
         a.tst[p] = T;
-        a.tpub[p] = T;
+        // with superstep-0 records T_pub travels in the record (k1_finish_row's rule): the position-indexed
+        // T_pub is written only for code 3 (gathered by the next superstep), so a hub that superstep removes
+        // leaves both T_pub buffers clean
+        if (!a.srec || tpub_code(T, tu) == 3u) a.tpub[p] = T;
         a.mlen[p] = static_cast<uint32_t>(cnt);
         a.malive[p] = static_cast<uint32_t>(cnt);
         const uint32_t ci = code_index(p, a.lr);
@@ -614,6 +617,7 @@ void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
   if (so)
     hipLaunchKernelGGL(k_hub_pack, dim3(xgrid(uint64_t(H) * 64)), dim3(kXBlock), 0, c.stream, c.d_hubinfo, H, d_soff,
                        c.d_offp, c.d_mcol, send);
+  debug_point(c, "delegate pack");
   c.comm->alltoallv(send, sb.data(), recv, rb.data(), c.stream);
   HubFinishArgs a{};
   a.ctrl = d_ctrl;
@@ -661,6 +665,7 @@ void shard_codes_after_first(Ctx& c) {
   hipLaunchKernelGGL(k_pack_codes, dim3(xgrid(c.nS_host)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tcode,
                      c.d_tpub[c.cur], c.k1_records ? c.d_srec : nullptr, c.xcode_wide ? 1 : 0, c.lr,
                      reinterpret_cast<uint32_t*>(send), reinterpret_cast<unsigned long long*>(send));
+  debug_point(c, "code pack");
   c.comm->allgather(send, recv, maxS * rb, c.stream);
   XCounts x{};
   for (uint32_t g = 0; g < G; ++g) x.n[g] = n[g];
@@ -727,6 +732,7 @@ void shard_replicate(Ctx& c) {
                        c.d_tpub[c.cur ^ 1]);
   }
   c.xcode_n.clear();
+  debug_point(c, "replica: code clear");
   // this shard's rows of S: counts first, then one gather of every shard's counts (one host sync)
   pack_state(c, nullptr, nullptr, 0, c.d_xcnt);
   const std::vector<uint64_t> cn = gather_counts(c, 2);
@@ -751,6 +757,12 @@ void shard_replicate(Ctx& c) {
   auto* erecv = grow<uint32_t>(c.d_xent_recv, c.xent_recv_cap, uint64_t(G) * maxE * 4);
   c.comm->allgather(rsend, rrecv, maxR * 16, c.stream);
   c.comm->allgather(esend, erecv, maxE * 4, c.stream);
+  // the replica's slist replaces this shard's: both T_pub buffers are cleared at this shard's entries first
+  // (rows the last superstep removed may hold an old T_pub -- a code-3 row of superstep 0 when no compaction
+  // ran, diameter 2 -- and would be outside every later clear); the rows of S get theirs back from the gather
+  debug_point(c, "replica: pack + gather");
+  launch_clear_tpub(c);
+  debug_point(c, "replica: own T_pub clear");
   if (!c.d_rmoff) PM_HIP_CHECK(hipMalloc(&c.d_rmoff, std::max<uint64_t>(c.n, 1) * sizeof(uint64_t)));
   if (c.rmcap < ents + 1 || !c.d_rmcol) {
     if (c.d_rmcol) (void)hipFree(c.d_rmcol);

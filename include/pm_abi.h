@@ -92,7 +92,7 @@ typedef struct pm_tp_stats {
 typedef struct pm_run_stats {
   uint64_t iterations;
   uint32_t terminated;          /* 0 when max_iterations stopped the loop           */
-  uint32_t reserved;
+  uint32_t hubs;                /* delegates: vertices of degree >= hub_threshold    */
   uint64_t lcc_edges;
   uint64_t nlcc_edges;
   uint64_t tds_edges;
@@ -103,6 +103,8 @@ typedef struct pm_run_stats {
   double device_seconds;        /* sum of device-event time inside the loop         */
   double lcc_first_kernel_ms;   /* duration of the fused superstep-0 scan kernel    */
   uint64_t lcc_first_bytes;     /* algorithmic bytes of that kernel                 */
+  uint64_t tds_chunks;          /* chunk launches of exact-path TDS enumerations (0: every TDS line ran in
+                                   the fused kernel; see run_tds_line, PM_TDS_CAP)    */
 } pm_run_stats;
 
 /* One shard (rank) of a sharded search: the rows of ids v % nshards == shard. */
@@ -244,6 +246,12 @@ int pm_debug_rccl_selftest(int device, uint64_t bytes, int op);
 int pm_debug_copy_gbs(int device, uint64_t bytes, int reps, double* gbs);
 /* Diagnostics: superstep-0 tiling statistics (real entries, loaded slots, rows, tiles, ranges, heavy rows). */
 int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n);
+
+/* Diagnostics: T_pub census (both ping-pong buffers) -- out[0], out[1]: nonzero entries of buffer 0 / 1,
+   out[2]: positions with a nonzero entry in either buffer that are not in the current slist (the invariant
+   the search-start clear relies on: 0).  deferred_reset != 0 first runs the search start's reset as a search
+   does (deferred, then flushed in one launch), so out[0..2] must all be 0 afterwards. */
+int pm_debug_tpub_census(pm_ctx* ctx, int deferred_reset, uint64_t* out);
 
 /* Build info: returns the offload arch the kernels were compiled for ("gfx950"). */
 const char* pm_build_arch(void);

@@ -137,3 +137,30 @@ def test_c4_s28_tree_one_gpu(tmp_path):
         m.close()
     assert diffs == [], diffs[:5]
     print(f"S=28 parity vs the oracle fixture: {sg}")
+
+
+@pytest.mark.parametrize("nshards", [2])
+def test_c4_s28_sharded_delegates_one_gpu(nshards, tmp_path):
+    """C4's sharded path at full size on one GPU: pm_run_rmat_local_shards(S=28, P_gen=8, tree, -d 1048576)
+    with `nshards` shards as threads of this process (the RCCL exchanges replaced by the in-process Comm):
+    every shard generates its generator ranks' streams, the entries reach their owners in one all-to-all,
+    the delegates' rows (degree >= 1048576) are split by target owner and meet at their controllers, the
+    survivors' codes are all-gathered and the state is replicated.  The result must equal the oracle's S=28
+    digest (LCC and TDS results are partition-independent; the fixture's result files are
+    written with one rank, so no rank attribution differs)."""
+    fixture = os.path.join(pmtest.ROOT, "tests", "golden", "rmat_s28_p8_tree.json")
+    import json
+    fx = json.load(open(fixture))
+    _graphs.clear()
+    out = tmp_path / "shards"
+    sg = pm.run_rmat_local_shards(28, 8, TREE, nshards, str(out), max_iterations=64, nranks=1,
+                                  hub_threshold=pm.DEFAULT_HUB_THRESHOLD)
+    print(f"S=28 sharded x{nshards}: {sg['hubs']} delegates at -d {pm.DEFAULT_HUB_THRESHOLD}, {sg}")
+    assert sg["hubs"] > 0  # hubs exist at C4's threshold: the delegate split runs
+    diffs = pmtest.digest_diffs(fx["digest"], pmtest.result_digest(str(out), 1))
+    for k_g, k_o in (("iterations", "iterations"), ("terminated", "terminated"), ("final_vertices", "final_vertices"),
+                     ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"),
+                     ("tds_edges", "tds_edges"), ("walks", "paths")):
+        if sg[k_g] != fx["stats"][k_o]:
+            diffs.append(f"{k_g}: gpu {sg[k_g]} != oracle {fx['stats'][k_o]}")
+    assert diffs == [], diffs[:5]

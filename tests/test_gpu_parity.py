@@ -202,3 +202,32 @@ def test_cli_end_to_end_matches_oracle(tmp_path):
     ora = tmp_path / "oracle"
     oracle.run(g.off, g.col, PATTERNS["cycle"], str(ora), labels=labels, nranks=4)
     assert pmtest.compare_result_dirs(str(ora), str(out), 4) == []
+
+
+def test_search_start_clears_tpub():
+    """Every nonzero T_pub entry (either ping-pong buffer) sits at an slist entry after a search, and the next
+    search's start -- the deferred clear batched into its first launch -- leaves both buffers all zero, after
+    full, capped and step-API searches alike (the superstep-0 records path writes nothing for a row the first
+    later superstep removes, so it relies on clean buffers)."""
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    m = pm.PatternMatcher(g, PATTERNS["cycle"], labels=labels)
+    try:
+        for cap in (0, 1, 0):
+            m.run_beta("", max_iterations=cap)
+            c0, c1, outside = m.tpub_census()
+            assert c0 + c1 > 0 and outside == 0, (c0, c1, outside)
+            assert m.tpub_census(deferred_reset=True) == (0, 0, 0)
+        m.reset()
+        m.lcc_bsp(True)
+        m.token_passing(0)
+        m.post_token_passing(0)
+        assert m.tpub_census()[2] == 0
+        assert m.tpub_census(deferred_reset=True) == (0, 0, 0)
+        # and the search after it still matches the oracle
+        so = oracle.run(g.off, g.col, PATTERNS["cycle"], None, labels=labels)
+        sg = m.run_beta("")
+        assert (sg["final_vertices"], sg["final_edges"], sg["walks"]) == (so["final_vertices"], so["final_edges"],
+                                                                         so["paths"])
+    finally:
+        m.close()

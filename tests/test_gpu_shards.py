@@ -19,6 +19,9 @@ pytestmark = pytest.mark.gpu
 PATTERNS = {
     "tree": os.path.join(pmtest.ROOT, "patterns", "rmat_log2_tree_pattern"),
     "cycle": os.path.join(pmtest.ROOT, "patterns", "rmat_log2_cycle4_pattern"),
+    # one label on three template vertices: the wide code exchange (64-bit records, T_pub by position)
+    "wstar": os.path.join(pmtest.ROOT, "patterns", "wide_star_pattern"),      # diameter 2
+    "wspider": os.path.join(pmtest.ROOT, "patterns", "wide_spider_pattern"),  # diameter 3
 }
 
 # (pattern, scale, P_gen, label alphabet or None, result-file ranks, shards)
@@ -76,6 +79,41 @@ def test_sharded_delegates_match_oracle(pat, scale, p_gen, thr, nranks, shards, 
     assert int((np.diff(g.off) >= thr).sum()) > 0  # some delegates
     so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, shards, None, nranks, hub_threshold=thr)
     assert diffs == []
+    _check(so, sg)
+
+
+# labels on three template vertices (xcode_wide): diameters 2 and 3, two and three shards, with delegates
+WIDE_CASES = [
+    ("wstar", 12, 4, 6, 64, 1, 2),
+    ("wstar", 14, 4, 8, 100, 2, 3),
+    ("wspider", 12, 4, 6, 48, 1, 3),
+    ("wspider", 14, 4, 8, 100, 3, 2),
+    ("wstar", 13, 4, 6, pm.DEFAULT_HUB_THRESHOLD, 1, 1),
+]
+
+
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,thr,nranks,shards", WIDE_CASES)
+def test_sharded_wide_codes_match_oracle(pat, scale, p_gen, alphabet, thr, nranks, shards, tmp_path):
+    g = pm.rmat_graph(scale, p_gen)
+    labels = pmtest.hash_labels(g.n, alphabet)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, shards, labels, nranks, hub_threshold=thr)
+    assert diffs == []
+    _check(so, sg)
+    assert so["final_vertices"] > 0 and so["nlcc_edges"] > 0
+    if thr < pm.DEFAULT_HUB_THRESHOLD:
+        assert sg["hubs"] > 0
+
+
+@pytest.mark.parametrize("pat", ["wstar", "wspider"])
+def test_wide_codes_one_gpu_match_oracle(pat, tmp_path):
+    g = pm.rmat_graph(13, 4)
+    labels = pmtest.hash_labels(g.n, 6)
+    so = oracle.run(g.off, g.col, PATTERNS[pat], str(tmp_path / "oracle"), labels=labels)
+    m = pm.PatternMatcher(pm.Graph(g.off, g.col, True), PATTERNS[pat], labels=labels)
+    sg = m.run_beta(str(tmp_path / "gpu"), 100)
+    assert m.tpub_census()[2] == 0
+    m.close()
+    assert pmtest.compare_result_dirs(str(tmp_path / "oracle"), str(tmp_path / "gpu"), 1) == []
     _check(so, sg)
 
 

@@ -1,10 +1,14 @@
 #!/bin/bash
-# GPU box: selected -m gpu tests (args: tag, pytest paths / -k ...), log under gpurun_out/.
+# GPU box: pytest over the given test paths / node ids (default: the whole -m gpu suite), log under gpurun_out/.
+# usage: TAG=x [LIMIT=seconds] tools/gpu_tests.sh [pytest args ...]
 set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-TAG=$1; shift
-timeout -k 10 1100 python3 -u -m pytest -m gpu -v --timeout 300 --timeout-method thread "$@" \
-    > gpurun_out/pytest_gpu_${TAG}.log 2>&1
+TAG=${TAG:-run}
+LIMIT=${LIMIT:-1100}
+[ $# -eq 0 ] && set -- tests
+timeout -k 10 "$LIMIT" python3 -u -m pytest "$@" -m gpu -x -v -s --timeout 600 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?
-tail -5 gpurun_out/pytest_gpu_${TAG}.log
+grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/pytest_gpu_$TAG.log | tail -40
 exit $rc
