@@ -51,6 +51,26 @@ def edges_of(s):
     return s["lcc_edges"] + s["nlcc_edges"] + s["tds_edges"]
 
 
+def host_cpu_share():
+    """Host CPUs this process may use: the affinity mask, bounded by the cgroup CPU quota and by the pool's
+    OMP_NUM_THREADS (a one-GPU lease is given 16 of the host's CPUs); every bound is reported."""
+    info = {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    share = info["affinity"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+            share = min(share, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        info["omp_num_threads"] = int(omp)
+        share = min(share, int(omp))
+    info["threads_used"] = share
+    return share, info
+
+
 def main():
     import faulthandler
     faulthandler.enable()  # a fatal signal prints the Python stack
@@ -74,6 +94,8 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="take the sharded (RCCL) path even at N=1 (rehearsal of the multi-GPU code on one GPU)")
     ap.add_argument("--pmc", default=None, help="PMC summary of k_lcc_first (default: the newest profiles/r*_pmc_lcc_first.json)")
+    ap.add_argument("--c3", choices=["auto", "off"], default="auto",
+                    help="also time BASELINE config C3 (S=26, P_gen=4, 4-cycle: the token-passing stress) at N=1")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -232,12 +254,46 @@ def main():
         roofline.update({"scanned_entries": real, "loaded_slots": slots,
                          "padded_slot_ratio": round(slots / max(real, 1), 4), "scanned_rows": rows, "tiles": tiles})
 
+    # a single run_pattern_matching_beta invocation: the layout (labels -> label-major CSR + tiling) and the
+    # first search, with and without the graph's generation
+    if "label_major_layout_and_tiling" in setup and setup.get("first_search_s"):
+        fe = edges_of(first)
+        setup["single_invocation_edges_per_s"] = round(
+            fe / (setup["label_major_layout_and_tiling"] + setup["first_search_s"]), 1)
+        setup["single_invocation_edges_per_s_incl_generation"] = round(fe / setup["first_search_including_setup_s"], 1)
+
+    # BASELINE.json configs[2] (C3): S=26, P_gen=4, the 4-cycle pattern -- the NLCC token-passing stress
+    c3 = None
+    if args.c3 == "auto" and world == 1 and not sharded:
+        cyc = os.path.join(ROOT, "patterns", "rmat_log2_cycle4_pattern")
+        m3, g3 = pm.rmat_matcher(26, 4, cyc, device=0)
+        f3 = m3.run_beta("", args.max_iterations)
+        for _ in range(2):
+            m3.run_beta("", args.max_iterations)
+        t3 = time.perf_counter()
+        r3 = [m3.run_beta("", args.max_iterations) for _ in range(5)]
+        e3 = (time.perf_counter() - t3) / 5
+        m3.close()
+        c3 = {"workload": "R-MAT scale-26 (P_gen=4) + rmat_log2_cycle4_pattern (4 cycle-check lines + TDS line), one GPU",
+              "value": round(edges_of(r3[-1]) / e3, 1), "unit": "edges/s", "ms_per_step": round(e3 * 1e3, 3),
+              "steps": 5, "edges_per_step": edges_of(r3[-1]), "lcc_edges": r3[-1]["lcc_edges"],
+              "nlcc_edges": r3[-1]["nlcc_edges"], "tds_edges": r3[-1]["tds_edges"], "walks": r3[-1]["walks"],
+              "iterations": r3[-1]["iterations"],
+              "nlcc_ms_per_step": round(sum(r["nlcc_seconds"] for r in r3) / 5 * 1e3, 3),
+              "nlcc_share": round(sum(r["nlcc_seconds"] for r in r3) / 5 / e3, 4),
+              "nlcc_edges_per_s": round((r3[-1]["nlcc_edges"] + r3[-1]["tds_edges"]) /
+                                        max(sum(r["nlcc_seconds"] for r in r3) / 5, 1e-9), 1),
+              "first_search_s": round(f3["seconds"], 4), "generate_rmat_gpu_s": round(g3, 3),
+              "parity": "tests/test_gpu_configs.py::test_c3_s26_cycle4 (every result file vs the oracle)"}
+        log(f"C3 S=26 4-cycle: {c3['ms_per_step']} ms/step, {c3['value'] / 1e9:.2f} G edges/s, "
+            f"NLC lines {c3['nlcc_ms_per_step']} ms ({c3['nlcc_share']:.0%})")
+
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         cscale = min(args.scale, args.cpu_scale)
-        threads = oracle.default_threads()
+        threads, cpu_info = host_cpu_share()
         t0 = time.time()
         gc = pm.rmat_graph(cscale, args.p_gen, device=0)
         runs = [oracle.run(gc.off, gc.col, pattern_dir, None, max_iterations=args.max_iterations, threads=threads)
@@ -264,7 +320,7 @@ def main():
                          f"sample of the headline search) by oracle/pm_oracle.cpp on {threads} host threads "
                          f"(rank-partitioned BSP), median of 3 runs ({', '.join(f'{x:.2f}' for x in secs)} s; "
                          f"{time.time() - t0:.1f}s incl. setup)",
-               "edges": oe,
+               "edges": oe, "host_cpus": cpu_info,
                "gpu_value_same_sample": round(ge / gsec, 1),
                "gpu_over_cpu_same_sample": round(ge / gsec / (oe / secs[1]), 1)}
         # BASELINE.json configs[0] (C1): R-MAT S=21, P_gen=4, the reference's CPU-runnable case with 4 MPI
@@ -323,6 +379,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "fixture": fixture,
+        "c3_config": c3,
         # one-time work outside the timed region (the reference's graph load + label init analogue)
         "setup_s": setup,
     }

@@ -83,6 +83,7 @@ class RunStats(ctypes.Structure):
         ("lcc_first_kernel_ms", ctypes.c_double),
         ("lcc_first_bytes", c_u64),
         ("tds_chunks", c_u64),
+        ("nlcc_seconds", ctypes.c_double),
     ]
 
     def as_dict(self):

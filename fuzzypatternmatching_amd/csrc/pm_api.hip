@@ -281,6 +281,8 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
   if (const char* e = std::getenv("PM_DIAG_STEP")) c->diag_step = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
+  c->any_sv = any_sv;
+  if (const char* e = std::getenv("PM_SPLIT_LINES")) c->split_min = std::strtoull(e, nullptr, 10);
   // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
   // asymmetric M then aborts the search: tests use it to find such inputs)
   if (const char* e = std::getenv("PM_FORCE_PULL")) c->force_pull = std::string(e) == "1" && c->symmetric;
@@ -326,7 +328,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
                   c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
-                  c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart,
+                  c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -697,6 +699,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
                                                                std::vector<std::vector<std::string>>(c.nranks));
   pm_run_stats s{};
   c.device_seconds = 0.0;
+  c.lines_seconds = 0.0;
   // pattern_time_start (beta.cpp:539): the reset above is only enqueued; the
   // search's kernels follow it on the stream without a host round trip
   const auto t_pattern = std::chrono::steady_clock::now();
@@ -837,6 +840,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           auto t3 = tick();
           count_state(c, vc, ec);
           ph_count += since(t3);
+          c.lines_seconds += since(t1);
         }
         if (pl >= 4) {
           s.tds_edges += tr.edges;
@@ -887,6 +891,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   s.iterations = itr;
   s.terminated = terminated ? 1 : 0;
   s.hubs = static_cast<uint32_t>(c.hubs_host.size());
+  s.nlcc_seconds = c.lines_seconds;
   s.seconds = secs;
   s.device_seconds = c.device_seconds;
   s.lcc_first_kernel_ms = c.lcc_first_ms;

@@ -220,6 +220,7 @@ struct LineStats {
   unsigned long long wn[20];    // TDS walks per position (1..C+1)
   unsigned long long wbase[20]; // TDS: slot offset of each position's walks
   unsigned int overflow, single;  // single: finished by block 0 alone
+  unsigned int split, pad_;       // split: run over this shard's own sources only, post-processing deferred
   unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
   unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)
@@ -432,6 +433,14 @@ struct Ctx {
   unsigned line_grid = 0;         // blocks of a full-chip line launch (one per CU)
   uint64_t live_hint = ~0ull;     // S members on this context after the last LCC call (line grid size)
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
+  bool any_sv = false;            // some line has selected_vertices (token-source sets span lines)
+  // sharded search on the replica: an NLC line whose census (sources on the replica) reaches split_min runs
+  // split by owner -- every shard passes the tokens of the sources it owns (hub ordinal % nshards, else
+  // id % nshards) -- and the shards then exchange the line's effects (pm_shard.hip split_line_finish);
+  // smaller lines run replicated (every shard all sources, no exchange).  0: never split.  PM_SPLIT_LINES.
+  uint64_t split_min = 16384;
+  unsigned long long* d_xsplit = nullptr;  // a split line's flagged M entries (replica entry indices), then
+  uint64_t xsplit_cap = 0;                 // the shard's cleared sources (positions) of its post-processing
   bool force_pull = false;        // PM_FORCE_PULL=1 (diagnostics): pull-form LCC in every call
 
   // token-source sets (vertex_token_source_set, nem_1.hpp:131-139, 270-285) of
@@ -452,6 +461,7 @@ struct Ctx {
   float lcc_first_ms = 0.f;
   uint64_t lcc_first_bytes = 0;
   double device_seconds = 0.0;
+  double lines_seconds = 0.0;     // NLC lines of the current search (pm_run_stats::nlcc_seconds)
   double layout_seconds = 0.0;    // last label-major layout + tiling build (one-time setup)
 
   std::string err;
@@ -515,6 +525,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line);
 struct FusedLineOut {
   TpResult tr;
   uint32_t deleted = 0;
+  bool split = false;           // ran split over the shards (stats, effects and walks combined over them)
   std::vector<uint64_t> rm_v, rm_e;
   std::vector<uint32_t> walks;  // kept TDS walks (positions), when requested
   uint32_t stride = 0;
@@ -548,6 +559,12 @@ uint64_t* pinned(Ctx& c, size_t words);  // pinned host staging (pm_api.hip)
 void debug_point(Ctx& c, const char* where);
 
 // Shard exchanges (pm_shard.hip); no-ops without a communicator.
+// After a split NLC line (its tokens passed for this shard's own sources, terminal effects local): agrees on
+// overflow over the shards (false: every shard reruns the line on the exact, replicated path), else runs this
+// shard's post-processing, exchanges the cleared sources and the flagged M entries (every replica applies
+// all of them), sums the stats, and gathers the kept walks (want_walks).  kept: this shard's kept walk slots.
+bool split_line_finish(Ctx& c, size_t pl, const LineStats& st, const uint32_t* kept_dev, bool want_walks,
+                       FusedLineOut& out);
 // after superstep 0 (sharded, delegates): the shares' TN / counts all-gathered and OR-ed / summed, the
 // shares' M entries sent to the controller (all-to-all), the controller verifies (slot: ss0 counters)
 void shard_hub_combine(Ctx& c, uint64_t* d_slot);

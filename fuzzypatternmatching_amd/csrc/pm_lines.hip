@@ -112,6 +112,14 @@ struct LineKernelArgs {
   uint32_t* act;   // S members at launch start (slist entries with T_pub != 0), built by k_lines
   unsigned long long* nact;
   uint64_t small_line;  // single-block threshold (kSmallLine)
+  // sharded replica: lines whose census reaches split_min run split by owner (so: the shard owner rule)
+  OwnerArgs so;
+  uint32_t shard;
+  uint64_t split_min;
+  int split;                      // the current line runs split: own sources, post-processing deferred
+  unsigned long long* xflag;      // split cycle lines: M entries this shard's terminals flagged
+  unsigned long long* nxflag;
+  uint64_t xflag_cap;
 };
 
 __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
@@ -178,7 +186,15 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
       const uint64_t mid = (lo + hi) >> 1;
       if (a.perm[a.mcol[mid] & kPosMask] < pid) lo = mid + 1; else hi = mid;
     }
-    if (lo < e && (a.mcol[lo] & kPosMask) == p && (a.mcol[lo] & kAlive)) a.mcol[lo] |= kFlag;
+    if (lo < e && (a.mcol[lo] & kPosMask) == p && (a.mcol[lo] & kAlive)) {
+      if (!a.split) {
+        a.mcol[lo] |= kFlag;
+      } else if (!(atomicOr(&a.mcol[lo], kFlag) & kFlag)) {  // newly flagged: the other replicas get it too
+        const unsigned long long at = atomicAdd(a.nxflag, 1ull);
+        if (at < a.xflag_cap) a.xflag[at] = lo;
+        else atomicOr(&a.st->overflow, 1u);
+      }
+    }
   }
 }
 
@@ -323,6 +339,7 @@ __device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t 
     const uint16_t T = a.tpub[s];
     ok = T && pos_ok(T, 0, *a.la);
     if (ok && !tds && !a.la->VC && !((T >> a.la->ilast) & 1u)) ok = false;
+    if (ok && a.split && owner_of(s, a.so) != a.shard) ok = false;  // a split line: this shard's sources
   }
   const uint64_t pos = wave_reserve(&a.st->nsrc, ok ? 1u : 0u);
   if (ok) {
@@ -530,7 +547,7 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
   if (ld_dev(&st->overflow)) return;  // the host clears the table and reruns the line
-  line_post(a, g, s_hist);
+  if (!a.split) line_post(a, g, s_hist);  // (split: after the shards agreed on overflow, split_line_finish)
   // hash cleanup: no insert happens after the last position
   const uint64_t nf = ld_dev(&st->ftotal);
   for (uint64_t i = g.tid; i < nf; i += g.nth) {
@@ -668,7 +685,7 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
   phase_sync(a, single);
-  line_post(a, g, s_hist);
+  if (!a.split) line_post(a, g, s_hist);
 }
 
 __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long long* s_hist, WaveRows& wr) {
@@ -778,13 +795,18 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     b.la = &d.la;
     b.i0 = d.i0;
     b.st = a.st + pl;
+    // census on the replica = the line's sources over all shards (an upper bound after an earlier line of
+    // the launch changed the state; identical on every shard, so every shard decides alike)
+    b.split = a.split_min && a.so.nranks > 1 && ld_dev(&a.st[pl].census) >= a.split_min ? 1 : 0;
+    if (b.split && blockIdx.x == 0 && threadIdx.x == 0) b.st->split = 1;
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[0] = __builtin_amdgcn_s_memrealtime();
     if (d.tds) tds_line(b, s_hist, wr);
     else path_line(b, s_hist, wr);
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[2] = __builtin_amdgcn_s_memrealtime();
     tree_barrier(a.gbar);
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[3] = __builtin_amdgcn_s_memrealtime();
-    const bool stop = ld_dev(&b.st->overflow) || (d.il && ld_dev(&b.st->deleted));
+    // a split line ends the launch: the shards exchange its effects before the next line selects sources
+    const bool stop = ld_dev(&b.st->overflow) || (d.il && ld_dev(&b.st->deleted)) || b.split;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.done = static_cast<unsigned>(pl + 1);
     if (stop) break;
   }
@@ -911,6 +933,25 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   a.lines = c.d_ldesc;
   a.small_line = kSmallLine;
   if (const char* e = std::getenv("PM_SMALL_LINE")) a.small_line = std::strtoull(e, nullptr, 10);
+  // split lines (sharded replica): owner rule of the shards, the flag list
+  a.so.hubs = c.d_hubs;
+  a.so.perm = c.d_perm;
+  a.so.nhubs = static_cast<uint32_t>(c.hubs_host.size());
+  a.so.nranks = c.comm ? c.nshards : 1;
+  a.shard = c.shard;
+  a.split_min = c.comm && c.nshards > 1 && c.pattern.lines.size() && !c.any_sv ? c.split_min : 0;
+  if (a.split_min) {
+    const uint64_t want = m_cap(c) + c.nS_host + 2;
+    if (c.xsplit_cap < want) {
+      if (c.d_xsplit) (void)hipFree(c.d_xsplit);
+      c.d_xsplit = nullptr;
+      PM_HIP_CHECK(hipMalloc(&c.d_xsplit, want * sizeof(unsigned long long)));
+      c.xsplit_cap = want;
+    }
+    a.xflag = c.d_xsplit;
+    a.xflag_cap = m_cap(c);
+    a.nxflag = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 6);  // zeroed with d_done
+  }
   a.pl_begin = static_cast<int>(pl0);
   a.pl_end = static_cast<int>(nl);
   a.done = d_done;
@@ -987,6 +1028,11 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
               hs.size() * sizeof(LineStats));
   const unsigned done = static_cast<unsigned>(pin[0] & 0xFFFFFFFFull);
   const unsigned long long kept_slots = pin[1];
+  {  // device time of the launch: its start stamp (kst[0], control word 4) to the last processed line's end
+    unsigned long long end = pin[5];
+    for (unsigned j = 0; j + pl0 < done; ++j) end = std::max(end, hs[j].tstamp[3]);
+    if (pin[4] && end > pin[4]) c.lines_seconds += (end - pin[4]) * 1e-8;  // s_memrealtime: 100 MHz
+  }
   std::vector<uint32_t> kept;
   if (want_walks && kept_slots) {
     kept.resize(kept_slots);
@@ -1011,6 +1057,24 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     const LineStats& st = hs[j];
     const size_t pl = pl0 + j;
     c.nsources = st.nsrc;
+    if (st.split) {  // (the launch's last line) effects, stats and walks combined over the shards
+      FusedLineOut out;
+      out.stride = static_cast<uint32_t>(c.pattern.lines[pl].cycle_length + 2);
+      if (!split_line_finish(c, pl, st, kept_dev, want_walks, out)) {  // some shard overflowed: exact path
+        overflow = true;
+        if (pl < 4) {
+          const uint64_t grow = c.hcap * 4;
+          PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+          PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+          ensure_hash(c, grow);
+        }
+        break;
+      }
+      c.last_acked = out.tr.acked;
+      outs.push_back(std::move(out));
+      ++completed;
+      break;
+    }
     if (st.overflow) {
       overflow = true;
       if (pl < 4) {

@@ -784,4 +784,156 @@ void shard_replicate(Ctx& c) {
   c.replicated = true;
 }
 
+// ---------------------------------------------------------------------------
+// Split NLC lines (sharded replica).  A line with many sources runs split by owner: each shard passes the
+// tokens of the sources it owns (the reference's visitors of a source live on its owner rank and its tokens
+// travel to the owners of the walk's vertices, nem_1.hpp:832-851 / tds_batch_1.hpp:1181; here every shard
+// reads the whole replica, so tokens need no exchange).  The line's effects are then combined: the sources
+// whose T_pub bit I[0] this shard's post-processing cleared (beta.cpp:956-1000) and the M entries its cycle
+// terminals flagged (nem_1.hpp:764-770) are all-gathered and applied to every replica.
+
+// Post-processing of a split line over this shard's own sources (line_post's rule); out: [0] acked,
+// [1] deleted, [2] cleared sources (their positions in dels), [3, 3 + 2P) vertices | edges per rank leaving S.
+__global__ void k_split_post(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint8_t* __restrict__ tsm,
+                             uint16_t* __restrict__ tpub, int i0, const uint32_t* __restrict__ malive, OwnerArgs oa,
+                             unsigned long long* __restrict__ dels, unsigned long long* __restrict__ out) {
+  const uint32_t P = oa.nranks <= 1 ? 1 : oa.nranks;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t s = sources[i];
+    if (tsm[s] == 2) {
+      atomicAdd(&out[0], 1ull);
+      continue;
+    }
+    uint16_t T = tpub[s];
+    if (!T) continue;
+    atomicAdd(&out[1], 1ull);
+    if (!((T >> i0) & 1u)) continue;
+    T &= static_cast<uint16_t>(~(1u << i0));
+    tpub[s] = T;
+    dels[atomicAdd(&out[2], 1ull)] = s;
+    if (!T) {  // vertex_active = false, erased from the state map
+      const uint32_t r = owner_of(s, oa);
+      atomicAdd(&out[3 + r], 1ull);
+      atomicAdd(&out[3 + P + r], static_cast<unsigned long long>(malive[s]));
+    }
+  }
+}
+
+// The other shards' effects on this replica: lists of block g at g * stride (nf[g] flagged entries, then nd[g]
+// cleared sources from offset fmax).
+__global__ void k_split_apply(const unsigned long long* __restrict__ all, uint64_t stride, uint64_t fmax, uint32_t G,
+                              uint32_t me, XCounts x, uint16_t* __restrict__ tpub, int i0, uint32_t* __restrict__ mcol) {
+  const uint64_t total = uint64_t(G) * stride;
+  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t g = static_cast<uint32_t>(j / stride);
+    const uint64_t k = j % stride;
+    if (g == me) continue;
+    if (k < fmax) {
+      if (k < x.n[g]) atomicOr(&mcol[all[j]], kFlag);
+    } else if (k - fmax < x.m[g]) {
+      const uint32_t p = static_cast<uint32_t>(all[j]);
+      tpub[p] &= static_cast<uint16_t>(~(1u << i0));
+    }
+  }
+}
+
+// Host vector of every shard (G x v.size(), shard order): one all-gather, one host sync.
+static std::vector<uint64_t> shard_allgather_host(Ctx& c, const std::vector<uint64_t>& v) {
+  const uint32_t G = c.nshards;
+  auto* d = grow<uint64_t>(c.d_xsend, c.xsend_cap, v.size() * sizeof(uint64_t));
+  auto* r = grow<uint64_t>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * v.size() * sizeof(uint64_t));
+  PM_HIP_CHECK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  c.comm->allgather(d, r, v.size() * sizeof(uint64_t), c.stream);
+  std::vector<uint64_t> out(uint64_t(G) * v.size());
+  PM_HIP_CHECK(hipMemcpyAsync(out.data(), r, out.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  return out;
+}
+
+bool split_line_finish(Ctx& c, size_t pl, const LineStats& st, const uint32_t* kept_dev, bool want_walks,
+                       FusedLineOut& out) {
+  if (!c.comm) throw std::runtime_error("internal: split NLC line without a communicator");
+  const uint32_t G = c.nshards, P = c.nranks <= 1 ? 1 : c.nranks;
+  const NlcLine& line = c.pattern.lines[pl];
+  const uint32_t stride = out.stride;
+  // 1. overflow anywhere: every shard reruns the line on the exact path (no post-processing ran yet; the
+  //    flags a finished shard set are among those the rerun sets everywhere)
+  const unsigned long long nflag = c.h_pin_lines[3];  // the flag-list counter (control words 6-7 of the launch)
+  const std::vector<uint64_t> a =
+      shard_allgather_host(c, {st.overflow ? 1ull : 0ull, nflag, st.nsrc, st.trav, st.tokens, st.walks});
+  for (uint32_t g = 0; g < G; ++g)
+    if (a[6 * g]) return false;
+  // 2. this shard's post-processing
+  unsigned long long* dels = c.d_xsplit + m_cap(c);
+  ensure_xcnt(c);
+  auto* d_out = reinterpret_cast<unsigned long long*>(c.d_xcnt);  // 3 + 2P <= 64 + 4 * 64 words
+  PM_HIP_CHECK(hipMemsetAsync(d_out, 0, (3 + 2 * P) * sizeof(uint64_t), c.stream));
+  OwnerArgs oa{c.d_hubs, c.d_perm, static_cast<uint32_t>(c.hubs_host.size()), c.nranks};
+  const int i0 = static_cast<int>(line.indices[0]);
+  if (st.nsrc)
+    hipLaunchKernelGGL(k_split_post, dim3(xgrid(st.nsrc)), dim3(kXBlock), 0, c.stream, c.d_sources, uint64_t(st.nsrc),
+                       c.d_tsm, c.d_tpub[c.cur], i0, c.d_malive, oa, dels, d_out);
+  PM_HIP_CHECK(hipGetLastError());
+  std::vector<uint64_t> loc(3 + 2 * P);
+  PM_HIP_CHECK(hipMemcpyAsync(loc.data(), d_out, loc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  // 3. every shard's post counts; then the lists, padded to the largest (flags | cleared sources)
+  const std::vector<uint64_t> b = shard_allgather_host(c, loc);
+  const size_t W = loc.size();
+  uint64_t fmax = 0, dmax = 0;
+  XCounts x{};
+  out.rm_v.assign(c.nranks, 0);
+  out.rm_e.assign(c.nranks, 0);
+  uint64_t acked = 0, deleted = 0;
+  for (uint32_t g = 0; g < G; ++g) {
+    x.n[g] = a[6 * g + 1];
+    x.m[g] = b[W * g + 2];
+    fmax = std::max(fmax, x.n[g]);
+    dmax = std::max(dmax, x.m[g]);
+    acked += b[W * g];
+    deleted += b[W * g + 1];
+    for (uint32_t r = 0; r < c.nranks; ++r) {
+      out.rm_v[r] += b[W * g + 3 + r];
+      out.rm_e[r] += b[W * g + 3 + P + r];
+    }
+    out.tr.sources += a[6 * g + 2];
+    out.tr.edges += a[6 * g + 3];
+    out.tr.tokens += a[6 * g + 4];
+    out.tr.walks += a[6 * g + 5];
+  }
+  out.tr.acked = acked;
+  out.deleted = deleted ? 1u : 0u;
+  out.split = true;
+  const uint64_t xs = fmax + dmax;
+  if (xs) {
+    auto* send = grow<unsigned long long>(c.d_xsend, c.xsend_cap, xs * 8);
+    auto* recv = grow<unsigned long long>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * xs * 8);
+    if (nflag) PM_HIP_CHECK(hipMemcpyAsync(send, c.d_xsplit, nflag * 8, hipMemcpyDeviceToDevice, c.stream));
+    if (loc[2]) PM_HIP_CHECK(hipMemcpyAsync(send + fmax, dels, loc[2] * 8, hipMemcpyDeviceToDevice, c.stream));
+    c.comm->allgather(send, recv, xs * 8, c.stream);
+    hipLaunchKernelGGL(k_split_apply, dim3(xgrid(uint64_t(G) * xs)), dim3(kXBlock), 0, c.stream, recv, xs, fmax, G,
+                       c.shard, x, c.d_tpub[c.cur], i0, m_col(c));
+    PM_HIP_CHECK(hipGetLastError());
+  }
+  // 4. the kept walks of every shard (shard order), for the result files
+  if (want_walks && pl >= 4) {
+    uint64_t wmax = 0;
+    for (uint32_t g = 0; g < G; ++g) wmax = std::max<uint64_t>(wmax, a[6 * g + 5] * stride);
+    if (wmax) {
+      auto* send = grow<uint32_t>(c.d_xsend, c.xsend_cap, wmax * 4);
+      auto* recv = grow<uint32_t>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * wmax * 4);
+      if (st.walks)
+        PM_HIP_CHECK(hipMemcpyAsync(send, kept_dev + st.wbase[0], st.walks * stride * 4, hipMemcpyDeviceToDevice,
+                                    c.stream));
+      c.comm->allgather(send, recv, wmax * 4, c.stream);
+      std::vector<uint32_t> all(uint64_t(G) * wmax);
+      PM_HIP_CHECK(hipMemcpyAsync(all.data(), recv, all.size() * 4, hipMemcpyDeviceToHost, c.stream));
+      PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+      for (uint32_t g = 0; g < G; ++g)
+        out.walks.insert(out.walks.end(), all.begin() + g * wmax, all.begin() + g * wmax + a[6 * g + 5] * stride);
+    }
+  }
+  return true;
+}
+
 }  // namespace pm

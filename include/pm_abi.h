@@ -105,6 +105,8 @@ typedef struct pm_run_stats {
   uint64_t lcc_first_bytes;     /* algorithmic bytes of that kernel                 */
   uint64_t tds_chunks;          /* chunk launches of exact-path TDS enumerations (0: every TDS line ran in
                                    the fused kernel; see run_tds_line, PM_TDS_CAP)    */
+  double nlcc_seconds;          /* NLC lines of the search: device time of the fused line launches (first
+                                   block start to the last line's end) + host time of exact-path lines */
 } pm_run_stats;
 
 /* One shard (rank) of a sharded search: the rows of ids v % nshards == shard. */

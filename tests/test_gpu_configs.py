@@ -6,12 +6,12 @@ result digest.
 C2: S=24, P_gen=4, tree, degree labels, 1 and 4 ranks of output attribution.
 C3: S=26, P_gen=4, 4-cycle pattern (NLCC token-passing stress).
 C5: ingested text edge list (-u 1) + explicit -v label files (hash32(v) % 64)
-    through the CLIs at S=18 (text size), and hash labels through the library at
-    S=22.
+    through the CLIs at S=18 (text size), hash labels through the library at
+    S=22, and at size (S=27, alphabet 256, GPU ingest, chunked TDS, oracle).
 C4': S=28, P_gen=8, tree on ONE GPU against tests/golden/rmat_s28_p8_tree.json
     (the oracle needs ~100 GB of host memory there, so its result was made once:
-    tests/golden/make_rmat_fixture.py); the sharding of C4 is covered by
-    tests/test_gpu_shards.py.  C5 at S=27: tools/c5_at_size.py.
+    tests/golden/make_rmat_fixture.py), and C4's sharded path at full size (two
+    in-process shards, delegates at -d 1048576) against the same fixture.
 """
 import os
 import subprocess
@@ -105,6 +105,79 @@ def test_c5_ingested_edge_list_with_label_files(tmp_path):
     ora = tmp_path / "oracle"
     oracle.run(g.off, g.col, CYCLE, str(ora), labels=labels, nranks=nranks, threads=oracle.default_threads())
     assert pmtest.compare_result_dirs(str(ora), str(out), nranks) == []
+
+
+C5_ALPHABET = 256
+
+
+def test_c5_s27_ingested_label_files(tmp_path, monkeypatch):
+    """BASELINE config C5 at size on one GPU: the S=27 R-MAT stream (P_gen=8) as 8 text edge-list files
+    (~40 GB, written from the GPU generator's stream) ingested on the GPU with -u 1 (ingest_edge_list.cpp:164-240,
+    parallel_edge_list_reader.hpp:242-266), explicit -v label files with hash32(v ^ 5) % 256 parsed on the GPU
+    (vertex_data_db.hpp:137-257), and the 4-cycle pattern, whose template-driven enumeration runs in chunks
+    (tds_batch_1.hpp:1139-1253).  Checks: the ingested graph's result directory equals the GPU-generated
+    graph's; the result does not depend on the TDS chunk cap; both equal the oracle's on the host CSR.
+    (An alphabet of 8 or 64 letters makes the 4-cycle enumeration ~10^13 edges at S=27 -- it grows ~6x per
+    scale from the oracle's S=20-22 counts -- for the reference as for this path; 256 letters keep it
+    tractable: tools/c5_at_size.py, DESIGN.md.)"""
+    import ctypes
+    import shutil
+    import tempfile
+    from fuzzypatternmatching_amd import _abi
+    scale, p_gen, nranks = 27, 8, 8
+    lib = _abi.load()
+    n = 1 << scale
+    shm = shutil.disk_usage("/dev/shm").free if os.path.isdir("/dev/shm") else 0
+    work = tempfile.mkdtemp(prefix="c5_", dir="/dev/shm" if shm > 60e9 else str(tmp_path))
+    _graphs.clear()
+    try:
+        nb = ctypes.c_uint64()
+        assert lib.pm_write_rmat_text(scale, p_gen, 0, os.path.join(work, "edges").encode(), ctypes.byref(nb)) == 0
+        files = [os.path.join(work, f"edges.{r}") for r in range(p_gen)]
+        labels = pmtest.hash_labels(n, C5_ALPHABET, salt=5)
+        assert lib.pm_write_label_text(labels.ctypes.data, n, os.path.join(work, "lab").encode(), 4, None) == 0
+        m, ingest_s = pm.edge_list_matcher(files, CYCLE, undirected=True, device=0, nranks=nranks)
+        for f in files:
+            os.remove(f)  # (host memory: the oracle below needs the room)
+        m.labels_from_files(os.path.join(work, "lab"))
+        out_i = tmp_path / "ingested"
+        si = m.run_beta(str(out_i), 64)
+        # chunk-cap invariance: the same search with at most 2^20 walks per level chunk
+        monkeypatch.setenv("PM_TDS_CAP", str(1 << 20))
+        out_c = tmp_path / "ingested_cap"
+        sc = m.run_beta(str(out_c), 64)
+        monkeypatch.delenv("PM_TDS_CAP")
+        m.close()
+        print(f"C5 S={scale}: ingest {ingest_s:.2f}s ({nb.value / ingest_s / 1e9:.1f} GB/s of text), search {si}, "
+              f"capped: {sc['tds_chunks']} chunks")
+        assert si["walks"] > 0 and si["tds_edges"] > 0
+        dig_i = pmtest.result_digest(str(out_i), nranks)
+        assert pmtest.digest_diffs(dig_i, pmtest.result_digest(str(out_c), nranks)) == []
+        assert sc["tds_chunks"] > si["tds_chunks"]
+        # the same graph generated on the GPU, the same labels
+        m2, _ = pm.rmat_matcher(scale, p_gen, CYCLE, device=0, nranks=nranks)
+        m2.set_labels(labels)
+        out_g = tmp_path / "generated"
+        sg = m2.run_beta(str(out_g), 64)
+        m2.close()
+        assert pmtest.digest_diffs(dig_i, pmtest.result_digest(str(out_g), nranks)) == []
+        keys = ("iterations", "terminated", "final_vertices", "final_edges", "lcc_edges", "nlcc_edges", "tds_edges",
+                "walks")
+        assert all(si[k] == sg[k] == sc[k] for k in keys)
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    # the oracle on the host CSR of the same graph (full size)
+    g = pm.rmat_graph(scale, p_gen, device=0)
+    so = oracle.run(g.off, g.col, CYCLE, str(tmp_path / "oracle"), labels=labels, nranks=nranks,
+                    threads=oracle.default_threads())
+    del g
+    diffs = pmtest.compare_result_dirs(str(tmp_path / "oracle"), str(out_i), nranks)
+    for k_g, k_o in (("final_vertices", "final_vertices"), ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"),
+                     ("nlcc_edges", "nlcc_edges"), ("tds_edges", "tds_edges"), ("walks", "paths"),
+                     ("iterations", "iterations")):
+        if si[k_g] != so[k_o]:
+            diffs.append(f"{k_g}: gpu {si[k_g]} != oracle {so[k_o]}")
+    assert diffs == [], diffs[:5]
 
 
 def check_against_fixture(m, fixture, tmp_path, max_iterations=64):

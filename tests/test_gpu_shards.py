@@ -22,6 +22,8 @@ PATTERNS = {
     # one label on three template vertices: the wide code exchange (64-bit records, T_pub by position)
     "wstar": os.path.join(pmtest.ROOT, "patterns", "wide_star_pattern"),      # diameter 2
     "wspider": os.path.join(pmtest.ROOT, "patterns", "wide_spider_pattern"),  # diameter 3
+    # cycle flags that break M's symmetry (push-form later LCC calls, hazards 4, 5, 9)
+    "triangle": os.path.join(pmtest.ROOT, "patterns", "triangle_tail_pattern"),
 }
 
 # (pattern, scale, P_gen, label alphabet or None, result-file ranks, shards)
@@ -115,6 +117,32 @@ def test_wide_codes_one_gpu_match_oracle(pat, tmp_path):
     m.close()
     assert pmtest.compare_result_dirs(str(tmp_path / "oracle"), str(tmp_path / "gpu"), 1) == []
     _check(so, sg)
+
+
+# split NLC lines (PM_SPLIT_LINES=1: every line with a source runs split by owner, its effects exchanged):
+# (pattern, scale, P_gen, alphabet, result ranks, shards, hub threshold, TDS cap forcing the exact-path rerun)
+SPLIT_CASES = [
+    ("cycle", 12, 4, 8, 3, 2, pm.DEFAULT_HUB_THRESHOLD, None),
+    ("cycle", 14, 4, None, 1, 3, pm.DEFAULT_HUB_THRESHOLD, None),
+    ("tree", 16, 4, None, 4, 4, 64, None),
+    ("cycle", 13, 4, 16, 2, 2, 16, None),
+    ("cycle", 12, 4, 8, 2, 3, pm.DEFAULT_HUB_THRESHOLD, 997),
+    ("triangle", 12, 4, 6, 1, 2, pm.DEFAULT_HUB_THRESHOLD, None),
+    ("wspider", 12, 4, 6, 1, 2, pm.DEFAULT_HUB_THRESHOLD, None),
+]
+
+
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards,thr,cap", SPLIT_CASES)
+def test_split_lines_match_oracle(pat, scale, p_gen, alphabet, nranks, shards, thr, cap, tmp_path, monkeypatch):
+    monkeypatch.setenv("PM_SPLIT_LINES", "1")
+    if cap:
+        monkeypatch.setenv("PM_TDS_CAP", str(cap))
+    g = pm.rmat_graph(scale, p_gen)
+    labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS[pat], tmp_path, shards, labels, nranks, hub_threshold=thr)
+    assert diffs == []
+    _check(so, sg)
+    assert so["nlcc_edges"] + so["tds_edges"] > 0
 
 
 def test_sharded_exact_count_lines(tmp_path, monkeypatch):

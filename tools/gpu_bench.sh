@@ -1,14 +1,13 @@
 #!/bin/bash
-# Default bench (C2, S=24) + rocprofv3 kernel-trace/stats of the same command.
-set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# GPU box: the default bench line, then the sharded path at N = 1 (rehearsal), logs under gpurun_out/.
+set -o pipefail
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-TAG=${TAG:-r01}
-timeout -k 10 900 python3 bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log
-rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; tail -4 gpurun_out/bench_$TAG.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-  python3 bench.py --cpu-baseline off > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.log
-rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof_$TAG.json
+TAG=${1:-r04}
+timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || exit $?
+tail -3 gpurun_out/bench_${TAG}.err
+timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29533 bench.py --gpus 1 --sharded --steps 20 --warmup 5 --cpu-baseline off \
+    > gpurun_out/bench_${TAG}_sharded.json 2> gpurun_out/bench_${TAG}_sharded.err
+rc=$?
+tail -3 gpurun_out/bench_${TAG}_sharded.err
 exit $rc

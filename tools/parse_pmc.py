@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc passes of k_lcc_first (tools/gpu_pmc_k1.sh) into a JSON file.
+"""Summarise rocprofv3 --pmc passes of k_lcc_first (tools/gpu_profile.sh) into a JSON file.
 
 usage: parse_pmc.py GPURUN_OUT TAG SCALE P_GEN OUT.json
 

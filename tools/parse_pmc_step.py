@@ -1,4 +1,4 @@
-"""Summarise the rocprofv3 --pmc passes of k_lcc_step (tools/gpu_profile_r03.sh, one bench step per pass) into
+"""Summarise the rocprofv3 --pmc passes of k_lcc_step (tools/gpu_profile.sh, one bench step per pass) into
 a JSON file: the later LCC supersteps of the LAST search in each pass, per dispatch in launch order (the first
 is the superstep right after superstep 0), with HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950,
 MI355X_MICROARCH.md "HBM [CDNA4]") and the dispatch's duration from the pass's own timestamps.
