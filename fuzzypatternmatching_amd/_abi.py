@@ -84,6 +84,7 @@ class RunStats(ctypes.Structure):
         ("lcc_first_bytes", c_u64),
         ("tds_chunks", c_u64),
         ("nlcc_seconds", ctypes.c_double),
+        ("split_lines", c_u64),
     ]
 
     def as_dict(self):

@@ -812,6 +812,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         if (fused) {
           tr = fo.tr;
           deleted = fo.deleted;
+          s.split_lines += fo.split ? 1 : 0;
           vc = cur_vc;
           ec = cur_ec;
           for (uint32_t r = 0; r < c.nranks; ++r) {

@@ -224,6 +224,7 @@ struct LineStats {
   unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
   unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)
+  unsigned long long ptime[20];  // s_memrealtime at the end of each position's phase (diagnostics, PM_PHASE_TIMES)
 };
 
 // One NLC line as seen by the fused line kernel (pm_lines.hip).

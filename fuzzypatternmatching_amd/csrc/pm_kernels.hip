@@ -548,7 +548,9 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
   // M stores in registers, one contributor per lane in list order.  A row's contributors are consecutive
   // lanes; its head lane (first lane of the row) verifies it with the row's TN (OR-ed in the row's LDS half
   // word) and |M| = its run of lanes; the kept lanes (rows that survive) store their entries compacted.
-  if (MODE == 0 && o.rarea && nlist <= static_cast<uint32_t>(kWave) && dcur + nlist <= dend) {
+  // (diagnostic builds: MODE 1024 / 2048 / 4096 drop the register path's code atomics / M stores / records)
+  if ((MODE & ~(1024 | 2048 | 4096)) == 0 && o.rarea && nlist <= static_cast<uint32_t>(kWave) &&
+      dcur + nlist <= dend) {
     const bool valid = static_cast<uint32_t>(lane) < nlist;
     uint32_t x = 0, row = kNoRow;
     if (valid) {
@@ -597,17 +599,18 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
     const uint64_t kb = __builtin_amdgcn_ballot_w64(kept);
     const uint32_t kidx = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(kb >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(kb), 0));
-    if (kept) o.mcol[o.dbase + dcur + kidx] = x | kAlive;
+    if (kept && !(MODE & 2048)) o.mcol[o.dbase + dcur + kidx] = x | kAlive;
     if (T) {
       const uint32_t u = ustart + row;
       const uint32_t code = tpub_code(T, tu);
       const uint32_t ci = cstart + row;
-      atomicOr(&o.tcode[ci >> 4], code << ((ci & 15u) << 1));
+      if (!(MODE & 1024)) atomicOr(&o.tcode[ci >> 4], code << ((ci & 15u) << 1));
       if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + u * 2u) = T;
       const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(sb >> 32),
                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(sb), 0));
       // the head's kidx: the kept entries before its row (consecutive lanes) = its first dense entry
-      o.rarea[rslot] = k1_record(u, T, cnt, static_cast<uint32_t>(dcur + kidx), qb + uint64_t(row) * g);
+      if (!(MODE & 4096))
+        o.rarea[rslot] = k1_record(u, T, cnt, static_cast<uint32_t>(dcur + kidx), qb + uint64_t(row) * g);
     }
     rcur = uniform64(rcur + __builtin_popcountll(sb));
     dcur = uniform64(dcur + __builtin_popcountll(kb));
@@ -1967,6 +1970,10 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 80: hipLaunchKernelGGL(k_lcc_first<80>, PM_K1_ARGS); break;
     case 128: hipLaunchKernelGGL(k_lcc_first<128>, PM_K1_ARGS); break;
     case 512: hipLaunchKernelGGL(k_lcc_first<512>, PM_K1_ARGS); break;
+    case 1024: hipLaunchKernelGGL(k_lcc_first<1024>, PM_K1_ARGS); break;
+    case 2048: hipLaunchKernelGGL(k_lcc_first<2048>, PM_K1_ARGS); break;
+    case 4096: hipLaunchKernelGGL(k_lcc_first<4096>, PM_K1_ARGS); break;
+    case 7168: hipLaunchKernelGGL(k_lcc_first<7168>, PM_K1_ARGS); break;
     case 5: hipLaunchKernelGGL((k_lcc_first<0, false, 5>), PM_K1_ARGS); break;  // 5 waves/SIMD, no spills
 #endif
     default: throw std::runtime_error("unknown superstep-0 kernel variant (ablation variants: lib/libpm_diag.so)");

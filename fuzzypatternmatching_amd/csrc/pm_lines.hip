@@ -543,6 +543,7 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
     }
     lo = hi;
     phase_sync(a, single);
+    if (g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
@@ -638,6 +639,7 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
     }
     in_base = out_base;
     phase_sync(a, single);
+    if (g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
   // every final walk may be kept: its room must exist before any terminal effect
   const uint64_t nw = single ? wr.wn[la.C + 1] : ld_dev(&st->wn[la.C + 1]);
@@ -1051,6 +1053,15 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
       std::fprintf(stderr, "[pm] line %zu: P1 %.1f us, rest %.1f us, end barrier %.1f us (%s, %llu sources)\n",
                    pl0 + j, (st.tstamp[1] - st.tstamp[0]) * 0.01, (st.tstamp[2] - st.tstamp[1]) * 0.01,
                    (st.tstamp[3] - st.tstamp[2]) * 0.01, st.single ? "block 0" : "grid", st.nsrc);
+      std::string pos = "[pm]   positions (walks in, us):";
+      unsigned long long prev = st.tstamp[1];
+      for (int k = 1; k < 20 && st.ptime[k]; ++k) {
+        char b[64];
+        std::snprintf(b, sizeof(b), " %d:(%llu, %.1f)", k, st.wn[k], (st.ptime[k] - prev) * 0.01);
+        pos += b;
+        prev = st.ptime[k];
+      }
+      std::fprintf(stderr, "%s\n", pos.c_str());
     }
   size_t completed = 0;
   for (unsigned j = 0; j + pl0 < done; ++j) {

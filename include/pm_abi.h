@@ -107,6 +107,7 @@ typedef struct pm_run_stats {
                                    the fused kernel; see run_tds_line, PM_TDS_CAP)    */
   double nlcc_seconds;          /* NLC lines of the search: device time of the fused line launches (first
                                    block start to the last line's end) + host time of exact-path lines */
+  uint64_t split_lines;         /* sharded: NLC lines run split by owner (sources over the shards)      */
 } pm_run_stats;
 
 /* One shard (rank) of a sharded search: the rows of ids v % nshards == shard. */
