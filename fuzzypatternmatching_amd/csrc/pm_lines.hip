@@ -788,18 +788,22 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
   bool fresh = true;  // no line of this launch has changed the state yet
   for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
     const LineDesc& d = a.lines[pl];
-    if (fresh && ld_dev(&a.st[pl].census) == 0) {
+    const unsigned long long cen = ld_dev(&a.st[pl].census);
+    if (fresh && cen == 0) {
       if (blockIdx.x == 0 && threadIdx.x == 0) *a.done = static_cast<unsigned>(pl + 1);
       continue;
     }
+    // a split line is decided on an exact census only -- the replica's sources, identical on every shard --
+    // so every shard splits the same lines: after a line of this launch changed the state the census is a
+    // bound, and a line it would split ends the launch unprocessed (the next launch counts again)
+    const bool split = a.split_min && a.so.nranks > 1 && cen >= a.split_min;
+    if (split && !fresh) break;
     fresh = false;
     LineKernelArgs b = a;
     b.la = &d.la;
     b.i0 = d.i0;
     b.st = a.st + pl;
-    // census on the replica = the line's sources over all shards (an upper bound after an earlier line of
-    // the launch changed the state; identical on every shard, so every shard decides alike)
-    b.split = a.split_min && a.so.nranks > 1 && ld_dev(&a.st[pl].census) >= a.split_min ? 1 : 0;
+    b.split = split ? 1 : 0;
     if (b.split && blockIdx.x == 0 && threadIdx.x == 0) b.st->split = 1;
     if (blockIdx.x == 0 && threadIdx.x == 0) b.st->tstamp[0] = __builtin_amdgcn_s_memrealtime();
     if (d.tds) tds_line(b, s_hist, wr);
@@ -903,8 +907,9 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     // one block per CU: the barrier cost grows with the number of blocks
     c.line_grid = static_cast<unsigned>(std::min<int>(prop.multiProcessorCount, 1024));
   }
-  // the table is sized from the superstep-0 matching rows (upper bound of |S|)
-  ensure_hash(c, std::max<uint64_t>(1ull << 16, 4 * c.ss0_rows));
+  // the table is sized from the superstep-0 matching rows (upper bound of |S|); a replica by its rows, the same
+  // on every shard
+  ensure_hash(c, std::max<uint64_t>(1ull << 16, 4 * (c.replicated ? uint64_t(c.nS_host) : c.ss0_rows)));
   unsigned* d_done = c.d_gbar + kGbarWords;                                   // [0] lines done
   auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
   const size_t ctl_bytes = 64 * sizeof(unsigned) + nl * sizeof(LineStats);  // control words + stats of lines < nl
