@@ -1148,6 +1148,19 @@ pm_ctx* pm_create_shard(const pm_shard_desc* d, const char* pattern_dir, int dev
   }
 }
 
+// Every failed shard's message (a device fault is seen by whichever shard calls the runtime next; the shard
+// whose work faulted names it in its own message).
+static void throw_shard_errors(const std::vector<std::string>& errs) {
+  std::string msg;
+  for (size_t q = 0; q < errs.size(); ++q)
+    if (!errs[q].empty() && errs[q] != "another shard failed")
+      msg += (msg.empty() ? "" : " | ") + ("shard " + std::to_string(q) + ": " + errs[q]);
+  if (msg.empty())
+    for (size_t q = 0; q < errs.size() && msg.empty(); ++q)
+      if (!errs[q].empty()) msg = "shard " + std::to_string(q) + ": " + errs[q];
+  if (!msg.empty()) throw std::runtime_error(msg);
+}
+
 // PM_SEGV_TRACE=1: backtrace of a host crash inside the shard threads (diagnostics)
 static void pm_segv_trace(int sig) {
   void* fr[64];
@@ -1228,11 +1241,7 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
     std::vector<std::thread> pool;
     for (uint32_t q = 0; q < nshards; ++q) pool.emplace_back(work, q);
     for (auto& t : pool) t.join();
-    for (uint32_t q = 0; q < nshards; ++q)
-      if (!errs[q].empty() && errs[q] != "another shard failed")
-        throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
-    for (uint32_t q = 0; q < nshards; ++q)
-      if (!errs[q].empty()) throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
+    throw_shard_errors(errs);
     if (out) *out = st[0];
     return 0;
   } catch (const std::exception& e) {
@@ -1519,11 +1528,7 @@ int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern
     std::vector<std::thread> pool;
     for (uint32_t q = 0; q < nshards; ++q) pool.emplace_back(work, q);
     for (auto& t : pool) t.join();
-    for (uint32_t q = 0; q < nshards; ++q)
-      if (!errs[q].empty() && errs[q] != "another shard failed")
-        throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
-    for (uint32_t q = 0; q < nshards; ++q)
-      if (!errs[q].empty()) throw std::runtime_error("shard " + std::to_string(q) + ": " + errs[q]);
+    throw_shard_errors(errs);
     if (out) *out = st[0];
     return 0;
   } catch (const std::exception& e) {

@@ -120,7 +120,23 @@ struct LineKernelArgs {
   unsigned long long* xflag;      // split cycle lines: M entries this shard's terminals flagged
   unsigned long long* nxflag;
   uint64_t xflag_cap;
+  // PM_DEBUG_SYNC (diagnostics): every row a line reads is checked against the vertex count and the M
+  // buffer first; the first bad one is recorded in dbg[0..3] (flag, vertex, row start, length) and skipped
+  unsigned long long* dbg;
+  uint64_t n, mcap;
 };
+
+// (diagnostics) false when the row (b, L) of vertex u lies outside the M buffer: recorded, not read
+__device__ __forceinline__ bool row_ok(const LineKernelArgs& a, uint32_t u, uint64_t b, uint64_t L) {
+  if (!a.dbg) return true;
+  if (u < a.n && b <= a.mcap && L <= a.mcap - b) return true;
+  if (atomicCAS(&a.dbg[0], 0ull, 1ull) == 0ull) {
+    a.dbg[1] = u;
+    a.dbg[2] = b;
+    a.dbg[3] = L;
+  }
+  return false;
+}
 
 __device__ __forceinline__ void wave_add(unsigned long long* ctr, uint64_t x) {
   x = wave_sum(x);
@@ -239,6 +255,7 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
   if (active) {
     b = a.offp[u];
     L = a.mlen[u];
+    if (!row_ok(a, u, b, L)) L = 0;
   }
   const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
   const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
@@ -256,7 +273,7 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
       const int r = row_of(wr.end[wv], t);
       const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
       const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
-      if (m & kAlive) {
+      if ((m & kAlive) && (!a.dbg || row_ok(a, m & kPosMask, 0, 0))) {
         const uint32_t w = m & kPosMask, sr = wr.t.s[wv][r], ur = wr.t.u[wv][r];
         if (w != wr.t.x[wv][r]) {
           ++emitted;
@@ -626,7 +643,8 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
         // the row of u is fetched together with its T_pub (used if the arrival checks pass)
         const uint16_t T = a.tpub[u];
         const uint64_t ob = a.offp[u];
-        const uint32_t ml = a.mlen[u], ma = a.malive[u];
+        uint32_t ml = a.mlen[u], ma = a.malive[u];
+        if (!row_ok(a, u, ob, ml)) ml = 0;
         if (pos_ok(T, k, la) && enum_ok(w, k, u, la)) {
           b = ob;
           L = ml;
@@ -707,6 +725,7 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
       b = a.offp[s];
       L = a.mlen[s];
       trav += a.malive[s];
+      if (!row_ok(a, s, b, L)) L = 0;
     }
     // walks [s, w] for every alive w in M[s] (flattened over the wave's sources)
     const int wv = threadIdx.x / kWave, lane = lane_id();
@@ -959,6 +978,10 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     a.xflag_cap = m_cap(c);
     a.nxflag = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 6);  // zeroed with d_done
   }
+  static const bool dbg_rows = std::getenv("PM_DEBUG_SYNC") != nullptr;
+  a.dbg = dbg_rows ? reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 16) : nullptr;  // zeroed below
+  a.n = c.n;
+  a.mcap = m_cap(c);
   a.pl_begin = static_cast<int>(pl0);
   a.pl_end = static_cast<int>(nl);
   a.done = d_done;
@@ -1035,6 +1058,11 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
               hs.size() * sizeof(LineStats));
   const unsigned done = static_cast<unsigned>(pin[0] & 0xFFFFFFFFull);
   const unsigned long long kept_slots = pin[1];
+  if (pin[8])  // (PM_DEBUG_SYNC row checks, control words 16-23)
+    throw std::runtime_error("NLC line kernel: row of vertex " + std::to_string(pin[9]) + " at " +
+                             std::to_string(pin[10]) + " + " + std::to_string(pin[11]) + " outside the M buffer (" +
+                             std::to_string(m_cap(c)) + " entries, shard " + std::to_string(c.shard) +
+                             (c.replicated ? ", replica)" : ")"));
   {  // device time of the launch: its start stamp (kst[0], control word 4) to the last processed line's end
     unsigned long long end = pin[5];
     for (unsigned j = 0; j + pl0 < done; ++j) end = std::max(end, hs[j].tstamp[3]);

@@ -432,16 +432,19 @@ __global__ void k_hub_partials(const HubInfo* __restrict__ info, uint32_t H, con
   }
 }
 
-// This shard's share of hub j: its alive M entries in row order to send[soff[j]..].
+// This shard's share of hub j: its alive M entries in row order to send[soff[j]..].  Only the share's own
+// slots are read (its unpadded length, offr): a share of at most kLightMax entries is padded to its class
+// length, and the padding slots of the M buffer hold no M entries (after a relayout the former adjacency's
+// kNone padding, whose bit pattern includes kAlive).
 __global__ void k_hub_pack(const HubInfo* __restrict__ info, uint32_t H, const uint64_t* __restrict__ soff,
-                           const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
-                           uint32_t* __restrict__ send) {
+                           const uint64_t* __restrict__ offp, const uint64_t* __restrict__ offr,
+                           const uint32_t* __restrict__ mcol, uint32_t* __restrict__ send) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * (blockDim.x / 64);
   for (uint32_t j = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; j < H; j += nw) {
     if (soff[j] == ~0ull) continue;
     const uint32_t p = info[j].pos;
-    const uint64_t b = offp[p], len = offp[p + 1] - b;
+    const uint64_t b = offp[p], len = offr[p + 1] - offr[p];
     uint64_t o = soff[j];
     for (uint64_t i0 = 0; i0 < len; i0 += 64) {
       const uint64_t i = i0 + lane;
@@ -616,7 +619,7 @@ void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
   auto* recv = grow<uint32_t>(c.d_xrecv, c.xrecv_cap, std::max<uint64_t>(ro, 1) * sizeof(uint32_t));
   if (so)
     hipLaunchKernelGGL(k_hub_pack, dim3(xgrid(uint64_t(H) * 64)), dim3(kXBlock), 0, c.stream, c.d_hubinfo, H, d_soff,
-                       c.d_offp, c.d_mcol, send);
+                       c.d_offp, c.d_offr, c.d_mcol, send);
   debug_point(c, "delegate pack");
   c.comm->alltoallv(send, sb.data(), recv, rb.data(), c.stream);
   HubFinishArgs a{};

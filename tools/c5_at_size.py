@@ -1,14 +1,17 @@
 """BASELINE config C5 at size on one GPU: an R-MAT text edge list of scale S (default 27, P_gen = 8 files,
 written from the GPU generator's stream), ingested on the GPU with -u 1 (ingest_edge_list.cpp:164-240,
 parallel_edge_list_reader.hpp:242-266), explicit -v label files (vertex_data_db.hpp:137-257) parsed on the GPU,
-and the pattern searched with result files.  Labels: --labels degree (default) writes the degree-log2 labels of
-the symmetrized graph as -v files; --labels hash writes hash32(v ^ 5) % alphabet.  (The hash-labelled 4-cycle's
-template-driven enumeration grows faster than the graph on R-MAT hubs -- 17 k walks at S=22 with alphabet 256,
-200 k with 128 -- and at S=27 exceeds both the oracle's host memory and the device walk arena, so the at-size
-run takes the tree pattern over explicit degree labels.)  Checks:
+and the pattern searched with result files.  Labels: --labels hash (default) writes hash32(v ^ 5) % alphabet
+(default 256) as -v files; --labels degree writes the degree-log2 labels of the symmetrized graph.  Pattern:
+the 4-cycle (default), whose template-driven enumeration runs in chunks of at most --tds-cap walks per level
+(run_tds_line; the reference batches its enumeration, tds_batch_1.hpp:1139-1253).  (With 8 or 64 letters the
+4-cycle enumeration at S=27 is ~10^13 edges -- it grows ~6x per scale from the oracle's S=20-22 counts -- for
+the reference as for this path; 256 letters keep it tractable.)  Checks:
   * the ingested context's result directory equals the GPU-generated graph's (same labels) -- the text path
     builds the same graph;
-  * with --oracle, both equal the oracle's result on the host CSR (16 threads; ~60 GB of host memory at S=27).
+  * the same search with a small TDS chunk cap gives the same result directory (chunk-size invariance);
+  * with --oracle, both equal the oracle's result on the host CSR (~60 GB of host memory at S=27).
+tests/test_gpu_configs.py::test_c5_s27_ingested_label_files runs the same checks in the GPU suite.
 Prints one JSON line (ingest GB/s, search time, digests, match flags); progress on stderr.
 
 usage: python3 tools/c5_at_size.py [--scale 27] [--p-gen 8] [--dir /dev/shm/c5] [--oracle] [--out FILE]
@@ -45,8 +48,9 @@ def main():
     ap.add_argument("--scale", type=int, default=27)
     ap.add_argument("--p-gen", type=int, default=8)
     ap.add_argument("--dir", default=None, help="text files (default: /dev/shm when it has room, else TMPDIR)")
-    ap.add_argument("--pattern", default="rmat_log2_tree_pattern")
-    ap.add_argument("--labels", choices=["degree", "hash"], default="degree")
+    ap.add_argument("--pattern", default="rmat_log2_cycle4_pattern")
+    ap.add_argument("--labels", choices=["degree", "hash"], default="hash")
+    ap.add_argument("--tds-cap", type=int, default=1 << 20, help="PM_TDS_CAP of the chunk-invariance rerun")
     ap.add_argument("--alphabet", type=int, default=256)
     ap.add_argument("--nranks", type=int, default=8, help="output ranks of the result files")
     ap.add_argument("--oracle", action="store_true")
@@ -115,6 +119,16 @@ def main():
         edges = si["lcc_edges"] + si["nlcc_edges"] + si["tds_edges"]
         res["search_ingested"]["edges_per_s"] = round(edges / min(reps), 1)
         log(f"search (ingested): {si}, {min(reps) * 1e3:.2f} ms without files")
+        os.environ["PM_TDS_CAP"] = str(args.tds_cap)
+        out_c = os.path.join(work, "res_capped")
+        scap = m.run_beta(out_c, 64)
+        del os.environ["PM_TDS_CAP"]
+        res["chunk_cap_invariance"] = {"cap": args.tds_cap, "chunks": scap["tds_chunks"],
+                                       "chunks_default": si["tds_chunks"],
+                                       "same": not pmtest.digest_diffs(pmtest.result_digest(out_i, args.nranks),
+                                                                       pmtest.result_digest(out_c, args.nranks))}
+        log(f"chunk cap {args.tds_cap}: {scap['tds_chunks']} chunks, same result: "
+            f"{res['chunk_cap_invariance']['same']}")
         m.close()
         dig_i = pmtest.result_digest(out_i, args.nranks)
         # 3. the same graph generated on the GPU, same labels
@@ -155,7 +169,8 @@ def main():
     if args.out:
         with open(args.out, "w") as f:
             f.write(line + "\n")
-    ok = res.get("ingested_equals_generated") and res.get("oracle_match", True)
+    ok = (res.get("ingested_equals_generated") and res.get("oracle_match", True)
+          and res.get("chunk_cap_invariance", {}).get("same", True))
     sys.exit(0 if ok else 3)
 
 
