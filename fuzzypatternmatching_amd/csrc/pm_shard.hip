@@ -21,6 +21,7 @@
 
 #include <rccl/rccl.h>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
@@ -682,6 +683,83 @@ void shard_codes_after_first(Ctx& c) {
 
 void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t* counts);
 
+// The replica's hub rows in neighbour-id order.  A delegate's M row was assembled at its controller share by
+// share (the entries of targets owned by shard 0, then shard 1, ...: each share in id order), but every M row
+// is searched by neighbour id -- the push-form receivers flag M[u][v] (k_lcc_push_verify), a cycle terminal
+// flags M[s][p] (nem_1.hpp:764-770) -- so the rows of the hubs in the replica are sorted once (segmented radix
+// sort by neighbour id) when the replica is built.
+__global__ void k_hub_rows(const HubInfo* __restrict__ info, uint32_t H, const uint16_t* __restrict__ tpub,
+                           const uint64_t* __restrict__ rmoff, const uint32_t* __restrict__ mlen,
+                           unsigned long long* __restrict__ out) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < H; j += gridDim.x * blockDim.x) {
+    const uint32_t p = info[j].pos;
+    out[2 * j] = tpub[p] ? rmoff[p] : 0ull;
+    out[2 * j + 1] = tpub[p] ? mlen[p] : 0ull;
+  }
+}
+
+__global__ void k_hub_gather(const uint64_t* __restrict__ seg, const uint64_t* __restrict__ src, uint32_t nseg,
+                             const uint32_t* __restrict__ rmcol, const uint32_t* __restrict__ perm,
+                             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, bool back,
+                             uint32_t* __restrict__ rmcol_out) {
+  // segment k: entries [seg[k], seg[k + 1]) of the temporary arrays <-> rmcol[src[k] ..]
+  const int lane = threadIdx.x & 63;
+  for (uint32_t k = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; k < nseg; k += gridDim.x * (blockDim.x / 64)) {
+    const uint64_t b = seg[k], n = seg[k + 1] - b, r = src[k];
+    for (uint64_t i = lane; i < n; i += 64) {
+      if (back) {
+        rmcol_out[r + i] = vals[b + i];
+      } else {
+        const uint32_t m = rmcol[r + i];
+        keys[b + i] = perm[m & kPosMask];
+        vals[b + i] = m;
+      }
+    }
+  }
+}
+
+static void sort_hub_rows(Ctx& c) {
+  const uint32_t H = static_cast<uint32_t>(c.hubinfo.size());
+  if (!H || !c.d_hubinfo) return;
+  auto* d_rows = static_cast<unsigned long long*>(c.arena.get(2 * size_t(H) * sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_hub_rows, dim3(xgrid(H)), dim3(kXBlock), 0, c.stream, c.d_hubinfo, H, c.d_tpub[c.cur],
+                     c.d_rmoff, c.d_mlen, d_rows);
+  std::vector<unsigned long long> rows(2 * size_t(H));
+  PM_HIP_CHECK(hipMemcpyAsync(rows.data(), d_rows, rows.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                              c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  std::vector<uint64_t> seg(1, 0), src;
+  for (uint32_t j = 0; j < H; ++j)
+    if (rows[2 * j + 1] > 1) {
+      src.push_back(rows[2 * j]);
+      seg.push_back(seg.back() + rows[2 * j + 1]);
+    }
+  const uint32_t ns = static_cast<uint32_t>(src.size());
+  const uint64_t total = seg.back();
+  if (!ns) return;
+  auto* d_seg = static_cast<uint64_t*>(c.arena.get(seg.size() * sizeof(uint64_t)));
+  auto* d_src = static_cast<uint64_t*>(c.arena.get(src.size() * sizeof(uint64_t)));
+  auto* k0 = static_cast<uint32_t*>(c.arena.get(total * 4));
+  auto* k1 = static_cast<uint32_t*>(c.arena.get(total * 4));
+  auto* v0 = static_cast<uint32_t*>(c.arena.get(total * 4));
+  auto* v1 = static_cast<uint32_t*>(c.arena.get(total * 4));
+  PM_HIP_CHECK(hipMemcpyAsync(d_seg, seg.data(), seg.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(d_src, src.data(), src.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  const unsigned g = static_cast<unsigned>(std::min<uint64_t>(ns, 4096) + 3) / 4;
+  hipLaunchKernelGGL(k_hub_gather, dim3(g), dim3(kXBlock), 0, c.stream, d_seg, d_src, ns, c.d_rmcol, c.d_perm, k0, v0,
+                     false, c.d_rmcol);
+  size_t tmp = 0;
+  PM_HIP_CHECK(rocprim::segmented_radix_sort_pairs(nullptr, tmp, k0, k1, v0, v1, size_t(total), ns, d_seg, d_seg + 1,
+                                                   0, 32, c.stream));
+  void* d_tmp = c.arena.get(std::max<size_t>(tmp, 1));
+  PM_HIP_CHECK(rocprim::segmented_radix_sort_pairs(d_tmp, tmp, k0, k1, v0, v1, size_t(total), ns, d_seg, d_seg + 1,
+                                                   0, 32, c.stream));
+  hipLaunchKernelGGL(k_hub_gather, dim3(g), dim3(kXBlock), 0, c.stream, d_seg, d_src, ns,
+                     static_cast<const uint32_t*>(nullptr), c.d_perm, k1, v1, true, c.d_rmcol);
+  PM_HIP_CHECK(hipGetLastError());
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));  // (seg / src live on the host stack)
+}
+
 uint64_t pack_state_entry_bound(Ctx& c) {
   // the exact count: pass 1 + scans, then one read-back (the caller sizes its buffer)
   ensure_xcnt(c);
@@ -785,6 +863,10 @@ void shard_replicate(Ctx& c) {
   c.smask_valid = false;
   c.k1_dense = false;
   c.replicated = true;
+  if (c.split_hubs) {
+    c.arena.reset();
+    sort_hub_rows(c);
+  }
 }
 
 // ---------------------------------------------------------------------------
