@@ -221,6 +221,10 @@ struct LineStats {
   unsigned long long wbase[20]; // TDS: slot offset of each position's walks
   unsigned int overflow, single;  // single: finished by block 0 alone
   unsigned int split, pad_;       // split: run over this shard's own sources only, post-processing deferred
+  // a line started on block 0 alone whose frontier outgrew the block: the grid continues from position esc_k
+  // (its walks / frontier from esc_base on)
+  unsigned int esc_k, pad2_;
+  unsigned long long esc_base;
   unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
   unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)

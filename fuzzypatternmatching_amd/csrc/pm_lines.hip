@@ -529,20 +529,33 @@ __device__ __forceinline__ void phase_sync(const LineKernelArgs& a, bool single)
   else tree_barrier(a.gbar);
 }
 
-// A line whose sources and position-1 frontier are at most this large is
-// finished by block 0 alone (block barriers instead of grid barriers);
-// LineKernelArgs::small_line, PM_SMALL_LINE overrides.
+// A line whose sources and position-1 frontier are at most this large starts on
+// block 0 alone (block barriers instead of grid barriers) while the other blocks
+// wait at a grid barrier; once a position's frontier outgrows it, block 0 stops
+// and the whole grid continues from that position (escalation: R-MAT hubs make
+// a small line's later positions explode).  LineKernelArgs::small_line,
+// PM_SMALL_LINE overrides.
 static constexpr uint64_t kSmallLine = 16384;
 
 // ---- path / cycle lines (nem_1) ----------------------------------------
 // Positions 2..C+1 and post-processing; every participating wave calls it.
-__device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
-                                          unsigned long long* s_hist, WaveRows& wr) {
+// Returns true when block 0 (single) handed the line to the grid at position esc_k.
+__device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
+                                          unsigned long long* s_hist, WaveRows& wr, int k0 = 1, uint64_t lo0 = 0) {
   LineStats* st = a.st;
-  uint64_t trav = 0, tokens = 0, lo = 0;
-  for (int k = 1; k <= a.la->C; ++k) {
+  uint64_t trav = 0, tokens = 0, lo = lo0;
+  for (int k = k0; k <= a.la->C; ++k) {
     if (ld_dev(&st->overflow)) break;  // same value in every wave after the barrier
     const uint64_t hi = ld_dev(&st->ftotal);
+    if (single && hi - lo > a.small_line) {  // the frontier outgrew the block: the grid takes position k
+      wave_add(&st->trav, trav);
+      wave_add(&st->tokens, tokens);
+      if (g.tid == 0) {
+        st->esc_base = lo;
+        st->esc_k = static_cast<unsigned>(k);
+      }
+      return true;
+    }
     for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
       const uint64_t i = i0 + lane_id();
       const bool act = i < hi;
@@ -564,7 +577,7 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
   }
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
-  if (ld_dev(&st->overflow)) return;  // the host clears the table and reruns the line
+  if (ld_dev(&st->overflow)) return false;  // the host clears the table and reruns the line
   if (!a.split) line_post(a, g, s_hist);  // (split: after the shards agreed on overflow, split_line_finish)
   // hash cleanup: no insert happens after the last position
   const uint64_t nf = ld_dev(&st->ftotal);
@@ -573,6 +586,7 @@ __device__ __forceinline__ void path_rest(const LineKernelArgs& a, const GridIdx
     a.hkey[h] = kEmpty;
     a.hval[h] = kEmpty;
   }
+  return false;
 }
 
 __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long long* s_hist, WaveRows& wr) {
@@ -594,21 +608,31 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
   const uint64_t nsrc = ld_dev(&st->nsrc);
   if (nsrc == 0) return;  // no tokens, nothing to post-process (every block agrees)
   const bool single = nsrc <= a.small_line && ld_dev(&st->ftotal) <= a.small_line;
-  if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
-  if (!single) path_rest(a, g, false, s_hist, wr);
-  else if (blockIdx.x == 0) path_rest(a, block_idx(), true, s_hist, wr);
+  if (!single) {
+    path_rest(a, g, false, s_hist, wr);
+    return;
+  }
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) st->single = 1;
+    path_rest(a, block_idx(), true, s_hist, wr);
+  }
+  tree_barrier(a.gbar);  // (the other blocks wait for block 0 here)
+  const unsigned ek = ld_dev(&st->esc_k);
+  if (ek) path_rest(a, g, false, s_hist, wr, static_cast<int>(ek), ld_dev(&st->esc_base));
 }
 
 // ---- TDS lines (tds_batch_1) -------------------------------------------
 // Positions 2..C+1, terminal and post-processing.  Walks of position L are
 // stored from wbase[L] on (fresh, 128-B aligned memory per position); kept
 // walks are appended to the launch's kept buffer.
-__device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
-                                         unsigned long long* s_hist, WaveRows& wr, uint64_t kept_base) {
+// Returns true when block 0 (single) handed the line to the grid at position esc_k.
+__device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx& g, bool single,
+                                         unsigned long long* s_hist, WaveRows& wr, uint64_t kept_base,
+                                         int k0 = 1, uint64_t in_base0 = 0) {
   LineStats* st = a.st;
   const LineArgs& la = *a.la;
   const int stride = la.C + 2;
-  uint64_t trav = 0, tokens = 0, in_base = 0;
+  uint64_t trav = 0, tokens = 0, in_base = in_base0;
   // single block: the walk counters live in LDS (no global atomic per wave and round)
   const bool stage = stride <= kStage;
   if (single) {
@@ -616,9 +640,19 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
     __syncthreads();
   }
   const int wv = threadIdx.x / kWave, lane = lane_id();
-  for (int k = 1; k <= la.C; ++k) {
+  for (int k = k0; k <= la.C; ++k) {
     if (ld_dev(&st->overflow)) break;
     const uint64_t nin = single ? wr.wn[k] : ld_dev(&st->wn[k]);
+    if (single && nin > a.small_line) {  // the walks outgrew the block: the grid takes position k
+      if (threadIdx.x >= 2 && threadIdx.x <= static_cast<unsigned>(k)) st->wn[threadIdx.x] = wr.wn[threadIdx.x];
+      wave_add(&st->trav, trav);
+      wave_add(&st->tokens, tokens);
+      if (g.tid == 0) {
+        st->esc_base = in_base;
+        st->esc_k = static_cast<unsigned>(k);
+      }
+      return true;
+    }
     const uint64_t out_base = (in_base + nin * stride + 31) & ~uint64_t(31);
     tokens += g.tid == 0 ? nin : 0;
     const uint32_t* win = a.wbuf + in_base;
@@ -667,7 +701,7 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   if (ld_dev(&st->overflow) || kept0 + nw * stride > a.kept_cap) {
     if (g.tid == 0) atomicOr(&st->overflow, 1u);
     wave_add(&st->trav, trav);
-    return;
+    return false;
   }
   // terminal position C+1 (tds_batch_1.hpp:641-758)
   {
@@ -706,6 +740,7 @@ __device__ __forceinline__ void tds_rest(const LineKernelArgs& a, const GridIdx&
   wave_add(&st->tokens, tokens);
   phase_sync(a, single);
   if (!a.split) line_post(a, g, s_hist);
+  return false;
 }
 
 __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long long* s_hist, WaveRows& wr) {
@@ -764,9 +799,17 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   const uint64_t nsrc = ld_dev(&st->nsrc);
   if (nsrc == 0) return;  // no walks, nothing to post-process (every block agrees)
   const bool single = nsrc <= a.small_line && ld_dev(&st->wn[1]) <= a.small_line;
-  if (single && blockIdx.x == 0 && threadIdx.x == 0) st->single = 1;
-  if (!single) tds_rest(a, g, false, s_hist, wr, kept_base);
-  else if (blockIdx.x == 0) tds_rest(a, block_idx(), true, s_hist, wr, kept_base);
+  if (!single) {
+    tds_rest(a, g, false, s_hist, wr, kept_base);
+    return;
+  }
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) st->single = 1;
+    tds_rest(a, block_idx(), true, s_hist, wr, kept_base);
+  }
+  tree_barrier(a.gbar);  // (the other blocks wait for block 0 here)
+  const unsigned ek = ld_dev(&st->esc_k);
+  if (ek) tds_rest(a, g, false, s_hist, wr, kept_base, static_cast<int>(ek), ld_dev(&st->esc_base));
 }
 
 // NLC lines [pl_begin, pl_end) in order, one grid barrier at each line end
