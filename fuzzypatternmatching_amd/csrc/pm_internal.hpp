@@ -370,6 +370,8 @@ struct Ctx {
   bool smask_valid = false;       // false right after superstep 0 (all entries live)
   uint32_t* d_flags = nullptr;    // [0] not_finished, [1] asymmetric edge state, [2] deleted
   uint32_t* d_tn = nullptr;       // TN per position for the push-form supersteps (allocated on first use)
+  unsigned long long* d_push = nullptr;  // push form: [send pieces, verify's first piece, pieces...]
+  uint64_t push_cap = 0;
   uint64_t* d_counts = nullptr;   // per-slot per-rank counts (vertices, edges) + traversed
   uint64_t* d_part = nullptr;     // per-block counter partials (kPartGridMax x slot_words)
   uint64_t* d_tmask = nullptr;    // superstep-0 survivor masks, kSub words per tile

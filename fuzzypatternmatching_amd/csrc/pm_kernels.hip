@@ -1340,46 +1340,195 @@ __device__ __forceinline__ int64_t m_find(const uint32_t* __restrict__ mcol, uin
   return lo < b + len ? static_cast<int64_t>(lo) : -1;
 }
 
-__global__ __launch_bounds__(kBlock) void k_lcc_push_send(
-    const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
-    const uint16_t* __restrict__ tcur, PatArgs pa, const uint32_t* __restrict__ perm, uint32_t* __restrict__ mcol,
-    const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive, uint32_t* __restrict__ tn,
-    unsigned long long* __restrict__ trav_out) {
-  __shared__ uint16_t s_adj[16];
-  load_adj(s_adj, pa);
-  __syncthreads();
-  const uint32_t nS = *nSp;
-  uint64_t trav = 0;
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t v = slist[i];
-    const uint16_t Tv = tcur[v];
-    if (!Tv) continue;
-    trav += malive[v];
-    const uint64_t b = offp[v];
-    const uint32_t L = mlen[v];
-    const uint32_t vid = perm[v];
-    for (uint32_t j = 0; j < L; ++j) {
-      const uint32_t m = mcol[b + j];
-      if (!(m & kAlive)) continue;
-      const uint32_t u = m & kPosMask;
-      const uint16_t Tu = tcur[u];
-      if (!Tu || !(Tv & nbr_mask(Tu, s_adj))) continue;  // u not in S, or not a valid parent
-      atomicOr(&tn[u], static_cast<uint32_t>(Tv));
-      const int64_t e = m_find(mcol, offp[u], mlen[u], perm, vid);
-      if (e >= 0) {
-        const uint32_t x = mcol[e];
-        if ((x & kPosMask) == v && (x & kAlive)) atomicOr(&mcol[e], kFlag);
-      }
-    }
+// Entry-parallel: each wave takes 64 slist entries (rows); rows of at most kPushLong entries are walked
+// flattened over the wave (every lane takes every 64th entry of their concatenation, four in flight), longer
+// rows (R-MAT hubs: a lane walking a row of 10^5..10^6 entries, each with a binary search, took seconds) are
+// cut into kPushLong-entry pieces appended to a list that every wave of a second launch works through.
+static constexpr uint32_t kPushLong = 256;
+
+struct PushArgs {
+  const uint64_t* offp;
+  const uint32_t* slist;
+  const uint32_t* nS;
+  const uint16_t* tcur;
+  uint16_t* tnxt;
+  uint16_t* tst;
+  const uint32_t* perm;
+  uint32_t* mcol;
+  const uint32_t* mlen;
+  uint32_t* malive;
+  uint32_t* tn;
+  unsigned long long* pieces;   // (slist index << 32 | piece) of the long rows
+  unsigned long long* npieces;  // zeroed before the send launch; the verify's pieces follow the send's
+  uint64_t piece_cap;
+};
+
+// Sender entry: v (id vid, T_pub Tv) delivers to the neighbour in entry m.
+__device__ __forceinline__ void push_send_entry(const PushArgs& a, const uint16_t* s_adj, uint32_t v, uint32_t vid,
+                                                uint16_t Tv, uint32_t m) {
+  if (!(m & kAlive)) return;
+  const uint32_t u = m & kPosMask;
+  const uint16_t Tu = a.tcur[u];
+  if (!Tu || !(Tv & nbr_mask(Tu, s_adj))) return;  // u not in S, or not a valid parent
+  atomicOr(&a.tn[u], static_cast<uint32_t>(Tv));
+  const int64_t e = m_find(a.mcol, a.offp[u], a.mlen[u], a.perm, vid);
+  if (e >= 0) {
+    const uint32_t x = a.mcol[e];
+    if ((x & kPosMask) == v && (x & kAlive)) atomicOr(&a.mcol[e], kFlag);
   }
-  block_atomic_add(trav_out, trav);  // the superstep's traversed-entries word
 }
 
-__global__ __launch_bounds__(kBlock) void k_lcc_push_verify(
-    const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
-    const uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
-    OwnerArgs oa, uint32_t* __restrict__ mcol, const uint32_t* __restrict__ mlen, uint32_t* __restrict__ malive,
-    uint32_t* __restrict__ tn, Partials pp) {
+// Receiver-side verify of one entry of a surviving row: keep flagged entries (flags cleared); returns kept.
+__device__ __forceinline__ uint32_t push_verify_entry(uint32_t* mcol, uint64_t e) {
+  const uint32_t m = mcol[e];
+  if (!(m & kAlive)) return 0u;
+  const bool keep = (m & kFlag) != 0;
+  mcol[e] = (m & kPosMask) | (keep ? kAlive : 0u);
+  return keep ? 1u : 0u;
+}
+
+// Appends the pieces of a long row (slist index i, len entries); false when the list is full.
+__device__ __forceinline__ bool push_pieces(const PushArgs& a, uint64_t i, uint32_t len) {
+  const uint32_t np = (len + kPushLong - 1) / kPushLong;
+  const unsigned long long b = atomicAdd(a.npieces, static_cast<unsigned long long>(np));
+  if (b + np > a.piece_cap) {  // full: the reserved slots below the cap are marked empty
+    for (uint64_t q = b; q < a.piece_cap && q < b + np; ++q) a.pieces[q] = ~0ull;
+    return false;
+  }
+  for (uint32_t q = 0; q < np; ++q) a.pieces[b + q] = (static_cast<unsigned long long>(i) << 32) | q;
+  return true;
+}
+
+// VERIFY = 0: the senders; 1: the receivers' verify (T from TN, survivors' entries compacted in place).
+template <int VERIFY>
+__global__ __launch_bounds__(kBlock) void k_lcc_push_rows(PushArgs a, PatArgs pa, OwnerArgs oa, Partials pp,
+                                                         unsigned long long* __restrict__ trav_out) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  __shared__ uint16_t s_adj[16];
+  __shared__ uint64_t s_beg[kWpb][kWave];
+  __shared__ uint32_t s_end[kWpb][kWave], s_v[kWpb][kWave], s_vid[kWpb][kWave], s_cnt[kWpb][kWave];
+  __shared__ uint16_t s_T[kWpb][kWave];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  load_adj(s_adj, pa);
+  __syncthreads();
+  BlockAcc acc;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nS = *a.nS;
+  const uint64_t nch = (nS + kWave - 1) / kWave;
+  for (uint64_t ch = uint64_t(blockIdx.x) * kWpb + w; ch < nch; ch += uint64_t(gridDim.x) * kWpb) {
+    const uint64_t i = ch * kWave + lane;
+    uint32_t v = 0, vid = 0, len = 0;
+    uint64_t beg = 0;
+    uint16_t T = 0;
+    bool lng = false;
+    if (i < nS) {
+      v = a.slist[i];
+      const uint16_t Tv = a.tcur[v];
+      if (!VERIFY) {
+        if (Tv) {
+          T = Tv;
+          vid = a.perm[v];
+          beg = a.offp[v];
+          len = a.mlen[v];
+          acc.trav += a.malive[v];
+        }
+      } else if (!Tv) {
+        a.tnxt[v] = 0;
+      } else {
+        T = keep_bits(a.tst[v], static_cast<uint16_t>(a.tn[v]), s_adj);
+        a.tn[v] = 0;
+        if (!T) {
+          a.tnxt[v] = 0;
+          a.malive[v] = 0;
+          acc.removed = 1;
+        } else {
+          a.tst[v] = T;
+          a.tnxt[v] = T;
+          beg = a.offp[v];
+          len = a.mlen[v];
+          if (oa.nranks <= 1) acc.vs += 1;
+          else acc_owner(s_hist, oa, v, 0);  // (its edges are added where its entries are counted)
+        }
+      }
+      if (len > kPushLong) {
+        lng = push_pieces(a, i, len);
+        if (lng) {
+          if (VERIFY) a.malive[v] = 0;  // (the pieces add their kept entries)
+          len = 0;
+        }
+      }
+    }
+    (void)lng;
+    // the short rows flattened over the wave (a long row whose pieces did not fit stays here)
+    const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(len));
+    const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+    if (!total) continue;
+    s_end[w][lane] = incl;
+    s_beg[w][lane] = beg;
+    s_v[w][lane] = v;
+    s_vid[w][lane] = vid;
+    s_T[w][lane] = T;
+    s_cnt[w][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t t0 = 0; t0 < total; t0 += 4 * kWave) {
+      uint32_t m[4];
+      int rr[4];
+      uint64_t e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t t = t0 + q * kWave + lane;
+        rr[q] = -1;
+        m[q] = 0;
+        e[q] = 0;
+        if (t < total) {
+          int lo = 0, hi = kWave - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_end[w][mid] > t) hi = mid; else lo = mid + 1;
+          }
+          rr[q] = lo;
+          e[q] = s_beg[w][lo] + (t - (lo ? s_end[w][lo - 1] : 0u));
+          m[q] = a.mcol[e[q]];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (rr[q] < 0) continue;
+        if (!VERIFY) {
+          push_send_entry(a, s_adj, s_v[w][rr[q]], s_vid[w][rr[q]], s_T[w][rr[q]], m[q]);
+        } else if (m[q] & kAlive) {
+          const bool keep = (m[q] & kFlag) != 0;
+          a.mcol[e[q]] = (m[q] & kPosMask) | (keep ? kAlive : 0u);
+          if (keep) atomicAdd(&s_cnt[w][rr[q]], 1u);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (VERIFY && len) {  // this lane's short row: its kept count
+      const uint32_t cnt = s_cnt[w][lane];
+      a.malive[v] = cnt;
+      if (oa.nranks <= 1) acc.es += cnt;
+      else atomicAdd(&s_hist[oa.nranks + owner_of(v, oa)], static_cast<unsigned long long>(cnt));
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!VERIFY) {
+    block_atomic_add(trav_out, acc.trav);  // the superstep's traversed-entries word
+  } else {
+    flush_block(acc, oa, s_hist, s_red, pp);
+  }
+}
+
+// The verify's pieces start where the send's ended (*p0, device word).
+__global__ __launch_bounds__(kBlock) void k_lcc_push_verify_pieces(PushArgs a, PatArgs pa, OwnerArgs oa,
+                                                                  Partials pp, const unsigned long long* p0);
+
+// The long rows' pieces (pieces [p0, *npieces) of the list): one wave per piece, four entries per lane.
+template <int VERIFY>
+__global__ __launch_bounds__(kBlock) void k_lcc_push_pieces(PushArgs a, PatArgs pa, OwnerArgs oa, Partials pp,
+                                                           uint64_t p0) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1387,39 +1536,67 @@ __global__ __launch_bounds__(kBlock) void k_lcc_push_verify(
   load_adj(s_adj, pa);
   __syncthreads();
   BlockAcc acc;
-  const uint32_t nS = *nSp;
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nS; i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint32_t u = slist[i];
-    if (!tcur[u]) {
-      tnxt[u] = 0;
-      continue;
-    }
-    const uint16_t T = keep_bits(tst[u], static_cast<uint16_t>(tn[u]), s_adj);
-    tn[u] = 0;
-    if (!T) {
-      tnxt[u] = 0;
-      malive[u] = 0;
-      acc.removed = 1;
-      continue;
-    }
-    tst[u] = T;
-    tnxt[u] = T;
-    const uint64_t b = offp[u];
-    const uint32_t L = mlen[u];
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t np = min<uint64_t>(*a.npieces, a.piece_cap);
+  for (uint64_t k = p0 + uint64_t(blockIdx.x) * kWpb + w; k < np; k += uint64_t(gridDim.x) * kWpb) {
+    const unsigned long long pc = a.pieces[k];
+    if (pc == ~0ull) continue;  // (a slot of a row that did not fit)
+    const uint32_t v = a.slist[pc >> 32];
+    const uint32_t q = static_cast<uint32_t>(pc);
+    const uint64_t b = a.offp[v] + uint64_t(q) * kPushLong;
+    const uint32_t len = min(kPushLong, a.mlen[v] - q * kPushLong);
     uint32_t cnt = 0;
-    for (uint32_t j = 0; j < L; ++j) {
-      const uint32_t m = mcol[b + j];
-      if (!(m & kAlive)) continue;
-      const bool keep = (m & kFlag) != 0;
-      mcol[b + j] = (m & kPosMask) | (keep ? kAlive : 0u);
-      cnt += keep ? 1u : 0u;
+    const uint16_t Tv = VERIFY ? 0 : a.tcur[v];
+    const uint32_t vid = VERIFY ? 0 : a.perm[v];
+#pragma unroll
+    for (int r = 0; r < static_cast<int>(kPushLong / kWave); ++r) {
+      const uint32_t j = r * kWave + lane;
+      if (j >= len) continue;
+      if (!VERIFY) push_send_entry(a, s_adj, v, vid, Tv, a.mcol[b + j]);
+      else cnt += push_verify_entry(a.mcol, b + j);
     }
-    malive[u] = cnt;
-    if (oa.nranks <= 1) {
-      acc.vs += 1;
-      acc.es += cnt;
-    } else {
-      acc_owner(s_hist, oa, u, cnt);
+    if (VERIFY) {
+      cnt = static_cast<uint32_t>(wave_sum(cnt));
+      if (lane == 0 && cnt) {
+        atomicAdd(&a.malive[v], cnt);
+        if (oa.nranks <= 1) acc.es += cnt;
+        else atomicAdd(&s_hist[oa.nranks + owner_of(v, oa)], static_cast<unsigned long long>(cnt));
+      }
+    }
+  }
+  if (VERIFY) flush_block(acc, oa, s_hist, s_red, pp);
+}
+
+__global__ __launch_bounds__(kBlock) void k_lcc_push_verify_pieces(PushArgs a, PatArgs pa, OwnerArgs oa,
+                                                                  Partials pp, const unsigned long long* p0) {
+  // (the body of k_lcc_push_pieces<1> from a device-side first piece)
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  __syncthreads();
+  BlockAcc acc;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t np = min<uint64_t>(*a.npieces, a.piece_cap);
+  for (uint64_t k = *p0 + uint64_t(blockIdx.x) * kWpb + w; k < np; k += uint64_t(gridDim.x) * kWpb) {
+    const unsigned long long pc = a.pieces[k];
+    if (pc == ~0ull) continue;  // (a slot of a row that did not fit)
+    const uint32_t v = a.slist[pc >> 32];
+    const uint32_t q = static_cast<uint32_t>(pc);
+    const uint64_t b = a.offp[v] + uint64_t(q) * kPushLong;
+    const uint32_t len = min(kPushLong, a.mlen[v] - q * kPushLong);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int r = 0; r < static_cast<int>(kPushLong / kWave); ++r) {
+      const uint32_t j = r * kWave + lane;
+      if (j < len) cnt += push_verify_entry(a.mcol, b + j);
+    }
+    cnt = static_cast<uint32_t>(wave_sum(cnt));
+    if (lane == 0 && cnt) {
+      atomicAdd(&a.malive[v], cnt);
+      if (oa.nranks <= 1) acc.es += cnt;
+      else atomicAdd(&s_hist[oa.nranks + owner_of(v, oa)], static_cast<unsigned long long>(cnt));
     }
   }
   flush_block(acc, oa, s_hist, s_red, pp);
@@ -2120,14 +2297,44 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
     PM_HIP_CHECK(hipMalloc(&c.d_tn, c.n * sizeof(uint32_t)));
     PM_HIP_CHECK(hipMemsetAsync(c.d_tn, 0, c.n * sizeof(uint32_t), c.stream));
   }
+  // the long rows' piece list (a row whose pieces do not fit is walked by its own wave: slower, exact)
+  const uint64_t want = 2 * uint64_t(c.nS_host) + 65536;
+  if (c.push_cap < want) {
+    if (c.d_push) (void)hipFree(c.d_push);
+    c.d_push = nullptr;
+    PM_HIP_CHECK(hipMalloc(&c.d_push, (want + 2) * sizeof(unsigned long long)));
+    c.push_cap = want;
+  }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
-  const unsigned grid = grid_for(c.nS_host, kBlock, 8192);
-  hipLaunchKernelGGL(k_lcc_push_send, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS,
-                     c.d_tpub[c.cur], c.pa, c.d_perm, m_col(c), c.d_mlen, c.d_malive, c.d_tn,
-                     reinterpret_cast<unsigned long long*>(d_slot + 2 * P));
-  hipLaunchKernelGGL(k_lcc_push_verify, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS,
-                     c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
-                     c.d_malive, c.d_tn, partials(c, d_slot));
+  PushArgs a{};
+  a.offp = m_off(c);
+  a.slist = c.d_slist;
+  a.nS = c.d_nS;
+  a.tcur = c.d_tpub[c.cur];
+  a.tnxt = c.d_tpub[c.cur ^ 1];
+  a.tst = c.d_tst;
+  a.perm = c.d_perm;
+  a.mcol = m_col(c);
+  a.mlen = c.d_mlen;
+  a.malive = c.d_malive;
+  a.tn = c.d_tn;
+  a.npieces = c.d_push;          // [0]: pieces appended by the send launch and then by the verify launch
+  a.pieces = c.d_push + 2;
+  a.piece_cap = c.push_cap;
+  PM_HIP_CHECK(hipMemsetAsync(c.d_push, 0, 2 * sizeof(unsigned long long), c.stream));
+  const unsigned grid = grid_for((uint64_t(c.nS_host) + kWave - 1) / kWave, kWpb, 16384);
+  auto* trav = reinterpret_cast<unsigned long long*>(d_slot + 2 * P);
+  const OwnerArgs oa = owner_args(c);
+  hipLaunchKernelGGL(k_lcc_push_rows<0>, dim3(grid), dim3(kBlock), 0, c.stream, a, c.pa, oa, partials(c, d_slot),
+                     trav);
+  hipLaunchKernelGGL(k_lcc_push_pieces<0>, dim3(kMaxGrid), dim3(kBlock), 0, c.stream, a, c.pa, oa,
+                     partials(c, d_slot), uint64_t(0));
+  // the verify's pieces are appended after the send's: copy the send's count to word 1 (the verify's first)
+  PM_HIP_CHECK(hipMemcpyAsync(c.d_push + 1, c.d_push, sizeof(unsigned long long), hipMemcpyDeviceToDevice, c.stream));
+  hipLaunchKernelGGL(k_lcc_push_rows<1>, dim3(grid), dim3(kBlock), 0, c.stream, a, c.pa, oa, partials(c, d_slot),
+                     trav);
+  hipLaunchKernelGGL(k_lcc_push_verify_pieces, dim3(kMaxGrid), dim3(kBlock), 0, c.stream, a, c.pa, oa,
+                     partials(c, d_slot), c.d_push + 1);
   PM_HIP_CHECK(hipGetLastError());
   c.cur ^= 1;
   c.smask_valid = false;  // the pull kernel's live masks are not maintained here
