@@ -225,6 +225,7 @@ struct LineStats {
   // (its walks / frontier from esc_base on)
   unsigned int esc_k, pad2_;
   unsigned long long esc_base;
+  unsigned long long lp[20];  // long-row pieces appended at each position (pm_lines.hip, kLineLong)
   unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
   unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)

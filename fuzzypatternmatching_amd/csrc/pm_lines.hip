@@ -120,6 +120,10 @@ struct LineKernelArgs {
   unsigned long long* xflag;      // split cycle lines: M entries this shard's terminals flagged
   unsigned long long* nxflag;
   uint64_t xflag_cap;
+  // long rows (hubs) of a position: cut into kLineLong-entry pieces that the whole grid works through after
+  // the position's other items (a wave walking a hub row of 10^5..10^6 entries alone held up the line)
+  unsigned long long* lpieces;
+  uint64_t lp_cap;
   // PM_DEBUG_SYNC (diagnostics): every row a line reads is checked against the vertex count and the M
   // buffer first; the first bad one is recorded in dbg[0..3] (flag, vertex, row start, length) and skipped
   unsigned long long* dbg;
@@ -184,6 +188,22 @@ __device__ __forceinline__ uint64_t ht_insert(const LineKernelArgs& a, uint32_t 
   return kEmpty;
 }
 
+// Index of vertex v in the row [b, e) (rows hold positions in neighbour-id order, one entry per neighbour), e
+// when absent.
+__device__ __forceinline__ uint64_t row_find(const LineKernelArgs& a, uint64_t b, uint64_t e, uint32_t v) {
+  const uint32_t pid = a.perm[v];
+  uint64_t lo = b, hi = e;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a.perm[a.mcol[mid] & kPosMask] < pid) lo = mid + 1; else hi = mid;
+  }
+  return lo < e && (a.mcol[lo] & kPosMask) == v ? lo : e;
+}
+__device__ __forceinline__ bool row_has_alive(const LineKernelArgs& a, uint64_t b, uint64_t e, uint32_t v) {
+  const uint64_t i = row_find(a, b, e, v);
+  return i < e && (a.mcol[i] & kAlive);
+}
+
 // Terminal position C+1 of a path / cycle line (nem_1.hpp:661-791).
 __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t p) {
   const LineArgs& la = *a.la;
@@ -194,15 +214,10 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
   } else {
     if (u != s) return;
     a.tsm[s] = 2;
-    // mark M[s][p]: rows hold positions in neighbour-id order
-    const uint32_t pid = a.perm[p];
+    // mark M[s][p]
     const uint64_t b = a.offp[s], e = b + a.mlen[s];
-    uint64_t lo = b, hi = e;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (a.perm[a.mcol[mid] & kPosMask] < pid) lo = mid + 1; else hi = mid;
-    }
-    if (lo < e && (a.mcol[lo] & kPosMask) == p && (a.mcol[lo] & kAlive)) {
+    const uint64_t lo = row_find(a, b, e, p);
+    if (lo < e && (a.mcol[lo] & kAlive)) {
       if (!a.split) {
         a.mcol[lo] |= kFlag;
       } else if (!(atomicOr(&a.mcol[lo], kFlag) & kFlag)) {  // newly flagged: the other replicas get it too
@@ -241,21 +256,55 @@ __device__ __forceinline__ int row_of(const uint32_t* end, uint32_t t) {
   return lo;
 }
 
+struct GridIdx {
+  uint64_t tid, nth, gw, nw;
+};
+
+static constexpr uint32_t kLineLong = 2048;
+static constexpr int kUnroll = 4;  // entry groups in flight per wave in the flattened row loops
+
+// Appends the pieces of a long row (item id of position k, len entries) to the position's list; false when it
+// is full (the caller's wave then walks the row itself).  Piece word: q << 32 | item.
+__device__ __forceinline__ bool line_pieces(const LineKernelArgs& a, int k, uint32_t item, uint32_t len) {
+  const uint32_t np = (len + kLineLong - 1) / kLineLong;
+  const unsigned long long b = atomicAdd(&a.st->lp[k], static_cast<unsigned long long>(np));
+  if (b + np > a.lp_cap) {
+    for (uint64_t q = b; q < a.lp_cap && q < b + np; ++q) a.lpieces[q] = ~0ull;
+    return false;
+  }
+  for (uint32_t q = 0; q < np; ++q) a.lpieces[b + q] = (static_cast<unsigned long long>(q) << 32) | item;
+  return true;
+}
+
 // Forwarding from u (token of source s at position k, excluded parent excl):
 // every alive w in M[u] other than excl goes to position k + 1 (terminal
 // action at C + 1, else arrival filter + hash insert).  All lanes of the wave
 // must call it; returns the lane's share of the emitted token count.
 __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows& wr, uint32_t u, uint32_t s,
-                                               uint32_t excl, int k, bool active) {
+                                               uint32_t excl, int k, bool active, uint32_t item) {
   uint32_t emitted = 0;
   const LineArgs& la = *a.la;
   const int wv = threadIdx.x / kWave, lane = lane_id();
   uint64_t b = 0;
   uint32_t L = 0;
+  const bool term = k == la.C;  // the row's entries reach the terminal position C + 1
   if (active) {
     b = a.offp[u];
     L = a.mlen[u];
     if (!row_ok(a, u, b, L)) L = 0;
+    if (term && L) {
+      // the token count of a terminal row is its alive entries other than excl, as the walk would count them;
+      // only the terminal actions need the entries
+      emitted = a.malive[u] - (excl != kNone && row_has_alive(a, b, b + L, excl) ? 1u : 0u);
+      if (la.VC) {
+        // cycle line: of the row's entries only w = s reaches the terminal action, so the row is searched for s
+        if (s != excl && row_has_alive(a, b, b + L, s)) tp_terminal(a, s, s, u);
+        L = 0;
+      } else if (!a.tpub[s] || a.tsm[s] == 2) {
+        L = 0;  // path line: the action acks an active source only, and s is inactive or acked already
+      }
+    }
+    if (L > kLineLong && line_pieces(a, k, item, L)) L = 0;  // (the pieces: tp_pieces)
   }
   const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
   const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
@@ -266,35 +315,107 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
   wr.t.u[wv][lane] = u;
   wr.t.x[wv][lane] = excl;
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
-    const uint32_t t = t0 + lane;
-    uint64_t slot = kEmpty;
-    if (t < total) {
-      const int r = row_of(wr.end[wv], t);
-      const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
-      const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
+  // kUnroll groups of 64 entries per round: their row searches and entry loads are independent (the loads
+  // of one round are in flight together), their first arrivals share one frontier reservation
+  for (uint32_t t0 = 0; t0 < total; t0 += kUnroll * kWave) {
+    uint32_t mm[kUnroll];
+    int rr[kUnroll];
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      const uint32_t t = t0 + j * kWave + lane;
+      mm[j] = 0;
+      rr[j] = 0;
+      if (t < total) {
+        const int r = row_of(wr.end[wv], t);
+        const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
+        rr[j] = r;
+        mm[j] = a.mcol[wr.beg[wv][r] + (t - first)];
+      }
+    }
+    uint32_t slots[kUnroll];
+    uint32_t nnew = 0;
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      const uint32_t m = mm[j];
+      const int r = rr[j];
       if ((m & kAlive) && (!a.dbg || row_ok(a, m & kPosMask, 0, 0))) {
         const uint32_t w = m & kPosMask, sr = wr.t.s[wv][r], ur = wr.t.u[wv][r];
         if (w != wr.t.x[wv][r]) {
-          ++emitted;
-          if (k + 1 == la.C + 1) {
-            tp_terminal(a, w, sr, ur);
-          } else if (w != sr && pos_ok(a.tpub[w], k + 1, la)) {
-            slot = ht_insert(a, sr, w, static_cast<uint32_t>(k + 1), ur);
+          if (term) {
+            tp_terminal(a, w, sr, ur);  // (counted above)
+          } else {
+            ++emitted;
+            if (w != sr && pos_ok(a.tpub[w], k + 1, la)) {
+              const uint64_t slot = ht_insert(a, sr, w, static_cast<uint32_t>(k + 1), ur);
+              if (slot != kEmpty) slots[nnew++] = static_cast<uint32_t>(slot);
+            }
           }
         }
       }
     }
-    const uint32_t is_new = slot != kEmpty ? 1u : 0u;
-    if (__ballot(is_new)) {
-      const uint64_t pos = wave_reserve(&a.st->ftotal, is_new);
-      if (is_new) {
-        if (pos < a.fcap) a.front[pos] = static_cast<uint32_t>(slot);
+    if (__ballot(nnew != 0)) {
+      const uint64_t pos = wave_reserve(&a.st->ftotal, nnew);
+      for (uint32_t j = 0; j < nnew; ++j) {
+        if (pos + j < a.fcap) a.front[pos + j] = slots[j];
         else atomicOr(&a.st->overflow, 1u);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
+  return emitted;
+}
+
+// The long-row pieces of position k of a path / cycle line (items: the source at k = 0, the frontier's hash
+// slot after): the entries [q kLineLong, (q + 1) kLineLong) of the item's row, one piece per wave and round,
+// with tp_forward's per-entry rule.  Returns the lane's share of the emitted tokens.
+__device__ __forceinline__ uint32_t tp_pieces(const LineKernelArgs& a, const GridIdx& g, int k) {
+  const LineArgs& la = *a.la;
+  const int lane = lane_id();
+  uint32_t emitted = 0;
+  const uint64_t np = min<uint64_t>(ld_dev(&a.st->lp[k]), a.lp_cap);
+  for (uint64_t pi = g.gw; pi < np; pi += g.nw) {
+    const unsigned long long pc = ld_dev(&a.lpieces[pi]);
+    if (pc == ~0ull) continue;
+    const uint32_t item = static_cast<uint32_t>(pc), q = static_cast<uint32_t>(pc >> 32);
+    uint32_t s, u, excl = kNone;
+    if (k == 0) {
+      s = u = item;
+    } else {
+      const unsigned long long key = ld_dev(&a.hkey[item]);
+      const uint32_t par = static_cast<uint32_t>(ld_dev(&a.hval[item]));
+      s = static_cast<uint32_t>(key >> 32);
+      u = static_cast<uint32_t>(key);
+      excl = par == kMulti ? kNone : par;
+    }
+    const uint64_t b = a.offp[u] + uint64_t(q) * kLineLong;
+    const uint32_t len = min(kLineLong, a.mlen[u] - q * kLineLong);
+    for (uint32_t t0 = 0; t0 < len; t0 += kWave) {
+      const uint32_t t = t0 + lane;
+      uint64_t slot = kEmpty;
+      if (t < len) {
+        const uint32_t m = a.mcol[b + t];
+        if ((m & kAlive) && (!a.dbg || row_ok(a, m & kPosMask, 0, 0))) {
+          const uint32_t w = m & kPosMask;
+          if (w != excl) {
+            if (k == la.C) {
+              tp_terminal(a, w, s, u);  // (the token count was taken when the row was listed)
+            } else {
+              ++emitted;
+              if (w != s && pos_ok(a.tpub[w], k + 1, la)) slot = ht_insert(a, s, w, static_cast<uint32_t>(k + 1), u);
+            }
+          }
+        }
+      }
+      const uint32_t is_new = slot != kEmpty ? 1u : 0u;
+      if (__ballot(is_new)) {
+        const uint64_t pos = wave_reserve(&a.st->ftotal, is_new);
+        if (is_new) {
+          if (pos < a.fcap) a.front[pos] = static_cast<uint32_t>(slot);
+          else atomicOr(&a.st->overflow, 1u);
+        }
+      }
+    }
+  }
   return emitted;
 }
 
@@ -330,9 +451,6 @@ static constexpr unsigned kGbarWords = 64 + 32 * 64;  // up to 1024 blocks
 
 static constexpr int kLineBlock = 1024;
 static_assert(kLineBlock / kWave == kLineWaves, "WaveRows is sized for kLineBlock");
-struct GridIdx {
-  uint64_t tid, nth, gw, nw;
-};
 __device__ __forceinline__ GridIdx grid_idx() {
   GridIdx g;
   const uint32_t wpb = blockDim.x / kWave;
@@ -485,33 +603,92 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
   wr.beg[wv][lane] = b;
   wr.end[wv][lane] = incl;
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
-    const uint32_t t = t0 + lane;
-    bool child = false;
-    uint32_t nb = 0;
-    const uint32_t* w = win;
-    if (t < total) {
-      const int r = row_of(wr.end[wv], t);
-      const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
-      const uint32_t m = a.mcol[wr.beg[wv][r] + (t - first)];
-      w = stage ? wr.walk[wv] + r * stride : win + (i0 + r) * stride;
-      if (m & kAlive) {
-        nb = m & kPosMask;
-        child = tds_child_ok(w, k, nb, la);
+  // kUnroll groups of 64 entries per round (tp_forward); the round's children share one reservation
+  for (uint32_t t0 = 0; t0 < total; t0 += kUnroll * kWave) {
+    uint32_t mm[kUnroll];
+    int rr[kUnroll];
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      const uint32_t t = t0 + j * kWave + lane;
+      mm[j] = 0;
+      rr[j] = 0;
+      if (t < total) {
+        const int r = row_of(wr.end[wv], t);
+        const uint32_t first = r ? wr.end[wv][r - 1] : 0u;
+        rr[j] = r;
+        mm[j] = a.mcol[wr.beg[wv][r] + (t - first)];
       }
     }
-    const uint64_t pos = wave_reserve(ctr, child ? 1u : 0u);
-    if (child) {
-      if ((pos + 1) * stride <= out_room) {
-        uint32_t* d = out + pos * stride;
+    uint32_t cm = 0;  // children of the round (bit j)
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      const uint32_t* w = stage ? wr.walk[wv] + rr[j] * stride : win + (i0 + rr[j]) * stride;
+      if ((mm[j] & kAlive) && tds_child_ok(w, k, mm[j] & kPosMask, la)) cm |= 1u << j;
+    }
+    const uint32_t nc = __popc(cm);
+    const uint64_t pos = wave_reserve(ctr, nc);
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      if (!((cm >> j) & 1u)) continue;
+      const uint32_t* w = stage ? wr.walk[wv] + rr[j] * stride : win + (i0 + rr[j]) * stride;
+      if ((pos + c + 1) * stride <= out_room) {
+        uint32_t* d = out + (pos + c) * stride;
         for (int p = 0; p <= k; ++p) d[p] = w[p];
-        d[k + 1] = nb;
+        d[k + 1] = mm[j] & kPosMask;
       } else {
         atomicOr(&a.st->overflow, 1u);
       }
+      ++c;
     }
   }
   __builtin_amdgcn_wave_barrier();
+}
+
+// The long-row pieces of position k of a TDS line (items: the source at k = 0, the walk's index in win after):
+// children of the entries [q kLineLong, (q + 1) kLineLong) of the row of the walk's last vertex, with
+// tds_expand_wave's checks, appended through ctr.  The walk itself passed the arrival checks when its piece
+// was listed.
+__device__ __forceinline__ void tds_pieces(const LineKernelArgs& a, const GridIdx& g, int k, const uint32_t* win,
+                                           uint32_t* out, uint64_t out_room, int stride, unsigned long long* ctr) {
+  const LineArgs& la = *a.la;
+  const int lane = lane_id();
+  const uint64_t np = min<uint64_t>(ld_dev(&a.st->lp[k]), a.lp_cap);
+  for (uint64_t pi = g.gw; pi < np; pi += g.nw) {
+    const unsigned long long pc = ld_dev(&a.lpieces[pi]);
+    if (pc == ~0ull) continue;
+    const uint32_t item = static_cast<uint32_t>(pc), q = static_cast<uint32_t>(pc >> 32);
+    const uint32_t* w = k == 0 ? nullptr : win + uint64_t(item) * stride;
+    const uint32_t u = k == 0 ? item : w[k];
+    const uint64_t b = a.offp[u] + uint64_t(q) * kLineLong;
+    const uint32_t len = min(kLineLong, a.mlen[u] - q * kLineLong);
+    for (uint32_t t0 = 0; t0 < len; t0 += kWave) {
+      const uint32_t t = t0 + lane;
+      bool child = false;
+      uint32_t nb = 0;
+      if (t < len) {
+        const uint32_t m = a.mcol[b + t];
+        if (m & kAlive) {
+          nb = m & kPosMask;
+          child = k == 0 || tds_child_ok(w, k, nb, la);
+        }
+      }
+      const uint64_t pos = wave_reserve(ctr, child ? 1u : 0u);
+      if (child) {
+        if ((pos + 1) * stride <= out_room) {
+          uint32_t* d = out + pos * stride;
+          if (k == 0) {
+            d[0] = u;
+          } else {
+            for (int p = 0; p <= k; ++p) d[p] = w[p];
+          }
+          d[k + 1] = nb;
+        } else {
+          atomicOr(&a.st->overflow, 1u);
+        }
+      }
+    }
+  }
 }
 
 // Block-local index (single-block mode: block 0 finishes a small line alone).
@@ -559,9 +736,9 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
     for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
       const uint64_t i = i0 + lane_id();
       const bool act = i < hi;
-      uint32_t s = 0, u = 0, excl = kNone;
+      uint32_t s = 0, u = 0, excl = kNone, h = 0;
       if (act) {
-        const uint32_t h = ld_dev(&a.front[i]);
+        h = ld_dev(&a.front[i]);
         const unsigned long long key = ld_dev(&a.hkey[h]);
         const uint32_t par = static_cast<uint32_t>(ld_dev(&a.hval[h]));
         s = static_cast<uint32_t>(key >> 32);
@@ -569,10 +746,14 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
         excl = par == kMulti ? kNone : par;
         trav += a.malive[u];
       }
-      tokens += tp_forward(a, wr, u, s, excl, k, act);
+      tokens += tp_forward(a, wr, u, s, excl, k, act, h);
     }
     lo = hi;
     phase_sync(a, single);
+    if (ld_dev(&st->lp[k])) {  // the position's long rows, spread over every wave
+      tokens += tp_pieces(a, g, k);
+      phase_sync(a, single);
+    }
     if (g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
   wave_add(&st->trav, trav);
@@ -599,7 +780,12 @@ __device__ __forceinline__ void path_line(const LineKernelArgs& a, unsigned long
     uint32_t s;
     const bool ok = select_source(a, i0 + lane_id(), nact, false, s);
     if (ok) trav += a.malive[s];
-    tokens += tp_forward(a, wr, s, s, kNone, 0, ok);
+    tokens += tp_forward(a, wr, s, s, kNone, 0, ok, s);
+  }
+  tree_barrier(a.gbar);
+  if (ld_dev(&st->lp[0])) {  // the sources' long rows, spread over every wave
+    tokens += tp_pieces(a, g, 0);
+    tree_barrier(a.gbar);
   }
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
@@ -657,10 +843,12 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
     tokens += g.tid == 0 ? nin : 0;
     const uint32_t* win = a.wbuf + in_base;
     unsigned long long* ctr = single ? &wr.wn[k + 1] : &st->wn[k + 1];
+    const bool closing = k == la.C && la.VC;
     for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
       const uint64_t i = i0 + lane;
       uint64_t b = 0;
       uint32_t L = 0;
+      const uint32_t* cw = nullptr;
       if (i < nin) {
         const uint32_t* w = win + i * stride;
         uint32_t u;
@@ -683,14 +871,39 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
           b = ob;
           L = ml;
           trav += ma;
+          if (closing) {
+            // the closing step of a cycle walk: its only child is w[0] (tds_child_ok), searched for in the row
+            L = row_has_alive(a, b, b + L, w[0]) ? 1u : 0u;
+            cw = w;
+          } else if (L > kLineLong && i <= 0xFFFFFFFFull && line_pieces(a, k, static_cast<uint32_t>(i), L)) {
+            L = 0;
+          }
         }
+      }
+      if (closing) {
+        const uint64_t pos = wave_reserve(ctr, L);
+        if (L) {
+          uint32_t* o = a.wbuf + out_base;
+          if ((pos + 1) * stride <= (a.wcap > out_base ? a.wcap - out_base : 0)) {
+            uint32_t* d = o + pos * stride;
+            for (int p = 0; p <= k; ++p) d[p] = cw[p];
+            d[k + 1] = cw[0];
+          } else {
+            atomicOr(&st->overflow, 1u);
+          }
+        }
+        continue;
       }
       __builtin_amdgcn_wave_barrier();
       tds_expand_wave(a, wr, win, i0, k, b, L, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride,
                       stage, ctr);
     }
-    in_base = out_base;
     phase_sync(a, single);
+    if (ld_dev(&st->lp[k])) {  // the position's long rows, spread over every wave
+      tds_pieces(a, g, k, win, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride, ctr);
+      phase_sync(a, single);
+    }
+    in_base = out_base;
     if (g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
   // every final walk may be kept: its room must exist before any terminal effect
@@ -761,6 +974,7 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
       L = a.mlen[s];
       trav += a.malive[s];
       if (!row_ok(a, s, b, L)) L = 0;
+      if (L > kLineLong && line_pieces(a, 0, s, L)) L = 0;  // (the pieces: tds_pieces)
     }
     // walks [s, w] for every alive w in M[s] (flattened over the wave's sources)
     const int wv = threadIdx.x / kWave, lane = lane_id();
@@ -795,6 +1009,10 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
   }
   wave_add(&st->trav, trav);
   tree_barrier(a.gbar);
+  if (ld_dev(&st->lp[0])) {  // the sources' long rows, spread over every wave
+    tds_pieces(a, g, 0, nullptr, a.wbuf, a.wcap, stride, &st->wn[1]);
+    tree_barrier(a.gbar);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) st->tstamp[1] = __builtin_amdgcn_s_memrealtime();
   const uint64_t nsrc = ld_dev(&st->nsrc);
   if (nsrc == 0) return;  // no walks, nothing to post-process (every block agrees)
@@ -1032,6 +1250,9 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   a.nact = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 4);  // zeroed with d_done
   c.arena.reset();
   a.act = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(c.nS_host, 1) * sizeof(uint32_t)));
+  // long-row pieces of one position (a full list leaves the rest of the rows to their waves)
+  a.lp_cap = std::min<uint64_t>(1ull << 22, std::max<uint64_t>(1024, m_cap(c) / kLineLong * 4));
+  a.lpieces = static_cast<unsigned long long*>(c.arena.get(a.lp_cap * sizeof(unsigned long long)));
   const uint64_t room = (c.arena.cap - c.arena.used - 8192) / sizeof(uint32_t);
   a.kept_cap = room / 4;
   a.kept = static_cast<uint32_t*>(c.arena.get(a.kept_cap * sizeof(uint32_t)));
