@@ -279,6 +279,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
+  if (const char* e = std::getenv("PM_ROW_COMPACTION")) c->no_row_compaction = std::string(e) == "0";
   if (const char* e = std::getenv("PM_DIAG_STEP")) c->diag_step = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
   c->any_sv = any_sv;
@@ -484,6 +485,9 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
+  // rows with dead entries compacted for the lines and the next call (k_compact_rows)
+  if (!c.no_row_compaction) launch_compact_rows(c);
+  debug_point(c, "row compaction");
   c.probe("lcc issued");
   // read-back through pinned memory: [nS | local counts | summed counts]
   uint64_t* pin = pinned(c, 1 + 2 * D * W);
@@ -799,10 +803,15 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
         if (c.comm && !c.replicated) throw std::runtime_error("internal: NLC line before the sharded state was replicated");
         if (c.fused_lines && pl != exact_at) {
           if (pl < batch_pl0 || pl >= batch_pl0 + batch.size()) {
-            bool overflow = false;
-            const size_t n = run_lines_fused(c, pl, files, batch, overflow);
-            batch_pl0 = pl;
-            if (overflow) exact_at = pl + n;
+            for (;;) {
+              bool overflow = false;
+              const size_t n = run_lines_fused(c, pl, files, batch, overflow);
+              batch_pl0 = pl;
+              const bool regrown = c.hash_regrown;
+              c.hash_regrown = false;
+              if (overflow && !regrown) exact_at = pl + n;  // (walk storage, or no room to grow the table)
+              if (!(overflow && regrown && n == 0)) break;   // the overflowed line reruns with the grown table
+            }
           }
           if (pl >= batch_pl0 && pl < batch_pl0 + batch.size()) {
             fo = std::move(batch[pl - batch_pl0]);

@@ -1370,7 +1370,9 @@ __device__ __forceinline__ void push_send_entry(const PushArgs& a, const uint16_
   const uint32_t u = m & kPosMask;
   const uint16_t Tu = a.tcur[u];
   if (!Tu || !(Tv & nbr_mask(Tu, s_adj))) return;  // u not in S, or not a valid parent
-  atomicOr(&a.tn[u], static_cast<uint32_t>(Tv));
+  // (bits already present are not sent again: a hub's TN word takes one atomic per new bit instead of one per
+  // neighbour, which serialised on the word)
+  if ((a.tn[u] & Tv) != Tv) atomicOr(&a.tn[u], static_cast<uint32_t>(Tv));
   const int64_t e = m_find(a.mcol, a.offp[u], a.mlen[u], a.perm, vid);
   if (e >= 0) {
     const uint32_t x = a.mcol[e];
@@ -2566,6 +2568,61 @@ __global__ void k_clear_tpub(const uint32_t* __restrict__ list, const uint32_t* 
     t0[p] = 0;
     t1[p] = 0;
   }
+}
+
+// End of an LCC call: the rows of S that are mostly dead entries (written length mlen above twice the alive count
+// plus 64) are compacted in place, alive entries to the front in order (rows stay in neighbour-id order, flags kept),
+// and mlen becomes the alive count.  Every later reader walks [offp, offp + mlen): without this a hub row kept
+// its superstep-0 length (10^5 entries at C5 S=27 with a few thousand alive) for every later superstep and
+// every NLC line position.  One wave per row with dead entries (reads precede the writes of each 64-entry
+// step, and a write never passes its lane's read position).
+__global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restrict__ slist,
+                                                         const uint32_t* __restrict__ nSp,
+                                                         const uint16_t* __restrict__ tcur,
+                                                         const uint64_t* __restrict__ offp, uint32_t* __restrict__ mcol,
+                                                         uint32_t* __restrict__ mlen,
+                                                         const uint32_t* __restrict__ malive) {
+  const int lane = lane_id();
+  const uint64_t gw = blockIdx.x * uint64_t(kWpb) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nw = uint64_t(gridDim.x) * kWpb;
+  const uint64_t nS = *nSp;
+  for (uint64_t c0 = gw * kWave; c0 < nS; c0 += nw * kWave) {
+    const uint64_t i = c0 + lane;
+    uint32_t v = 0;
+    bool dead = false;
+    if (i < nS) {
+      v = slist[i];
+      const uint32_t L = mlen[v];
+      dead = tcur[v] && L > 2 * malive[v] + kWave;  // (a row mostly alive is left as it is)
+    }
+    uint64_t bal = __ballot(dead);
+    while (bal) {
+      const int r = __ffsll(static_cast<long long>(bal)) - 1;
+      bal &= bal - 1;
+      const uint32_t u = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), r));
+      const uint64_t b = offp[u];
+      const uint32_t L = mlen[u];
+      uint32_t cnt = 0;
+      for (uint32_t j0 = 0; j0 < L; j0 += kWave) {
+        const uint32_t j = j0 + lane;
+        const uint32_t m = j < L ? mcol[b + j] : 0u;
+        const bool keep = (m & kAlive) != 0;
+        const uint64_t km = __ballot(keep);
+        if (keep) mcol[b + cnt + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km), 0u))] = m;
+        cnt += static_cast<uint32_t>(__popcll(km));
+      }
+      if (lane == 0) mlen[u] = cnt;
+    }
+  }
+}
+
+void launch_compact_rows(Ctx& c) {
+  if (!c.nS_host) return;
+  hipLaunchKernelGGL(k_compact_rows, dim3(grid_for((uint64_t(c.nS_host) + kWave - 1) / kWave, kWpb, 4096)),
+                     dim3(kBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tpub[c.cur], m_off(c), m_col(c), c.d_mlen,
+                     c.d_malive);
+  PM_HIP_CHECK(hipGetLastError());
 }
 
 void launch_clear_tpub(Ctx& c) {

@@ -1122,6 +1122,21 @@ static void ensure_hash(Ctx& c, uint64_t want) {
   c.hcap = cap;
 }
 
+// After a path / cycle line overflowed the (source, vertex) table: partial inserts are not all recorded in the
+// frontier list, so the table is cleared; it grows 4x while the device has room (c.hash_regrown: the caller
+// reruns the line on the fused path), else the line goes to the exact per-position path.
+static void regrow_hash(Ctx& c) {
+  PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+  const uint64_t grow = c.hcap * 4;
+  constexpr uint64_t kSlotBytes = 2 * sizeof(unsigned long long) + sizeof(uint32_t) / 2;  // key, value, frontier
+  size_t free_b = 0, total_b = 0;
+  PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+  if (grow > (1ull << 31) || grow * kSlotBytes + (size_t(2) << 30) > free_b + c.hcap * kSlotBytes) return;
+  ensure_hash(c, grow);
+  c.hash_regrown = true;
+}
+
 void free_line_buffers(Ctx& c) {
   void* ptrs[] = {c.d_hkey, c.d_hval, c.d_front, c.d_gbar, c.d_ldesc};  // (d_lstats lives in d_gbar)
   for (void* p : ptrs)
@@ -1189,7 +1204,7 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   }
   // the table is sized from the superstep-0 matching rows (upper bound of |S|); a replica by its rows, the same
   // on every shard
-  ensure_hash(c, std::max<uint64_t>(1ull << 16, 4 * (c.replicated ? uint64_t(c.nS_host) : c.ss0_rows)));
+  ensure_hash(c, std::max<uint64_t>(1ull << 20, 4 * (c.replicated ? uint64_t(c.nS_host) : c.ss0_rows)));
   unsigned* d_done = c.d_gbar + kGbarWords;                                   // [0] lines done
   auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
   const size_t ctl_bytes = 64 * sizeof(unsigned) + nl * sizeof(LineStats);  // control words + stats of lines < nl
@@ -1350,11 +1365,11 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
       std::fprintf(stderr, "[pm] line %zu: P1 %.1f us, rest %.1f us, end barrier %.1f us (%s, %llu sources)\n",
                    pl0 + j, (st.tstamp[1] - st.tstamp[0]) * 0.01, (st.tstamp[2] - st.tstamp[1]) * 0.01,
                    (st.tstamp[3] - st.tstamp[2]) * 0.01, st.single ? "block 0" : "grid", st.nsrc);
-      std::string pos = "[pm]   positions (walks in, us):";
+      std::string pos = "[pm]   positions (walks in, us, long-row pieces):";
       unsigned long long prev = st.tstamp[1];
       for (int k = 1; k < 20 && st.ptime[k]; ++k) {
-        char b[64];
-        std::snprintf(b, sizeof(b), " %d:(%llu, %.1f)", k, st.wn[k], (st.ptime[k] - prev) * 0.01);
+        char b[96];
+        std::snprintf(b, sizeof(b), " %d:(%llu, %.1f, %llu)", k, st.wn[k], (st.ptime[k] - prev) * 0.01, st.lp[k]);
         pos += b;
         prev = st.ptime[k];
       }
@@ -1368,14 +1383,9 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     if (st.split) {  // (the launch's last line) effects, stats and walks combined over the shards
       FusedLineOut out;
       out.stride = static_cast<uint32_t>(c.pattern.lines[pl].cycle_length + 2);
-      if (!split_line_finish(c, pl, st, kept_dev, want_walks, out)) {  // some shard overflowed: exact path
+      if (!split_line_finish(c, pl, st, kept_dev, want_walks, out)) {  // some shard overflowed (all agree)
         overflow = true;
-        if (pl < 4) {
-          const uint64_t grow = c.hcap * 4;
-          PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
-          PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
-          ensure_hash(c, grow);
-        }
+        if (pl < 4) regrow_hash(c);
         break;
       }
       c.last_acked = out.tr.acked;
@@ -1385,13 +1395,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     }
     if (st.overflow) {
       overflow = true;
-      if (pl < 4) {
-        // partial inserts are not all recorded in the frontier list: clear all, grow
-        const uint64_t grow = c.hcap * 4;
-        PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
-        PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
-        ensure_hash(c, grow);
-      }
+      if (pl < 4) regrow_hash(c);
       break;
     }
     FusedLineOut out;

@@ -45,6 +45,6 @@ if [ "${SKIP_STEP:-0}" != 1 ]; then
   done
 fi
 if [ "${SKIP_VARIANTS:-0}" != 1 ]; then
-  timeout -k 10 200 python3 tools/k1_variants.py $SCALE $PGEN 0 8 16 32 128 1 > gpurun_out/k1_variants_${TAG}.log 2>&1
+  timeout -k 10 200 python3 tools/k1_variants.py $SCALE $PGEN ${VARIANTS:-0 1024 2048 4096 7168 8 16} > gpurun_out/k1_variants_${TAG}.log 2>&1
   echo "variants rc=$?"; cat gpurun_out/k1_variants_${TAG}.log | tail -8
 fi
