@@ -9,7 +9,7 @@ with its degree labels (pm_run_rmat_local_shards).  Prints one JSON line: per N 
 run split, and the result counters (which must not depend on N).
 
 usage: python3 tools/split_lines_scaling.py [--scale 22] [--p-gen 4] [--labels hash|degree] [--alphabet 64]
-                                            [--shards 1 2 4] [--out FILE]
+                                            [--shards 1 2 4] [--split-min N] [--out FILE]
 """
 import argparse
 import json
@@ -33,8 +33,11 @@ def main():
     ap.add_argument("--p-gen", type=int, default=4)
     ap.add_argument("--pattern", default="rmat_log2_cycle4_pattern")
     ap.add_argument("--shards", type=int, nargs="+", default=[1, 2, 4])
+    ap.add_argument("--split-min", type=int, default=None, help="PM_SPLIT_LINES (source census from which a line splits)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
+    if args.split_min is not None:
+        os.environ["PM_SPLIT_LINES"] = str(args.split_min)
     pattern = os.path.join(ROOT, "patterns", args.pattern)
     lab = f"hash32(v ^ 5) % {args.alphabet} labels" if args.labels == "hash" else "degree-log2 labels"
     res = {"what": f"R-MAT S={args.scale} P_gen={args.p_gen} {lab}, {args.pattern}, N in-process shards on one "
