@@ -264,7 +264,8 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_smask[0] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
   c->d_smask[1] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
   c->d_sources = dalloc<uint32_t>(c->n);
-  c->d_nS = dalloc<uint32_t>(1);
+  c->d_nS = dalloc<uint32_t>(2);  // [1]: long-row stamp (launch_compact_rows)
+  PM_HIP_CHECK(hipMemset(c->d_nS, 0, 2 * sizeof(uint32_t)));
   c->d_flags = dalloc<uint32_t>(4);
   c->d_tsm = dalloc<uint8_t>(c->n);
   c->d_tcode = dalloc<uint32_t>((c->n + 15) / 16 + 1);
@@ -379,6 +380,7 @@ static void reset_state(Ctx& c, bool defer = false) {
   if (!defer) flush_zero(c);
   c.cur = 0;
   c.nS_host = 0;
+  c.push_long = true;  // full-length rows until the first row compaction
   c.lcc_started = false;
   c.replicated = false;
   c.k1_dense = false;
@@ -486,12 +488,13 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
   // rows with dead entries compacted for the lines and the next call (k_compact_rows)
-  if (!c.no_row_compaction) launch_compact_rows(c);
+  const uint32_t stamp = ++c.lcc_calls;
+  if (!c.no_row_compaction) launch_compact_rows(c, stamp);
   debug_point(c, "row compaction");
   c.probe("lcc issued");
   // read-back through pinned memory: [nS | local counts | summed counts]
   uint64_t* pin = pinned(c, 1 + 2 * D * W);
-  PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));  // + stamp
   // sharded: the supersteps before the replica counted this shard's rows only: their slots are summed
   // over the shards (the replica's supersteps count the whole state on every shard)
   const uint64_t sharded_slots = c.comm && init_step ? std::min<uint64_t>(D, 2) : 0;
@@ -508,6 +511,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   std::vector<uint64_t> local = sharded_slots ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
   const uint32_t nS = static_cast<uint32_t>(pin[0] & 0xFFFFFFFFull);
   c.nS_host = nS;
+  c.push_long = c.no_row_compaction || !nS || static_cast<uint32_t>(pin[0] >> 32) == stamp;
   LccOut out;
   bool asym = false;
   {

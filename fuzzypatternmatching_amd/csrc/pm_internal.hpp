@@ -437,7 +437,9 @@ struct Ctx {
   unsigned long long* d_hval = nullptr;
   uint64_t hcap = 0;
   bool hash_regrown = false;
-  bool no_row_compaction = false;  // PM_ROW_COMPACTION=0 (diagnostics): rows keep their dead entries  // the last fused launch overflowed the table and grew it (rerun the line fused)
+  bool no_row_compaction = false;
+  uint32_t lcc_calls = 0;  // stamp of the LCC calls (the compaction's long-row word)
+  bool push_long = true;   // some row of S may be longer than a push-form piece (unknown: true)  // PM_ROW_COMPACTION=0 (diagnostics): rows keep their dead entries  // the last fused launch overflowed the table and grew it (rerun the line fused)
   uint32_t* d_front = nullptr;    // slots inserted by a fused path line (cleared by it)
   unsigned* d_gbar = nullptr;     // grid barrier state of the fused line kernels
   unsigned line_grid = 0;         // blocks of a full-chip line launch (one per CU)
@@ -507,7 +509,7 @@ void ensure_slist2(Ctx& c);
 // Push form of a later superstep (send + verify launches): directed inputs and
 // LCC calls after the first (M may be asymmetric there).
 void launch_lcc_push(Ctx& c, uint64_t* d_slot);
-void launch_compact_rows(Ctx& c);
+void launch_compact_rows(Ctx& c, uint32_t stamp);
 void launch_count_state(Ctx& c, uint64_t* d_slot);
 void launch_compact_slist(Ctx& c);  // keeps the live entries of the last superstep's mask
 // Zero T_pub (both buffers) at the slist entries of the last search (every

@@ -1359,7 +1359,7 @@ struct PushArgs {
   uint32_t* malive;
   uint32_t* tn;
   unsigned long long* pieces;   // (slist index << 32 | piece) of the long rows
-  unsigned long long* npieces;  // zeroed before the send launch; the verify's pieces follow the send's
+  unsigned long long* npieces;  // zeroed before the launches (the send and the verify have lists of their own)
   uint64_t piece_cap;
 };
 
@@ -1523,10 +1523,6 @@ __global__ __launch_bounds__(kBlock) void k_lcc_push_rows(PushArgs a, PatArgs pa
   }
 }
 
-// The verify's pieces start where the send's ended (*p0, device word).
-__global__ __launch_bounds__(kBlock) void k_lcc_push_verify_pieces(PushArgs a, PatArgs pa, OwnerArgs oa,
-                                                                  Partials pp, const unsigned long long* p0);
-
 // The long rows' pieces (pieces [p0, *npieces) of the list): one wave per piece, four entries per lane.
 template <int VERIFY>
 __global__ __launch_bounds__(kBlock) void k_lcc_push_pieces(PushArgs a, PatArgs pa, OwnerArgs oa, Partials pp,
@@ -1568,40 +1564,6 @@ __global__ __launch_bounds__(kBlock) void k_lcc_push_pieces(PushArgs a, PatArgs 
     }
   }
   if (VERIFY) flush_block(acc, oa, s_hist, s_red, pp);
-}
-
-__global__ __launch_bounds__(kBlock) void k_lcc_push_verify_pieces(PushArgs a, PatArgs pa, OwnerArgs oa,
-                                                                  Partials pp, const unsigned long long* p0) {
-  // (the body of k_lcc_push_pieces<1> from a device-side first piece)
-  __shared__ unsigned long long s_hist[2 * kMaxRanks];
-  __shared__ unsigned long long s_red[kWpb * 6];
-  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
-  __syncthreads();
-  BlockAcc acc;
-  const int lane = lane_id();
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t np = min<uint64_t>(*a.npieces, a.piece_cap);
-  for (uint64_t k = *p0 + uint64_t(blockIdx.x) * kWpb + w; k < np; k += uint64_t(gridDim.x) * kWpb) {
-    const unsigned long long pc = a.pieces[k];
-    if (pc == ~0ull) continue;  // (a slot of a row that did not fit)
-    const uint32_t v = a.slist[pc >> 32];
-    const uint32_t q = static_cast<uint32_t>(pc);
-    const uint64_t b = a.offp[v] + uint64_t(q) * kPushLong;
-    const uint32_t len = min(kPushLong, a.mlen[v] - q * kPushLong);
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int r = 0; r < static_cast<int>(kPushLong / kWave); ++r) {
-      const uint32_t j = r * kWave + lane;
-      if (j < len) cnt += push_verify_entry(a.mcol, b + j);
-    }
-    cnt = static_cast<uint32_t>(wave_sum(cnt));
-    if (lane == 0 && cnt) {
-      atomicAdd(&a.malive[v], cnt);
-      if (oa.nranks <= 1) acc.es += cnt;
-      else atomicAdd(&s_hist[oa.nranks + owner_of(v, oa)], static_cast<unsigned long long>(cnt));
-    }
-  }
-  flush_block(acc, oa, s_hist, s_red, pp);
 }
 
 // Counts of the current state (after token-passing post-processing).
@@ -2299,12 +2261,13 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
     PM_HIP_CHECK(hipMalloc(&c.d_tn, c.n * sizeof(uint32_t)));
     PM_HIP_CHECK(hipMemsetAsync(c.d_tn, 0, c.n * sizeof(uint32_t), c.stream));
   }
-  // the long rows' piece list (a row whose pieces do not fit is walked by its own wave: slower, exact)
+  // the long rows' piece lists of the send and of the verify (a row whose pieces do not fit is walked by its
+  // own wave: slower, exact)
   const uint64_t want = 2 * uint64_t(c.nS_host) + 65536;
   if (c.push_cap < want) {
     if (c.d_push) (void)hipFree(c.d_push);
     c.d_push = nullptr;
-    PM_HIP_CHECK(hipMalloc(&c.d_push, (want + 2) * sizeof(unsigned long long)));
+    PM_HIP_CHECK(hipMalloc(&c.d_push, (2 * want + 2) * sizeof(unsigned long long)));
     c.push_cap = want;
   }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
@@ -2320,23 +2283,28 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
   a.mlen = c.d_mlen;
   a.malive = c.d_malive;
   a.tn = c.d_tn;
-  a.npieces = c.d_push;          // [0]: pieces appended by the send launch and then by the verify launch
+  a.npieces = c.d_push;  // [0] the send's piece count, [1] the verify's
   a.pieces = c.d_push + 2;
   a.piece_cap = c.push_cap;
-  PM_HIP_CHECK(hipMemsetAsync(c.d_push, 0, 2 * sizeof(unsigned long long), c.stream));
+  PushArgs av = a;
+  av.npieces = c.d_push + 1;
+  av.pieces = c.d_push + 2 + c.push_cap;
+  // no row of S longer than a piece (the last row compaction says so, c.push_long): no piece lists
+  const bool pieces = c.push_long;
+  if (pieces) PM_HIP_CHECK(hipMemsetAsync(c.d_push, 0, 2 * sizeof(unsigned long long), c.stream));
   const unsigned grid = grid_for((uint64_t(c.nS_host) + kWave - 1) / kWave, kWpb, 16384);
   auto* trav = reinterpret_cast<unsigned long long*>(d_slot + 2 * P);
   const OwnerArgs oa = owner_args(c);
   hipLaunchKernelGGL(k_lcc_push_rows<0>, dim3(grid), dim3(kBlock), 0, c.stream, a, c.pa, oa, partials(c, d_slot),
                      trav);
-  hipLaunchKernelGGL(k_lcc_push_pieces<0>, dim3(kMaxGrid), dim3(kBlock), 0, c.stream, a, c.pa, oa,
-                     partials(c, d_slot), uint64_t(0));
-  // the verify's pieces are appended after the send's: copy the send's count to word 1 (the verify's first)
-  PM_HIP_CHECK(hipMemcpyAsync(c.d_push + 1, c.d_push, sizeof(unsigned long long), hipMemcpyDeviceToDevice, c.stream));
-  hipLaunchKernelGGL(k_lcc_push_rows<1>, dim3(grid), dim3(kBlock), 0, c.stream, a, c.pa, oa, partials(c, d_slot),
+  if (pieces)
+    hipLaunchKernelGGL(k_lcc_push_pieces<0>, dim3(kMaxGrid), dim3(kBlock), 0, c.stream, a, c.pa, oa,
+                       partials(c, d_slot), uint64_t(0));
+  hipLaunchKernelGGL(k_lcc_push_rows<1>, dim3(grid), dim3(kBlock), 0, c.stream, av, c.pa, oa, partials(c, d_slot),
                      trav);
-  hipLaunchKernelGGL(k_lcc_push_verify_pieces, dim3(kMaxGrid), dim3(kBlock), 0, c.stream, a, c.pa, oa,
-                     partials(c, d_slot), c.d_push + 1);
+  if (pieces)
+    hipLaunchKernelGGL(k_lcc_push_pieces<1>, dim3(kMaxGrid), dim3(kBlock), 0, c.stream, av, c.pa, oa,
+                       partials(c, d_slot), uint64_t(0));
   PM_HIP_CHECK(hipGetLastError());
   c.cur ^= 1;
   c.smask_valid = false;  // the pull kernel's live masks are not maintained here
@@ -2345,7 +2313,8 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
 void ensure_slist2(Ctx& c) {
   if (c.d_slist2) return;
   PM_HIP_CHECK(hipMalloc(&c.d_slist2, std::max<uint64_t>(c.n, 1) * sizeof(uint32_t)));
-  PM_HIP_CHECK(hipMalloc(&c.d_nS2, sizeof(uint32_t)));
+  PM_HIP_CHECK(hipMalloc(&c.d_nS2, 2 * sizeof(uint32_t)));  // [1]: long-row stamp (launch_compact_rows)
+  PM_HIP_CHECK(hipMemset(c.d_nS2, 0, 2 * sizeof(uint32_t)));
 }
 
 void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
@@ -2581,7 +2550,8 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
                                                          const uint16_t* __restrict__ tcur,
                                                          const uint64_t* __restrict__ offp, uint32_t* __restrict__ mcol,
                                                          uint32_t* __restrict__ mlen,
-                                                         const uint32_t* __restrict__ malive) {
+                                                         const uint32_t* __restrict__ malive,
+                                                         uint32_t* __restrict__ long_stamp, uint32_t stamp) {
   const int lane = lane_id();
   const uint64_t gw = blockIdx.x * uint64_t(kWpb) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint64_t nw = uint64_t(gridDim.x) * kWpb;
@@ -2592,8 +2562,12 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
     bool dead = false;
     if (i < nS) {
       v = slist[i];
-      const uint32_t L = mlen[v];
-      dead = tcur[v] && L > 2 * malive[v] + kWave;  // (a row mostly alive is left as it is)
+      if (tcur[v]) {
+        const uint32_t L = mlen[v];
+        dead = L > 2 * malive[v] + kWave;  // (a row mostly alive is left as it is)
+        // a row longer than a push-form piece after the compaction: the next call needs its piece lists
+        if (!dead && L > kPushLong) *long_stamp = stamp;
+      }
     }
     uint64_t bal = __ballot(dead);
     while (bal) {
@@ -2612,16 +2586,21 @@ __global__ __launch_bounds__(kBlock) void k_compact_rows(const uint32_t* __restr
                                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km), 0u))] = m;
         cnt += static_cast<uint32_t>(__popcll(km));
       }
-      if (lane == 0) mlen[u] = cnt;
+      if (lane == 0) {
+        mlen[u] = cnt;
+        if (cnt > kPushLong) *long_stamp = stamp;
+      }
     }
   }
 }
 
-void launch_compact_rows(Ctx& c) {
+// (the long-row stamp goes to the word after the list count, read back with it: c.d_nS[1] == stamp <=> some row
+// of S is longer than a push-form piece)
+void launch_compact_rows(Ctx& c, uint32_t stamp) {
   if (!c.nS_host) return;
   hipLaunchKernelGGL(k_compact_rows, dim3(grid_for((uint64_t(c.nS_host) + kWave - 1) / kWave, kWpb, 4096)),
                      dim3(kBlock), 0, c.stream, c.d_slist, c.d_nS, c.d_tpub[c.cur], m_off(c), m_col(c), c.d_mlen,
-                     c.d_malive);
+                     c.d_malive, c.d_nS + 1, stamp);
   PM_HIP_CHECK(hipGetLastError());
 }
 
