@@ -1006,6 +1006,10 @@ __device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
   return x;
 }
 
+#ifndef PM_STEP_UNROLL
+#define PM_STEP_UNROLL 4  // entries in flight per lane in k_lcc_step's flattened rows
+#endif
+static constexpr int kStepUnroll = PM_STEP_UNROLL;
 #ifndef PM_STEP_WAVES
 #define PM_STEP_WAVES 6  // waves per SIMD the register budget of k_lcc_step is sized for
 #endif
@@ -1120,13 +1124,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
       s_tn[w][lane] = 0;
       s_cnt[w][lane] = 0;
       __builtin_amdgcn_wave_barrier();
-      for (uint32_t t0 = 0; t0 < total; t0 += 4 * kWave) {
-        uint32_t m[4];
-        uint16_t tv[4];
-        int rr[4];
-        uint64_t e[4];
+      for (uint32_t t0 = 0; t0 < total; t0 += kStepUnroll * kWave) {
+        uint32_t m[kStepUnroll];
+        uint16_t tv[kStepUnroll];
+        int rr[kStepUnroll];
+        uint64_t e[kStepUnroll];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kStepUnroll; ++q) {
           const uint32_t t = t0 + q * kWave + lane;
           m[q] = 0u;
           rr[q] = 0;
@@ -1143,10 +1147,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
           }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < kStepUnroll; ++q)
           tv[q] = (m[q] & kAlive) ? ((diag & 1) ? uint16_t(m[q] & 0x7Fu) : tpub_of(m[q] & kPosMask)) : uint16_t(0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < kStepUnroll; ++q)
           if (m[q] & kAlive) {
             uint32_t tq = 0, cq = 0;
             k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym);

@@ -12,7 +12,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log
   [ $rc -eq 0 ] || exit $rc
 fi
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-  python3 bench.py --steps 3 --warmup 1 --cpu-baseline off > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.log
+PM_LINES_NOCOOP=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
+  python3 bench.py --steps 3 --warmup 1 --cpu-baseline off --c3 off --fixture-check off > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.log
 rc=$?; echo "rocprof rc=$rc"; cat gpurun_out/prof_$TAG.json; tail -2 gpurun_out/prof_$TAG.log
 exit $rc
