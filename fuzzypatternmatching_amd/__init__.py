@@ -329,6 +329,12 @@ class PatternMatcher:
         self._check(_lib().pm_run_beta(self._ctx, result_dir.encode(), max_iterations, ctypes.byref(st)))
         return st.as_dict()
 
+    def run_beta_into(self, st, max_iterations=0):
+        """One search without result files into a caller-owned _abi.RunStats (no dict built: the bench's timed
+        loop converts after the clock stops)."""
+        self._check(_lib().pm_run_beta(self._ctx, b"", max_iterations, ctypes.byref(st)))
+        return st
+
     def tpub_census(self, deferred_reset=False):
         """(nonzero T_pub entries of buffer 0, of buffer 1, positions nonzero in either buffer outside the
         current slist) -- diagnostics of the invariant the search-start clear relies on

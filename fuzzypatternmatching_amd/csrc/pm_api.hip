@@ -885,6 +885,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     if (lines_on) f.iteration.push_back(std::to_string(itr) + ", " + fmt_double(since(t_itr)));
     ++itr;
   } while (nf);
+  c.probe("iterations done");
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   c.probe("end");
   const double secs = since(t_pattern);

@@ -1233,8 +1233,9 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   a.fcap = c.hcap / 2;
   a.st = c.d_lstats;
   a.lines = c.d_ldesc;
-  a.small_line = kSmallLine;
-  if (const char* e = std::getenv("PM_SMALL_LINE")) a.small_line = std::strtoull(e, nullptr, 10);
+  static const uint64_t small_line =
+      std::getenv("PM_SMALL_LINE") ? std::strtoull(std::getenv("PM_SMALL_LINE"), nullptr, 10) : kSmallLine;
+  a.small_line = small_line;
   // split lines (sharded replica): owner rule of the shards, the flag list
   a.so.hubs = c.d_hubs;
   a.so.perm = c.d_perm;
@@ -1353,13 +1354,14 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     PM_HIP_CHECK(hipMemcpy(kept.data(), kept_dev, kept_slots * sizeof(uint32_t), hipMemcpyDeviceToHost));
   }
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
-  if (std::getenv("PM_PHASE_TIMES")) {
+  static const bool phase_times = std::getenv("PM_PHASE_TIMES") != nullptr;
+  if (phase_times) {
     unsigned long long ks[2] = {0, 0};
     PM_HIP_CHECK(hipMemcpy(ks, c.d_gbar + kGbarWords + 8, sizeof(ks), hipMemcpyDeviceToHost));
     std::fprintf(stderr, "[pm] lines launch: active list %.1f us, to line start %.1f us\n", (ks[1] - ks[0]) * 0.01,
                  (hs[0].tstamp[0] - ks[1]) * 0.01);
   }
-  if (std::getenv("PM_PHASE_TIMES"))
+  if (phase_times)
     for (unsigned j = 0; j + pl0 < done; ++j) {
       const LineStats& st = hs[j];
       std::fprintf(stderr, "[pm] line %zu: P1 %.1f us, rest %.1f us, end barrier %.1f us (%s, %llu sources)\n",
@@ -1422,6 +1424,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
     outs.push_back(std::move(out));
     ++completed;
   }
+  c.probe("lines parsed");
   return completed;
 }
 
