@@ -112,6 +112,7 @@ struct LineKernelArgs {
   uint32_t* act;   // S members at launch start (slist entries with T_pub != 0), built by k_lines
   unsigned long long* nact;
   uint64_t small_line;  // single-block threshold (kSmallLine)
+  int stamps;           // per-position time stamps (PM_PHASE_TIMES)
   // sharded replica: lines whose census reaches split_min run split by owner (so: the shard owner rule)
   OwnerArgs so;
   uint32_t shard;
@@ -244,6 +245,7 @@ struct WaveRows {
     uint32_t walk[kLineWaves][kWave * kStage];    // the wave's walks (TDS positions)
   };
   unsigned long long wn[20];  // walks per position of a single-block TDS line
+  unsigned lpany[20];         // a row of this position went to the piece list (single-block lines: no global read)
 };
 
 // Lane owning concatenated entry t (end[] inclusive scan of the wave's rows).
@@ -265,7 +267,9 @@ static constexpr int kUnroll = 4;  // entry groups in flight per wave in the fla
 
 // Appends the pieces of a long row (item id of position k, len entries) to the position's list; false when it
 // is full (the caller's wave then walks the row itself).  Piece word: q << 32 | item.
-__device__ __forceinline__ bool line_pieces(const LineKernelArgs& a, int k, uint32_t item, uint32_t len) {
+__device__ __forceinline__ bool line_pieces(const LineKernelArgs& a, int k, uint32_t item, uint32_t len,
+                                            unsigned* lpany) {
+  lpany[k] = 1u;
   const uint32_t np = (len + kLineLong - 1) / kLineLong;
   const unsigned long long b = atomicAdd(&a.st->lp[k], static_cast<unsigned long long>(np));
   if (b + np > a.lp_cap) {
@@ -304,7 +308,7 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
         L = 0;  // path line: the action acks an active source only, and s is inactive or acked already
       }
     }
-    if (L > kLineLong && line_pieces(a, k, item, L)) L = 0;  // (the pieces: tp_pieces)
+    if (L > kLineLong && line_pieces(a, k, item, L, wr.lpany)) L = 0;  // (the pieces: tp_pieces)
   }
   const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
   const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
@@ -721,6 +725,10 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
                                           unsigned long long* s_hist, WaveRows& wr, int k0 = 1, uint64_t lo0 = 0) {
   LineStats* st = a.st;
   uint64_t trav = 0, tokens = 0, lo = lo0;
+  if (single) {
+    if (threadIdx.x < 20) wr.lpany[threadIdx.x] = 0u;
+    __syncthreads();
+  }
   for (int k = k0; k <= a.la->C; ++k) {
     if (ld_dev(&st->overflow)) break;  // same value in every wave after the barrier
     const uint64_t hi = ld_dev(&st->ftotal);
@@ -750,11 +758,11 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
     }
     lo = hi;
     phase_sync(a, single);
-    if (ld_dev(&st->lp[k])) {  // the position's long rows, spread over every wave
+    if (single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull) {  // the position's long rows, over every wave
       tokens += tp_pieces(a, g, k);
       phase_sync(a, single);
     }
-    if (g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
+    if (a.stamps && g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
   wave_add(&st->trav, trav);
   wave_add(&st->tokens, tokens);
@@ -822,7 +830,10 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
   // single block: the walk counters live in LDS (no global atomic per wave and round)
   const bool stage = stride <= kStage;
   if (single) {
-    if (threadIdx.x < 20) wr.wn[threadIdx.x] = threadIdx.x == 1 ? ld_dev(&st->wn[1]) : 0ull;
+    if (threadIdx.x < 20) {
+      wr.wn[threadIdx.x] = threadIdx.x == 1 ? ld_dev(&st->wn[1]) : 0ull;
+      wr.lpany[threadIdx.x] = 0u;
+    }
     __syncthreads();
   }
   const int wv = threadIdx.x / kWave, lane = lane_id();
@@ -875,7 +886,7 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
             // the closing step of a cycle walk: its only child is w[0] (tds_child_ok), searched for in the row
             L = row_has_alive(a, b, b + L, w[0]) ? 1u : 0u;
             cw = w;
-          } else if (L > kLineLong && i <= 0xFFFFFFFFull && line_pieces(a, k, static_cast<uint32_t>(i), L)) {
+          } else if (L > kLineLong && i <= 0xFFFFFFFFull && line_pieces(a, k, static_cast<uint32_t>(i), L, wr.lpany)) {
             L = 0;
           }
         }
@@ -899,12 +910,12 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
                       stage, ctr);
     }
     phase_sync(a, single);
-    if (ld_dev(&st->lp[k])) {  // the position's long rows, spread over every wave
+    if (single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull) {  // the position's long rows, over every wave
       tds_pieces(a, g, k, win, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride, ctr);
       phase_sync(a, single);
     }
     in_base = out_base;
-    if (g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
+    if (a.stamps && g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
   // every final walk may be kept: its room must exist before any terminal effect
   const uint64_t nw = single ? wr.wn[la.C + 1] : ld_dev(&st->wn[la.C + 1]);
@@ -974,7 +985,7 @@ __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long 
       L = a.mlen[s];
       trav += a.malive[s];
       if (!row_ok(a, s, b, L)) L = 0;
-      if (L > kLineLong && line_pieces(a, 0, s, L)) L = 0;  // (the pieces: tds_pieces)
+      if (L > kLineLong && line_pieces(a, 0, s, L, wr.lpany)) L = 0;  // (the pieces: tds_pieces)
     }
     // walks [s, w] for every alive w in M[s] (flattened over the wave's sources)
     const int wv = threadIdx.x / kWave, lane = lane_id();
@@ -1236,6 +1247,8 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   static const uint64_t small_line =
       std::getenv("PM_SMALL_LINE") ? std::strtoull(std::getenv("PM_SMALL_LINE"), nullptr, 10) : kSmallLine;
   a.small_line = small_line;
+  static const bool phase_stamps = std::getenv("PM_PHASE_TIMES") != nullptr;
+  a.stamps = phase_stamps ? 1 : 0;
   // split lines (sharded replica): owner rule of the shards, the flag list
   a.so.hubs = c.d_hubs;
   a.so.perm = c.d_perm;
