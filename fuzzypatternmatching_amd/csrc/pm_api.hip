@@ -328,7 +328,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_ktab, c->d_ttab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_slist2, c->d_nS2, c->d_ccnt, c->d_cbase, c->d_ctmp, c->d_smask[0], c->d_smask[1], c->d_kmask, c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp,
+                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit, c->d_push,
                   };

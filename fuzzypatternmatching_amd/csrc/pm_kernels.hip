@@ -1008,6 +1008,16 @@ __device__ __forceinline__ uint32_t wave_max32(uint32_t x) {
   return x;
 }
 
+// The superstep-0 records in place (one context): the concatenation of the waves' slices is indexed through the
+// slice of each 64-record chunk (cdesc) and the slices' output offsets (rofs, rofs[W] = the light records); the
+// heavy survivors' records follow in srec.  The first later superstep writes slist (the positions) as it reads.
+struct RecSrc {
+  const uint4* rarea;
+  const uint64_t* rbase;
+  const uint64_t* rofs;
+  const uint32_t* cdesc;
+  uint32_t W;
+};
 #ifndef PM_STEP_UNROLL
 #define PM_STEP_UNROLL 4  // entries in flight per lane in k_lcc_step's flattened rows
 #endif
@@ -1021,7 +1031,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
     uint16_t* __restrict__ tcur, uint16_t* __restrict__ tnxt, uint16_t* __restrict__ tst, PatArgs pa,
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
-    const uint4* __restrict__ srec, uint64_t dbase, unsigned long long* __restrict__ keep_out) {
+    const uint4* __restrict__ srec, uint64_t dbase, unsigned long long* __restrict__ keep_out, RecSrc rs,
+    uint32_t* __restrict__ slist_out) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1076,7 +1087,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
       // row, T_pub = 0, ignores it)
       uint32_t l, dm = kNone;
       if (srec) {  // dense superstep-0 output: the records, in slist order (coalesced)
-        const uint4 r = srec[i];
+        uint4 r;
+        if (rs.rarea) {  // in place: the chunk's slice, then the lane's (a slice may end inside the chunk)
+          const uint64_t nl = rs.rofs[rs.W];
+          if (i < nl) {
+            uint32_t sl = rs.cdesc[chunk];
+            while (i >= rs.rofs[sl + 1]) ++sl;
+            r = rs.rarea[rs.rbase[sl] + (i - rs.rofs[sl])];
+          } else {
+            r = srec[i];
+          }
+          slist_out[i] = r.x;  // (the list the compaction and the next supersteps read)
+        } else {
+          r = srec[i];
+        }
         u = r.x;
         Tu = static_cast<uint16_t>(r.y);
         dm = r.z;
@@ -2010,10 +2034,11 @@ void build_tiling(Ctx& c) {
   // record slices of the superstep-0 waves (dense mode): each wave's bound is the rows of the light tiles
   // it visits (tile t goes to wave (t / kTileBlock) % W of a persistent grid of W waves)
   {
-    void* ptrs[] = {c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.d_hrec, c.d_srec, c.d_rscan_tmp};
+    void* ptrs[] = {c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.d_hrec, c.d_srec, c.d_rscan_tmp, c.d_cdesc};
     for (void* q : ptrs)
       if (q) (void)hipFree(q);
     c.d_rarea = c.d_hrec = c.d_srec = nullptr;
+    c.d_cdesc = nullptr;
     c.d_rbase = c.d_rofs = nullptr;
     c.d_rcnt = nullptr;
     c.d_rscan_tmp = nullptr;
@@ -2200,6 +2225,29 @@ __global__ void k_slist_heavy(const uint4* __restrict__ hrec, uint32_t nheavy, c
   }
 }
 
+// Records in place (one context): the slice holding the first record of each 64-record chunk of the slices'
+// concatenation, rofs[W] = the number of light records, and the list count (the heavy survivors are appended
+// after them by k_slist_heavy).
+__global__ void k_chunk_slices(const uint64_t* __restrict__ rofs_in, const uint32_t* __restrict__ rcnt, uint32_t W,
+                               uint64_t* __restrict__ rofs, uint32_t* __restrict__ cdesc, uint32_t* __restrict__ nS) {
+  const uint64_t total = rofs_in[W - 1] + rcnt[W - 1];
+  const uint64_t nch = (total + kWave - 1) / kWave;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rofs[W] = total;
+    *nS = static_cast<uint32_t>(total);
+  }
+  for (uint64_t ch = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; ch < nch; ch += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t o0 = ch * kWave;
+    uint32_t lo = 0, hi = W - 1;  // the last slice starting at or before o0 (empty slices share offsets)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (rofs_in[mid] <= o0) lo = mid;
+      else hi = mid - 1;
+    }
+    cdesc[ch] = lo;
+  }
+}
+
 // heavy-row scratch, heavy records and the 2-bit codes of a superstep-0 launch (queued with the search's reset)
 void queue_lcc_first_fills(Ctx& c) {
   if (c.ntiles == 0) return;
@@ -2236,8 +2284,17 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
     size_t tb = c.rscan_tmp_bytes;
     PM_HIP_CHECK(rocprim::exclusive_scan(c.d_rscan_tmp, tb, rit, c.d_rofs, uint64_t(0), size_t(c.rwaves),
                                          rocprim::plus<uint64_t>(), c.stream));
-    hipLaunchKernelGGL(k_slist_from_records, dim3(grid_for(c.rwaves, kWpb, 8192)), dim3(kBlock), 0, c.stream,
-                       c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.rwaves, c.d_srec, c.d_slist, c.d_nS);
+    // one context: the first later superstep reads the records in place (no copy); a sharded context packs the
+    // survivors' codes from slist before that superstep, so it copies
+    c.records_in_place = !c.comm;
+    if (c.records_in_place) {
+      if (!c.d_cdesc) PM_HIP_CHECK(hipMalloc(&c.d_cdesc, (c.rarea_cap / kWave + 2) * sizeof(uint32_t)));
+      hipLaunchKernelGGL(k_chunk_slices, dim3(grid_for(c.rarea_cap / kWave + 1, kBlock, 1024)), dim3(kBlock), 0,
+                         c.stream, c.d_rofs, c.d_rcnt, c.rwaves, c.d_rofs, c.d_cdesc, c.d_nS);
+    } else {
+      hipLaunchKernelGGL(k_slist_from_records, dim3(grid_for(c.rwaves, kWpb, 8192)), dim3(kBlock), 0, c.stream,
+                         c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.rwaves, c.d_srec, c.d_slist, c.d_nS);
+    }
     if (c.nheavy)
       hipLaunchKernelGGL(k_slist_heavy, dim3(grid_for(c.nheavy, kBlock, 1024)), dim3(kBlock), 0, c.stream, c.d_hrec,
                          c.nheavy, c.d_tst, c.d_srec, c.d_slist, c.d_nS);
@@ -2334,11 +2391,14 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   const unsigned long long* min = c.smask_valid ? reinterpret_cast<const unsigned long long*>(c.d_smask[c.smask_cur])
                                                 : nullptr;
   auto* mout = reinterpret_cast<unsigned long long*>(c.d_smask[c.smask_cur ^ 1]);
+  RecSrc rs{};
+  if (first_after_ss0 && c.k1_records && c.records_in_place)
+    rs = RecSrc{c.d_rarea, c.d_rbase, c.d_rofs, c.d_cdesc, c.rwaves};
   hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                      c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,
-                     reinterpret_cast<unsigned long long*>(c.d_kmask));
+                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist);
   PM_HIP_CHECK(hipGetLastError());
   c.k1_dense = false;  // every M row of S is in its padded row from here on
   c.k1_records = false;
