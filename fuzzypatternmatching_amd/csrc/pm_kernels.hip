@@ -1015,7 +1015,7 @@ struct RecSrc {
   const uint4* rarea;
   const uint64_t* rbase;
   const uint64_t* rofs;
-  const uint32_t* cdesc;
+  const uint4* cdesc;  // per chunk {rarea index of its first record (lo, hi), its records in that slice, next slice}
   uint32_t W;
 };
 #ifndef PM_STEP_UNROLL
@@ -1088,10 +1088,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
       uint32_t l, dm = kNone;
       if (srec) {  // dense superstep-0 output: the records, in slist order (coalesced)
         uint4 r;
-        if (rs.rarea) {  // in place: the chunk's slice, then the lane's (a slice may end inside the chunk)
-          const uint64_t nl = rs.rofs[rs.W];
-          if (i < nl) {
-            uint32_t sl = rs.cdesc[chunk];
+        if (rs.rarea) {  // in place: the chunk's first slice, a later one for lanes past its end (rare)
+          const uint4 d = rs.cdesc[chunk];
+          if (static_cast<uint32_t>(lane) < d.z) {
+            r = rs.rarea[((uint64_t(d.y) << 32) | d.x) + lane];
+          } else if (i < rs.rofs[rs.W]) {
+            uint32_t sl = d.w;
             while (i >= rs.rofs[sl + 1]) ++sl;
             r = rs.rarea[rs.rbase[sl] + (i - rs.rofs[sl])];
           } else {
@@ -2228,8 +2230,9 @@ __global__ void k_slist_heavy(const uint4* __restrict__ hrec, uint32_t nheavy, c
 // Records in place (one context): the slice holding the first record of each 64-record chunk of the slices'
 // concatenation, rofs[W] = the number of light records, and the list count (the heavy survivors are appended
 // after them by k_slist_heavy).
-__global__ void k_chunk_slices(const uint64_t* __restrict__ rofs_in, const uint32_t* __restrict__ rcnt, uint32_t W,
-                               uint64_t* __restrict__ rofs, uint32_t* __restrict__ cdesc, uint32_t* __restrict__ nS) {
+__global__ void k_chunk_slices(const uint64_t* __restrict__ rofs_in, const uint32_t* __restrict__ rcnt,
+                               const uint64_t* __restrict__ rbase, uint32_t W, uint64_t* __restrict__ rofs,
+                               uint4* __restrict__ cdesc, uint32_t* __restrict__ nS) {
   const uint64_t total = rofs_in[W - 1] + rcnt[W - 1];
   const uint64_t nch = (total + kWave - 1) / kWave;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2244,7 +2247,10 @@ __global__ void k_chunk_slices(const uint64_t* __restrict__ rofs_in, const uint3
       if (rofs_in[mid] <= o0) lo = mid;
       else hi = mid - 1;
     }
-    cdesc[ch] = lo;
+    const uint64_t end = lo + 1 < W ? rofs_in[lo + 1] : total;  // (rofs[W] is being written by thread 0)
+    const uint64_t b = rbase[lo] + (o0 - rofs_in[lo]);
+    cdesc[ch] = make_uint4(static_cast<uint32_t>(b), static_cast<uint32_t>(b >> 32),
+                           static_cast<uint32_t>(min<uint64_t>(kWave, end - o0)), lo + 1);
   }
 }
 
@@ -2288,9 +2294,9 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
     // survivors' codes from slist before that superstep, so it copies
     c.records_in_place = !c.comm;
     if (c.records_in_place) {
-      if (!c.d_cdesc) PM_HIP_CHECK(hipMalloc(&c.d_cdesc, (c.rarea_cap / kWave + 2) * sizeof(uint32_t)));
+      if (!c.d_cdesc) PM_HIP_CHECK(hipMalloc(&c.d_cdesc, (c.rarea_cap / kWave + 2) * sizeof(uint4)));
       hipLaunchKernelGGL(k_chunk_slices, dim3(grid_for(c.rarea_cap / kWave + 1, kBlock, 1024)), dim3(kBlock), 0,
-                         c.stream, c.d_rofs, c.d_rcnt, c.rwaves, c.d_rofs, c.d_cdesc, c.d_nS);
+                         c.stream, c.d_rofs, c.d_rcnt, c.d_rbase, c.rwaves, c.d_rofs, c.d_cdesc, c.d_nS);
     } else {
       hipLaunchKernelGGL(k_slist_from_records, dim3(grid_for(c.rwaves, kWpb, 8192)), dim3(kBlock), 0, c.stream,
                          c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.rwaves, c.d_srec, c.d_slist, c.d_nS);
