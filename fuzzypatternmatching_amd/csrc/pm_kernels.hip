@@ -1089,13 +1089,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
       if (srec) {  // dense superstep-0 output: the records, in slist order (coalesced)
         uint4 r;
         if (rs.rarea) {  // in place: the chunk's first slice, a later one for lanes past its end (rare)
-          const uint4 d = rs.cdesc[chunk];
-          if (static_cast<uint32_t>(lane) < d.z) {
-            r = rs.rarea[((uint64_t(d.y) << 32) | d.x) + lane];
-          } else if (i < rs.rofs[rs.W]) {
-            uint32_t sl = d.w;
-            while (i >= rs.rofs[sl + 1]) ++sl;
-            r = rs.rarea[rs.rbase[sl] + (i - rs.rofs[sl])];
+          // (descriptors exist for the light records' chunks only: the heavy records after them are in srec)
+          const uint64_t nl = rs.rofs[rs.W];
+          if (i < nl) {
+            const uint4 d = rs.cdesc[chunk];
+            if (static_cast<uint32_t>(lane) < d.z) {
+              r = rs.rarea[((uint64_t(d.y) << 32) | d.x) + lane];
+            } else {
+              uint32_t sl = d.w;
+              while (i >= rs.rofs[sl + 1]) ++sl;
+              r = rs.rarea[rs.rbase[sl] + (i - rs.rofs[sl])];
+            }
           } else {
             r = srec[i];
           }
