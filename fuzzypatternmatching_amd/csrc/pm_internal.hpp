@@ -396,7 +396,8 @@ struct Ctx {
   uint4* d_hrec = nullptr;        // heavy rows' records (w = 1: survivor)
   uint4* d_srec = nullptr;        // records in slist order (the first later superstep)
   uint4* d_cdesc = nullptr;       // one context: where each 64-record chunk lies (records read in place, k_chunk_slices)
-  bool records_in_place = false;  // the first later superstep reads the records from the superstep-0 slices
+  bool records_in_place = false;
+  bool removed_cleared = false;   // the last pull superstep cleared its removed rows' T_pub (records mode)  // the first later superstep reads the records from the superstep-0 slices
   uint64_t rarea_cap = 0, srec_cap = 0;
   uint32_t rwaves = 0;            // waves of the superstep-0 grid the slices were sized for
   void* d_rscan_tmp = nullptr;

@@ -2410,6 +2410,7 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
                      c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,
                      reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist);
   PM_HIP_CHECK(hipGetLastError());
+  c.removed_cleared = first_after_ss0 && c.k1_records;  // (its removed rows cleared the T_pub they read)
   c.k1_dense = false;  // every M row of S is in its padded row from here on
   c.k1_records = false;
   reduce_into(c, grid, d_slot);
@@ -2453,18 +2454,31 @@ __global__ void k_live_keep(const uint32_t* __restrict__ slist, const unsigned l
 // The same from the superstep's own keep mask (k_lcc_step keep_out): no T_pub gather; the slist entries are
 // read only for live entries that were not kept (removed now: the buffer the superstep read is cleared).
 // One lane per chunk.
+// PER_ENTRY: one thread per entry (the removed entries of a chunk cleared in parallel: after the second later
+// superstep almost every entry goes); else one thread per chunk (after the first, whose removed rows cleared their
+// T_pub themselves: few entries go, and a thread per entry would only read the masks).
+template <bool PER_ENTRY>
 __global__ void k_live_keep_masks(const uint32_t* __restrict__ slist, const unsigned long long* __restrict__ mask,
                                   const unsigned long long* __restrict__ keep, const uint32_t* __restrict__ nSp,
                                   uint64_t cap, uint16_t* __restrict__ told, uint32_t* __restrict__ cnt) {
   const uint64_t nch = min(cap, (static_cast<uint64_t>(*nSp) + kWave - 1) / kWave);
-  for (uint64_t c = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; c < nch; c += uint64_t(gridDim.x) * blockDim.x) {
-    const unsigned long long k = keep[c];
-    cnt[c] = static_cast<uint32_t>(__builtin_popcountll(k));
-    unsigned long long gone = mask[c] & ~k;
-    while (gone) {
-      const int b = __builtin_ctzll(gone);
-      gone &= gone - 1;
-      told[slist[c * kWave + b]] = 0;
+  const uint64_t n = PER_ENTRY ? nch * kWave : nch;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    if (PER_ENTRY) {
+      const uint64_t c = i / kWave;
+      const uint32_t b = static_cast<uint32_t>(i % kWave);
+      const unsigned long long k = keep[c];
+      if (b == 0) cnt[c] = static_cast<uint32_t>(__builtin_popcountll(k));
+      if (((mask[c] & ~k) >> b) & 1ull) told[slist[i]] = 0;
+    } else {
+      const unsigned long long k = keep[i];
+      cnt[i] = static_cast<uint32_t>(__builtin_popcountll(k));
+      unsigned long long gone = mask[i] & ~k;
+      while (gone) {
+        const int b = __builtin_ctzll(gone);
+        gone &= gone - 1;
+        told[slist[i * kWave + b]] = 0;
+      }
     }
   }
 }
@@ -2507,8 +2521,12 @@ void launch_compact_slist(Ctx& c) {
   // cleared at its live entries that were not kept (after launch_lcc_step: tpub[cur] was just written,
   // tpub[cur ^ 1] was read)
   auto* kmask = reinterpret_cast<unsigned long long*>(c.d_kmask);
-  hipLaunchKernelGGL(k_live_keep_masks, dim3(grid_for(cap, kBlock, 2048)), dim3(kBlock), 0, c.stream, c.d_slist,
-                     mask, kmask, c.d_nS, cap, c.d_tpub[c.cur ^ 1], c.d_ccnt);
+  if (c.removed_cleared)
+    hipLaunchKernelGGL(k_live_keep_masks<false>, dim3(grid_for(cap, kBlock, 2048)), dim3(kBlock), 0, c.stream,
+                       c.d_slist, mask, kmask, c.d_nS, cap, c.d_tpub[c.cur ^ 1], c.d_ccnt);
+  else
+    hipLaunchKernelGGL(k_live_keep_masks<true>, dim3(grid_for(cap * kWave, kBlock, 8192)), dim3(kBlock), 0, c.stream,
+                       c.d_slist, mask, kmask, c.d_nS, cap, c.d_tpub[c.cur ^ 1], c.d_ccnt);
   size_t tb = c.ctmp_bytes;
   PM_HIP_CHECK(rocprim::exclusive_scan(c.d_ctmp, tb, c.d_ccnt, c.d_cbase, 0u, size_t(cap), rocprim::plus<uint32_t>(),
                                        c.stream));
