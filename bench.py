@@ -96,6 +96,10 @@ def main():
     ap.add_argument("--pmc", default=None, help="PMC summary of k_lcc_first (default: the newest profiles/r*_pmc_lcc_first.json)")
     ap.add_argument("--c3", choices=["auto", "off"], default="auto",
                     help="also time BASELINE config C3 (S=26, P_gen=4, 4-cycle: the token-passing stress) at N=1")
+    ap.add_argument("--nlcc", choices=["auto", "off"], default="auto",
+                    help="also time the token-passing path with real work at N=1: config C5's search (S=27, "
+                         "hash32(v ^ 5) % 256 labels, 4-cycle) on the GPU-generated graph, checked against "
+                         "tests/golden/rmat_s27_p8_cycle4_hash256.json")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -290,6 +294,62 @@ def main():
         log(f"C3 S=26 4-cycle: {c3['ms_per_step']} ms/step, {c3['value'] / 1e9:.2f} G edges/s, "
             f"NLC lines {c3['nlcc_ms_per_step']} ms ({c3['nlcc_share']:.0%})")
 
+    # the token-passing path with real work: config C5's search (S=27, explicit hash labels, 4-cycle) on the
+    # GPU-generated graph, checked against the oracle's digest of the same search
+    nlcc = None
+    if args.nlcc == "auto" and world == 1 and not sharded:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import pmtest
+        cyc = os.path.join(ROOT, "patterns", "rmat_log2_cycle4_pattern")
+        s5, p5, alphabet, salt = 27, 8, 256, 5
+        m5, g5 = pm.rmat_matcher(s5, p5, cyc, device=0)
+        t5 = time.perf_counter()
+        m5.set_labels(pmtest.hash_labels(1 << s5, alphabet, salt=salt))
+        lay5 = time.perf_counter() - t5
+        f5 = m5.run_beta("", args.max_iterations)
+        m5.run_beta("", args.max_iterations)
+        raw5 = [_abi.RunStats() for _ in range(5)]
+        t5 = time.perf_counter()
+        for st5 in raw5:
+            m5.run_beta_into(st5, args.max_iterations)
+        e5 = (time.perf_counter() - t5) / len(raw5)
+        r5 = [x.as_dict() for x in raw5]
+        last = r5[-1]
+        nl_s = sum(r["nlcc_seconds"] for r in r5) / len(r5)
+        nlcc = {"workload": f"R-MAT scale-{s5} (P_gen={p5}), labels hash32(v ^ {salt}) % {alphabet} (config C5's "
+                            f"explicit labels, generated instead of ingested), rmat_log2_cycle4_pattern (4 cycle-check "
+                            f"lines + TDS line), one GPU",
+                "value": round(edges_of(last) / e5, 1), "unit": "edges/s", "ms_per_step": round(e5 * 1e3, 3),
+                "steps": len(r5), "edges_per_step": edges_of(last), "lcc_edges": last["lcc_edges"],
+                "path_cycle_edges": last["nlcc_edges"], "tds_edges": last["tds_edges"], "walks": last["walks"],
+                "iterations": last["iterations"], "split_lines": last["split_lines"],
+                "line_overflows": last["line_overflows"], "exact_lines": last["exact_lines"],
+                "nlc_lines_ms_per_step": round(nl_s * 1e3, 3), "nlc_lines_share": round(nl_s / e5, 4),
+                "path_cycle_and_tds_edges_per_s_in_lines": round((last["nlcc_edges"] + last["tds_edges"]) /
+                                                                 max(nl_s, 1e-9), 1),
+                "first_search_s": round(f5["seconds"], 4), "generate_rmat_gpu_s": round(g5, 3),
+                "labels_and_layout_s": round(lay5, 3)}
+        fx5 = os.path.join(ROOT, "tests", "golden", f"rmat_s{s5}_p{p5}_cycle4_hash{alphabet}.json")
+        if os.path.exists(fx5):
+            fx = json.load(open(fx5))
+            td = tempfile.mkdtemp(prefix="pmbench5")
+            sf = m5.run_beta(td, args.max_iterations)
+            diffs = pmtest.digest_diffs(fx["digest"], pmtest.result_digest(td, fx["nranks"]))
+            for k_g, k_o in (("final_vertices", "final_vertices"), ("final_edges", "final_edges"),
+                             ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"), ("tds_edges", "tds_edges"),
+                             ("walks", "paths"), ("iterations", "iterations")):
+                if sf[k_g] != fx["stats"][k_o] or last[k_g] != fx["stats"][k_o]:
+                    diffs.append(f"{k_g}: gpu {last[k_g]}/{sf[k_g]} != oracle {fx['stats'][k_o]}")
+            import shutil
+            shutil.rmtree(td, ignore_errors=True)
+            nlcc["fixture"] = {"file": os.path.relpath(fx5, ROOT), "match": not diffs}
+            if diffs:
+                invalid.append("C5-like search differs from the oracle's fixture: " + "; ".join(diffs[:4]))
+        m5.close()
+        log(f"NLCC config (S=27 hash-256 4-cycle): {nlcc['ms_per_step']} ms/step, {nlcc['value'] / 1e9:.2f} G edges/s, "
+            f"lines {nlcc['nlc_lines_ms_per_step']} ms ({nlcc['nlc_lines_share']:.0%}), fixture "
+            f"{nlcc.get('fixture', {}).get('match')}")
+
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -382,6 +442,7 @@ def main():
         "cpu_baseline": cpu,
         "fixture": fixture,
         "c3_config": c3,
+        "nlcc_config": nlcc,
         # one-time work outside the timed region (the reference's graph load + label init analogue)
         "setup_s": setup,
     }

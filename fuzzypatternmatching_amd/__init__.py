@@ -17,7 +17,8 @@ from . import _abi
 
 __all__ = ["Graph", "rmat_graph", "rmat_matcher", "rmat_shard_matcher", "mt19937_jump_outputs", "rmat_edges",
            "pattern_summary", "write_graph", "read_graph", "PatternMatcher", "ShardedPatternMatcher", "partition_edges",
-           "comm_unique_id", "run_beta_local_shards", "run_rmat_local_shards", "PMError"]
+           "comm_unique_id", "run_beta_local_shards", "run_rmat_local_shards", "run_rmat_local_shards_each",
+           "TorchHostComm", "PMError"]
 
 DEFAULT_HUB_THRESHOLD = 1048576  # generate_rmat.cpp:106
 
@@ -229,6 +230,23 @@ def run_rmat_local_shards(scale, p_gen, pattern_dir, nshards, result_dir="", max
     return st.as_dict()
 
 
+def run_rmat_local_shards_each(scale, p_gen, pattern_dir, nshards, result_dir="", max_iterations=0, device=0,
+                               nranks=1, hub_threshold=DEFAULT_HUB_THRESHOLD, labels=None, repeats=1):
+    """run_rmat_local_shards with labels (None: degree labels), the search repeated `repeats` times (result
+    files from the first run) and every shard's statistics of the last run: a list of nshards dicts (the
+    shard_* fields give the partition balance and each shard's device time of the sharded part)."""
+    if result_dir:
+        os.makedirs(result_dir, exist_ok=True)
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.uint64)
+    st = (_abi.RunStats * nshards)()
+    rc = _lib().pm_run_rmat_local_shards2(scale, p_gen, pattern_dir.encode(), device, nshards, nranks, hub_threshold,
+                                          None if lab is None else lab.ctypes.data, result_dir.encode(),
+                                          max_iterations, repeats, st)
+    if rc != 0:
+        raise _err()
+    return [s.as_dict() for s in st]
+
+
 def pattern_summary(pattern_dir):
     """Parsed pattern directory (graph.hpp / pattern_util.hpp rules) as a dict."""
     import json
@@ -417,14 +435,77 @@ def edge_list_matcher(files, pattern_dir, undirected=False, device=0, nranks=1,
     return m, secs.value
 
 
+class TorchHostComm:
+    """pm_host_comm (include/pm_abi.h) over a torch.distributed process group: the sharded search's
+    collectives staged through host memory and carried by the group's backend (gloo on CPU tensors) --
+    the exchange a maintainer binds to MPI_Allgather / MPI_Allreduce / MPI_Alltoallv in the reference's
+    own MPI world.  The processes may share one device."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self._torch, self._dist, self._group = torch, dist, group
+        self.nshards = dist.get_world_size(group)
+        self.shard = dist.get_rank(group)
+        self.error = None
+        # the ctypes callbacks must outlive the context that calls them
+        self._cbs = (_abi.HostAllgather(self._guard(self._allgather)),
+                     _abi.HostAllreduce64(self._guard(self._allreduce64)),
+                     _abi.HostAllreduce32(self._guard(self._allreduce32)),
+                     _abi.HostAlltoallv(self._guard(self._alltoallv)))
+        self.struct = _abi.HostComm(None, self.nshards, self.shard, *self._cbs)
+
+    def _guard(self, fn):
+        def call(*a):
+            try:
+                fn(*a)
+                return 0
+            except Exception as ex:  # noqa: BLE001 (reported through the C-ABI's status)
+                self.error = ex
+                return 1
+        return call
+
+    def _u8(self, addr, nbytes):
+        return self._torch.frombuffer((ctypes.c_char * nbytes).from_address(addr), dtype=self._torch.uint8)
+
+    def _allgather(self, user, send, recv, nbytes):
+        if not nbytes:
+            return
+        out = self._u8(recv, nbytes * self.nshards)
+        self._dist.all_gather(list(out.split(nbytes)), self._u8(send, nbytes), group=self._group)
+
+    def _allreduce64(self, user, buf, count):
+        if count:
+            t = self._torch.frombuffer((ctypes.c_int64 * count).from_address(buf), dtype=self._torch.int64)
+            self._dist.all_reduce(t, group=self._group)  # (two's complement: the u64 sum wraps alike)
+
+    def _allreduce32(self, user, buf, count):
+        if count:
+            t = self._torch.frombuffer((ctypes.c_int32 * count).from_address(buf), dtype=self._torch.int32)
+            w = t.to(self._torch.int64) & 0xFFFFFFFF
+            self._dist.all_reduce(w, group=self._group)
+            t.copy_(((w & 0xFFFFFFFF) - ((w & 0x80000000) << 1)).to(self._torch.int32))
+
+    def _alltoallv(self, user, send, sbytes, recv, rbytes):
+        G = self.nshards
+        sb = [int(x) for x in (ctypes.c_uint64 * G).from_address(sbytes)]
+        rb = [int(x) for x in (ctypes.c_uint64 * G).from_address(rbytes)]
+        empty = self._torch.empty(0, dtype=self._torch.uint8)
+        inp = self._u8(send, sum(sb)) if sum(sb) else empty
+        out = self._u8(recv, sum(rb)) if sum(rb) else empty
+        self._dist.all_to_all_single(out, inp, rb, sb, group=self._group)
+
+
 class ShardedPatternMatcher(PatternMatcher):
     """One rank of a sharded search (one process per GPU; RCCL between the shards).
 
     off/col/degree come from partition_edges(); unique_id from comm_unique_id() on one rank,
-    distributed to all.  Construction, run_beta, set_labels and export_state are collective."""
+    distributed to all.  Construction, run_beta, set_labels and export_state are collective.
+    host_comm=TorchHostComm(group) (instead of unique_id) carries the exchanges through the host over a
+    torch.distributed group (pm_create_shard_host_comm): processes that share a device, or a host transport."""
 
-    def __init__(self, n, off, col, degree, pattern_dir, nshards, shard, unique_id, device=0, nranks=1,
-                 hub_threshold=DEFAULT_HUB_THRESHOLD, symmetric=True):
+    def __init__(self, n, off, col, degree, pattern_dir, nshards, shard, unique_id=None, device=0, nranks=1,
+                 hub_threshold=DEFAULT_HUB_THRESHOLD, symmetric=True, host_comm=None):
         self._off = np.ascontiguousarray(off, dtype=np.uint64)
         self._col = np.ascontiguousarray(col if len(col) else np.zeros(1, np.uint32), dtype=np.uint32)
         self._deg = np.ascontiguousarray(degree, dtype=np.uint32)
@@ -432,7 +513,12 @@ class ShardedPatternMatcher(PatternMatcher):
         self.graph.n = int(n)
         self._sdesc = _abi.ShardDesc(n, self._off.ctypes.data, self._col.ctypes.data, self._deg.ctypes.data,
                                      int(symmetric), nranks, hub_threshold, nshards, shard)
-        uid = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
-        self._ctx = _lib().pm_create_shard(ctypes.byref(self._sdesc), pattern_dir.encode(), device, uid)
+        self._host_comm = host_comm
+        if host_comm is not None:
+            self._ctx = _lib().pm_create_shard_host_comm(ctypes.byref(self._sdesc), pattern_dir.encode(), device,
+                                                         ctypes.byref(host_comm.struct))
+        else:
+            uid = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
+            self._ctx = _lib().pm_create_shard(ctypes.byref(self._sdesc), pattern_dir.encode(), device, uid)
         if not self._ctx:
             raise _err()

@@ -42,6 +42,25 @@ class ShardDesc(ctypes.Structure):
     ]
 
 
+# pm_host_comm callbacks (include/pm_abi.h): host buffers, 0 on success
+HostAllgather = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, c_vp, c_u64)
+HostAllreduce64 = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, c_u64)
+HostAllreduce32 = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, c_u64)
+HostAlltoallv = ctypes.CFUNCTYPE(ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp)
+
+
+class HostComm(ctypes.Structure):
+    _fields_ = [
+        ("user", c_vp),
+        ("nshards", c_u32),
+        ("shard", c_u32),
+        ("allgather", HostAllgather),
+        ("allreduce_sum_u64", HostAllreduce64),
+        ("allreduce_sum_u32", HostAllreduce32),
+        ("alltoallv", HostAlltoallv),
+    ]
+
+
 class LccStats(ctypes.Structure):
     _fields_ = [
         ("supersteps", c_u64),
@@ -85,6 +104,20 @@ class RunStats(ctypes.Structure):
         ("tds_chunks", c_u64),
         ("nlcc_seconds", ctypes.c_double),
         ("split_lines", c_u64),
+        ("line_overflows", c_u64),
+        ("exact_lines", c_u64),
+        ("shard_entries", c_u64),
+        ("shard_rows", c_u64),
+        ("shard_hub_entries", c_u64),
+        ("shard_hubs_controlled", c_u64),
+        ("shard_ss0_entries", c_u64),
+        ("shard_ss0_survivors", c_u64),
+        ("shard_sharded_ms", ctypes.c_double),
+        ("comm_calls", c_u64),
+        ("comm_bytes", c_u64),
+        ("replica_rows", c_u64),
+        ("replica_entries", c_u64),
+        ("comm_seconds", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -121,6 +154,8 @@ SIGNATURES = [
     ("pm_build_arch", c_char_p, []),
     ("pm_comm_unique_id", ctypes.c_int, [c_vp, c_u64]),
     ("pm_create_shard", c_vp, [ctypes.POINTER(ShardDesc), c_char_p, ctypes.c_int, c_vp]),
+    ("pm_create_shard_host_comm", c_vp, [ctypes.POINTER(ShardDesc), c_char_p, ctypes.c_int,
+                                         ctypes.POINTER(HostComm)]),
     ("pm_run_beta_local_shards", ctypes.c_int, [ctypes.POINTER(GraphDesc), c_char_p, ctypes.c_int, c_u32, c_vp,
                                                 c_char_p, c_u64, ctypes.POINTER(RunStats)]),
     ("pm_rmat_edges", ctypes.c_int, [c_u64, c_u64, c_u64, c_u64, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
@@ -132,6 +167,8 @@ SIGNATURES = [
                                     ctypes.POINTER(ctypes.c_double)]),
     ("pm_run_rmat_local_shards", ctypes.c_int, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u32, c_u64, c_char_p,
                                                 c_u64, ctypes.POINTER(RunStats)]),
+    ("pm_run_rmat_local_shards2", ctypes.c_int, [c_u64, c_u64, c_char_p, ctypes.c_int, c_u32, c_u32, c_u64, c_vp,
+                                                 c_char_p, c_u64, c_u32, ctypes.POINTER(RunStats)]),
     ("pm_mt19937_jump_outputs", ctypes.c_int, [c_u32, c_u64, c_vp, c_u64]),
     ("pm_vertex_data_files", ctypes.c_int, [c_vp, c_char_p]),
     ("pm_graph_size", ctypes.c_int, [c_vp, ctypes.POINTER(c_u64), ctypes.POINTER(c_u64), ctypes.POINTER(ctypes.c_int)]),

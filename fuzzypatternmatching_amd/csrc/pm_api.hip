@@ -88,6 +88,7 @@ struct CtxInput {
   uint32_t nshards = 1, shard = 0;
   Comm* comm = nullptr;            // ownership passes to the context
   bool col_on_device = false;      // col is device memory (GPU-built graph); off stays host
+  bool col_release = false;        // ... and the context frees it once copied (the caller must not)
   uint32_t inprocess_shards = 1;   // shards of this process on the same device (ThreadComm groups)
   const uint64_t* in_off = nullptr;  // directed graphs: in-rows built by the caller (host offsets,
   const uint32_t* in_col = nullptr;  // columns where col lives), e.g. by the GPU ingest
@@ -110,17 +111,10 @@ static void transpose_csr(uint64_t n, const uint64_t* off, const uint32_t* col, 
     for (uint64_t e = off[v]; e < off[v + 1]; ++e) tcol[at[col[e]]++] = static_cast<uint32_t>(v);
 }
 
-// Degree labels (vertex_data_db_degree.hpp:109) from the global out-degrees.
+// Degree labels (vertex_data_db_degree.hpp:109) from the global out-degrees (host: the layout uploads them).
 static void set_degree_labels(Ctx& c) {
   c.labels_host.assign(c.n, 0);
   for (uint64_t v = 0; v < c.n; ++v) c.labels_host[v] = degree_label(c.deg_host[v]);
-  if (c.symmetric) {
-    launch_degree_labels(c);  // d_off holds the (global) degrees
-  } else {
-    PM_HIP_CHECK(hipMemcpyAsync(c.d_labels, c.labels_host.data(), c.n * sizeof(uint64_t), hipMemcpyHostToDevice,
-                                c.stream));
-  }
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
 }
 
 // Host pages registered with the runtime for the lifetime of the object (large
@@ -147,6 +141,15 @@ struct PinnedRange {
 
 static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int device) {
   std::unique_ptr<Comm> comm(in.comm);
+  // a device-resident input the caller handed over (col_release) is freed as soon as it is copied
+  struct ColRelease {
+    const uint32_t* p;
+    void now() {
+      if (p) (void)hipFree(const_cast<uint32_t*>(p));
+      p = nullptr;
+    }
+    ~ColRelease() { now(); }
+  } col_release{in.col_on_device && in.col_release ? in.col : nullptr};
   if (!in.off || !in.col) throw std::runtime_error("pm_create: null graph");
   if (in.nshards == 0 || in.shard >= in.nshards) throw std::runtime_error("pm_create: bad shard index");
   if (in.nshards > 1 && !comm) throw std::runtime_error("pm_create: sharded context without a communicator");
@@ -204,8 +207,9 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
     if (pl >= 4 || l.valid_cycle)  // the reference applies it in nem_1 path checks only
       throw std::runtime_error("pattern_nlc selected_vertices=1 is supported on path lines (index < 4, valid_cycle 0)");
   }
-  // global degrees (labels, hubs, layout order) and offsets of the rows scanned here
+  // global degrees (labels, hubs, layout order) and the lengths of the rows held here
   c->deg_host.resize(c->n);
+  if (in.gdeg) c->ldeg_host.reserve(c->n);
   for (uint64_t v = 0; v < c->n; ++v) {
     const uint64_t d = in.gdeg ? in.gdeg[v] : in.off[v + 1] - in.off[v];
     if (d > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
@@ -217,22 +221,17 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
                                "and delegate rows (degree >= hub threshold) split by target owner");
     c->deg_host[v] = static_cast<uint32_t>(d);
     if (d >= c->hub_threshold) c->hubs_host.push_back(v);
+    if (in.gdeg) c->ldeg_host.push_back(static_cast<uint32_t>(ld));
+    c->held_rows += ld != 0;
+    if (ld && d >= c->hub_threshold && c->nshards > 1) c->held_hub_entries += ld;
   }
   c->split_hubs = c->nshards > 1 && !c->hubs_host.empty();
   for (uint64_t j = c->shard; c->split_hubs && j < c->hubs_host.size(); j += c->nshards)
     c->hub_area += c->deg_host[c->hubs_host[j]];
-  std::vector<uint64_t> goff;
-  if (in.gdeg) {
-    goff.assign(c->n + 1, 0);
-    for (uint64_t v = 0; v < c->n; ++v) goff[v + 1] = goff[v] + in.gdeg[v];
-  }
-  const uint64_t* off_all = in.gdeg ? goff.data() : soff;
   // device graph + state; padded slot count of the rows scanned here (label independent)
   c->nq = 0;
   for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(soff[v + 1] - soff[v]);
   c->mcap = c->nq;
-  c->d_off = dalloc<uint64_t>(c->n + 1);
-  c->d_offl = in.gdeg ? dalloc<uint64_t>(c->n + 1) : c->d_off;
   c->d_offp = dalloc<uint64_t>(c->n + 1);
   c->d_offr = dalloc<uint64_t>(c->n + 1);
   // slot buffers carry kTileEntries entries of tail padding (superstep-0 tile loads read whole tiles)
@@ -243,17 +242,10 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
   c->d_perm = dalloc<uint32_t>(c->n);
   c->d_pos = dalloc<uint32_t>(c->n);
-  c->d_labs = dalloc<uint64_t>(c->n);
-  {
-    PinnedRange pin(off_all, (c->n + 1) * sizeof(uint64_t));
-    PM_HIP_CHECK(hipMemcpy(c->d_off, off_all, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
-  }
-  if (in.gdeg) PM_HIP_CHECK(hipMemcpy(c->d_offl, soff, (c->n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice));
   if (!c->hubs_host.empty()) {
     c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
     PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   }
-  c->d_labels = dalloc<uint64_t>(c->n);
   c->d_tpub[0] = dalloc<uint16_t>(c->n);
   c->d_tpub[1] = dalloc<uint16_t>(c->n);
   c->d_tst = dalloc<uint16_t>(c->n);
@@ -277,6 +269,9 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (in.inprocess_shards > 1)  // in-process shard groups share one device
     arena = std::min<size_t>(arena, std::max<size_t>(size_t(1) << 30, free_b / (2 * in.inprocess_shards)));
   arena = std::max<size_t>(arena, size_t(64) << 20);
+  // one size on every shard: the replicated lines' walk storage and TDS chunk caps come from it, and a line
+  // that overflowed on some shards only would send those into collectives the others never make
+  arena = static_cast<size_t>(shard_agree_min(*c, arena));
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
@@ -285,6 +280,8 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
   c->any_sv = any_sv;
   if (const char* e = std::getenv("PM_SPLIT_LINES")) c->split_min = std::strtoull(e, nullptr, 10);
+  if (const char* e = std::getenv("PM_HASH_SLOTS")) c->hash_slots = std::strtoull(e, nullptr, 10);
+  if (const char* e = std::getenv("PM_DEBUG_NOGROW_SHARD")) c->nogrow_shard = std::strtoll(e, nullptr, 10);
   // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
   // asymmetric M then aborts the search: tests use it to find such inputs)
   if (const char* e = std::getenv("PM_FORCE_PULL")) c->force_pull = std::string(e) == "1" && c->symmetric;
@@ -293,6 +290,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (c->nnz) {
     if (in.col_on_device) {
       PM_HIP_CHECK(hipMemcpy(c->d_mcol, scol, c->nnz * sizeof(uint32_t), hipMemcpyDeviceToDevice));
+      col_release.now();
     } else {
       // pinned staging: the caller's pages are registered for the copy, so the
       // adjacency moves by DMA without a bounce through driver staging buffers
@@ -324,11 +322,11 @@ static pm_ctx* create_ctx(const pm_graph_desc* g, const char* pattern_dir, int d
 static void destroy_ctx(pm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_off, c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_labels, c->d_hubs,
+  void* ptrs[] = {c->d_offp, c->d_offr, c->d_colp, c->d_perm, c->d_pos, c->d_labs, c->d_hubs,
                   c->d_ktab, c->d_ttab, c->d_hseg, c->d_hscr, c->d_tpub[0], c->d_tpub[1], c->d_tst, c->d_mcol,
                   c->d_mlen, c->d_malive, c->d_slist, c->d_slist2, c->d_nS2, c->d_ccnt, c->d_cbase, c->d_ctmp, c->d_smask[0], c->d_smask[1], c->d_kmask, c->d_sources, c->d_nS, c->d_flags, c->d_tsm,
                   c->d_counts, c->d_part, c->d_tmask, c->d_tbase, c->d_scan_tmp, c->arena.base, c->d_tn, c->d_pseen,
-                  c->d_offl != c->d_off ? c->d_offl : nullptr, c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
+                  c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit, c->d_push,
                   };
@@ -339,6 +337,7 @@ static void destroy_ctx(pm_ctx* c) {
   if (c->h_pin_lines) (void)hipHostFree(c->h_pin_lines);
   free_line_buffers(*c);
   for (auto e : c->events) (void)hipEventDestroy(e);
+  if (c->ev_handoff) (void)hipEventDestroy(c->ev_handoff);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -447,7 +446,15 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   if (init_step) queue_lcc_first_fills(c);
   flush_zero(c);
   PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
-  bool k_timed = false;
+  bool k_timed = false, handed_off = false;
+  // sharded: the state became the replica (the sharded part of the search ends here)
+  auto handoff = [&] {
+    if (!c.comm) return;
+    if (!c.ev_handoff) PM_HIP_CHECK(hipEventCreate(&c.ev_handoff));
+    PM_HIP_CHECK(hipEventRecord(c.ev_handoff, c.stream));
+    c.comm_wall_handoff = c.comm->wall;
+    handed_off = true;
+  };
   for (uint64_t ss = 0; ss < D; ++ss) {
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
@@ -464,7 +471,10 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       if (c.split_hubs) shard_hub_combine(c, slot);
       debug_point(c, "delegate combine");
       if (D >= 2) shard_codes_after_first(c);
-      else shard_replicate(c);
+      else {
+        shard_replicate(c);
+        handoff();
+      }
       debug_point(c, "code exchange / replica");
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
@@ -482,7 +492,10 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         debug_point(c, "list compaction");
       }
       // sharded: after the first later superstep the state of S goes to the replica
-      if (init_step && ss == 1) shard_replicate(c);
+      if (init_step && ss == 1) {
+        shard_replicate(c);
+        handoff();
+      }
       debug_point(c, "superstep end");
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
@@ -555,6 +568,12 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     float ms = 0.f;
     PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[D + 1], ev[D + 2]));
     c.lcc_first_ms = ms;
+  }
+  if (handed_off) {  // minus the collectives' host time, during which the stream idles (in-process shards wait
+                     // for each other there): the shard's own device work and launch gaps
+    float ms = 0.f;
+    PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], c.ev_handoff));
+    c.sharded_ms = static_cast<float>(std::max(0.0, ms - (c.comm_wall_handoff - c.comm_wall0) * 1e3));
   }
   c.probe("lcc parsed");
   if (asym)
@@ -706,6 +725,8 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   std::vector<std::vector<std::vector<std::string>>> subgraphs(P.lines.size(),
                                                                std::vector<std::vector<std::string>>(c.nranks));
   pm_run_stats s{};
+  const uint64_t comm_calls0 = c.comm ? c.comm->calls : 0, comm_bytes0 = c.comm ? c.comm->bytes : 0;
+  if (c.comm) c.comm_wall0 = c.comm->wall;
   c.device_seconds = 0.0;
   c.lines_seconds = 0.0;
   // pattern_time_start (beta.cpp:539): the reset above is only enqueued; the
@@ -810,6 +831,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
             for (;;) {
               bool overflow = false;
               const size_t n = run_lines_fused(c, pl, files, batch, overflow);
+              s.line_overflows += overflow ? 1 : 0;
               batch_pl0 = pl;
               const bool regrown = c.hash_regrown;
               c.hash_regrown = false;
@@ -837,6 +859,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
           ph_tp += since(t1);
         } else {
           // exact-count path (one launch + sync per position)
+          ++s.exact_lines;
           if (pl >= 4) {  // beta.cpp:762-767
             // the kept walks become subgraph lines chunk by chunk (the chunked enumeration bounds the device
             // memory, the lines are all the host keeps)
@@ -914,6 +937,20 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   s.lcc_first_bytes = c.lcc_first_bytes;
   s.final_vertices = last_v;
   s.final_edges = last_e;
+  s.shard_entries = c.nnz;
+  s.shard_rows = c.held_rows;
+  s.shard_hub_entries = c.held_hub_entries;
+  for (uint64_t j = c.shard; c.split_hubs && j < c.hubs_host.size(); j += c.nshards) ++s.shard_hubs_controlled;
+  s.shard_ss0_entries = first_scanned;
+  s.shard_ss0_survivors = first_surv;
+  s.shard_sharded_ms = c.comm ? c.sharded_ms : 0.0;
+  if (c.comm) {
+    s.comm_calls = c.comm->calls - comm_calls0;
+    s.comm_bytes = c.comm->bytes - comm_bytes0;
+    s.comm_seconds = c.comm->wall - c.comm_wall0;
+  }
+  s.replica_rows = c.replica_rows;
+  s.replica_entries = c.replica_entries;
   if (files) {
     // result dump (beta.cpp:1370-1425) -- after pattern_time_end, as in the reference
     std::vector<uint16_t> tpub;
@@ -1006,7 +1043,6 @@ int pm_vertex_data_set(pm_ctx* ctx, const uint64_t* labels) {
   PM_API_BODY(ctx, {
     if (!labels) throw std::runtime_error("null labels");
     ctx->labels_host.assign(labels, labels + ctx->n);
-    PM_HIP_CHECK(hipMemcpy(ctx->d_labels, labels, ctx->n * sizeof(uint64_t), hipMemcpyHostToDevice));
     pm::relayout(*ctx);
   });
 }
@@ -1015,11 +1051,19 @@ int pm_vertex_data_files(pm_ctx* ctx, const char* prefix) {
   PM_API_BODY(ctx, {
     if (!prefix) throw std::runtime_error("null label prefix");
     const std::vector<std::string> files = pm::vertex_label_files(prefix);
-    pm::labels_from_files_device(files, ctx->n, ctx->d_labels, ctx->stream);
-    ctx->labels_host.resize(ctx->n);
-    PM_HIP_CHECK(hipMemcpyAsync(ctx->labels_host.data(), ctx->d_labels, ctx->n * sizeof(uint64_t),
-                                hipMemcpyDeviceToHost, ctx->stream));
-    PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    uint64_t* d_labels = nullptr;  // (parsed on the device, kept on the host: the layout's input)
+    PM_HIP_CHECK(hipMalloc(&d_labels, std::max<uint64_t>(ctx->n, 1) * sizeof(uint64_t)));
+    try {
+      pm::labels_from_files_device(files, ctx->n, d_labels, ctx->stream);
+      ctx->labels_host.resize(ctx->n);
+      PM_HIP_CHECK(hipMemcpyAsync(ctx->labels_host.data(), d_labels, ctx->n * sizeof(uint64_t),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+      PM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+      (void)hipFree(d_labels);
+      throw;
+    }
+    (void)hipFree(d_labels);
     pm::relayout(*ctx);
   });
 }
@@ -1162,6 +1206,32 @@ pm_ctx* pm_create_shard(const pm_shard_desc* d, const char* pattern_dir, int dev
   }
 }
 
+pm_ctx* pm_create_shard_host_comm(const pm_shard_desc* d, const char* pattern_dir, int device,
+                                  const pm_host_comm* comm) {
+  try {
+    if (!d || !comm) throw std::runtime_error("pm_create_shard_host_comm: null argument");
+    if (comm->nshards != d->nshards || comm->shard != d->shard)
+      throw std::runtime_error("pm_create_shard_host_comm: communicator and shard disagree on nshards / shard");
+    PM_HIP_CHECK(hipSetDevice(device));
+    pm::CtxInput in;
+    in.n = d->n;
+    in.off = d->off;
+    in.col = d->col;
+    in.gdeg = d->degree;
+    if (!in.gdeg) throw std::runtime_error("pm_create_shard_host_comm: null degree array");
+    in.symmetric = d->symmetric != 0;
+    in.nranks = d->nranks;
+    in.hub_threshold = d->hub_threshold;
+    in.nshards = d->nshards;
+    in.shard = d->shard;
+    in.comm = pm::make_host_comm(*comm);
+    return pm::create_ctx(in, pattern_dir, device);
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return nullptr;
+  }
+}
+
 // Every failed shard's message (a device fault is seen by whichever shard calls the runtime next; the shard
 // whose work faulted names it in its own message).
 static void throw_shard_errors(const std::vector<std::string>& errs) {
@@ -1242,7 +1312,6 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
         ctx = pm::create_ctx(in, pattern_dir, device);
         if (labels) {
           ctx->labels_host.assign(labels, labels + n);
-          PM_HIP_CHECK(hipMemcpy(ctx->d_labels, labels, n * sizeof(uint64_t), hipMemcpyHostToDevice));
           pm::relayout(*ctx);
         }
         pm::run_beta(*ctx, dir, max_iterations, &st[q]);
@@ -1369,11 +1438,12 @@ pm_ctx* pm_create_rmat(uint64_t scale, uint64_t p_gen, const char* pattern_dir, 
     in.off = off.data();
     in.col = g.d_col;
     in.col_on_device = true;
+    in.col_release = true;  // the context frees the generated adjacency once it holds its copy
+    g.d_col = nullptr;
     in.symmetric = true;
     in.nranks = nranks;
     in.hub_threshold = hub_threshold;
     pm_ctx* c = pm::create_ctx(in, pattern_dir, device);
-    (void)hipFree(g.d_col);
     (void)hipStreamDestroy(s);
     return c;
   } catch (const std::exception& e) {
@@ -1479,6 +1549,8 @@ static pm_ctx* create_rmat_shard_ctx(uint64_t scale, uint64_t p_gen, const char*
     in.off = off.data();
     in.col = g.d_col;
     in.col_on_device = true;
+    in.col_release = true;  // freed by the context once copied (in-process shards: before the next shard builds)
+    g.d_col = nullptr;
     in.gdeg = gdeg.data();
     in.symmetric = true;
     in.nranks = nranks;
@@ -1488,7 +1560,6 @@ static pm_ctx* create_rmat_shard_ctx(uint64_t scale, uint64_t p_gen, const char*
     in.comm = owned.release();
     in.inprocess_shards = inprocess;
     pm_ctx* c = create_ctx(in, pattern_dir, device);
-    (void)hipFree(g.d_col);
     (void)hipStreamDestroy(s);
     return c;
   } catch (...) {
@@ -1516,9 +1587,9 @@ pm_ctx* pm_create_rmat_shard(uint64_t scale, uint64_t p_gen, const char* pattern
   }
 }
 
-int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
-                             uint32_t nranks, uint64_t hub_threshold, const char* result_dir, uint64_t max_iterations,
-                             pm_run_stats* out) {
+int pm_run_rmat_local_shards2(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
+                              uint32_t nranks, uint64_t hub_threshold, const uint64_t* labels, const char* result_dir,
+                              uint64_t max_iterations, uint32_t repeats, pm_run_stats* per_shard) {
   try {
     if (nshards == 0 || nshards > 64) throw std::runtime_error("pm_run_rmat_local_shards: 1..64 shards");
     pm::ThreadGroup grp(static_cast<int>(nshards));
@@ -1532,7 +1603,12 @@ int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern
         PM_HIP_CHECK(hipSetDevice(device));
         ctx = pm::create_rmat_shard_ctx(scale, p_gen, pattern_dir, device, nranks, hub_threshold, nshards, q,
                                         pm::make_thread_comm(&grp, static_cast<int>(q)), nshards, nullptr);
-        pm::run_beta(*ctx, dir, max_iterations, &st[q]);
+        if (labels) {
+          ctx->labels_host.assign(labels, labels + ctx->n);
+          pm::relayout(*ctx);
+        }
+        for (uint32_t r = 0; r < std::max<uint32_t>(repeats, 1); ++r)
+          pm::run_beta(*ctx, r == 0 ? dir : std::string(), max_iterations, &st[q]);
       } catch (const std::exception& e) {
         errs[q] = e.what();
         grp.abort();
@@ -1543,12 +1619,26 @@ int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern
     for (uint32_t q = 0; q < nshards; ++q) pool.emplace_back(work, q);
     for (auto& t : pool) t.join();
     throw_shard_errors(errs);
-    if (out) *out = st[0];
+    if (per_shard) std::copy(st.begin(), st.end(), per_shard);
     return 0;
   } catch (const std::exception& e) {
     pm::g_last_error = e.what();
     return -1;
   }
+}
+
+int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
+                             uint32_t nranks, uint64_t hub_threshold, const char* result_dir, uint64_t max_iterations,
+                             pm_run_stats* out) {
+  if (nshards == 0 || nshards > 64) {
+    pm::g_last_error = "pm_run_rmat_local_shards: 1..64 shards";
+    return -1;
+  }
+  std::vector<pm_run_stats> st(nshards);
+  const int rc = pm_run_rmat_local_shards2(scale, p_gen, pattern_dir, device, nshards, nranks, hub_threshold, nullptr,
+                                           result_dir, max_iterations, 1, st.data());
+  if (rc == 0 && out) *out = st[0];
+  return rc;
 }
 
 static std::vector<std::string> file_list(const char* const* files, uint32_t nfiles) {

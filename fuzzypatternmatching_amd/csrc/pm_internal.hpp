@@ -65,6 +65,19 @@ struct LineArgs {
 // one process on one device, parity tests) implement it (pm_shard.hip).
 struct Comm {
   virtual ~Comm() {}
+  // collectives issued and bytes this shard contributed (send side), for the per-shard statistics
+  uint64_t calls = 0, bytes = 0;
+  double wall = 0.0;  // host seconds spent inside the collectives (the stream idles meanwhile)
+  void count(uint64_t b) {
+    ++calls;
+    bytes += b;
+  }
+  struct Timer {  // adds the scope's host time to wall
+    explicit Timer(Comm* c) : c_(c), t0_(std::chrono::steady_clock::now()) {}
+    ~Timer() { c_->wall += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count(); }
+    Comm* c_;
+    std::chrono::steady_clock::time_point t0_;
+  };
   // recv receives nshards consecutive `bytes` blocks, block g = shard g's send
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   virtual void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) = 0;
@@ -256,23 +269,28 @@ struct Ctx {
   // vertex positions ordered by (label, degree, id); every device array below
   // is indexed by position and the adjacency holds neighbour positions (each
   // row keeps the id order of the input, so duplicates stay adjacent).
-  uint64_t* d_off = nullptr;      // id-major offsets of the whole graph (degrees: labels, layout), V+1
-  uint64_t* d_offl = nullptr;     // id-major offsets of this shard's rows (== d_off unsharded), V+1
+  // Degrees by vertex id live on the host; the layout uploads what it needs to scratch (the device keeps no
+  // id-major array but pos: 8 B per vertex less than resident offsets, per context -- in-process shards of
+  // one S=28 search on one device need the room).
   std::vector<uint32_t> deg_host; // global (out-)degree by vertex id: labels, hubs, ss0 senders' entries
   std::vector<uint32_t> rdeg_host;// directed graphs: in-degree (length of the row superstep 0 scans)
+  std::vector<uint32_t> ldeg_host;// sharded: length of this shard's row of each id (owned rows, delegate shares)
   uint32_t row_degree(uint64_t v) const { return rdeg_host.empty() ? deg_host[v] : rdeg_host[v]; }
+  // the layout's sort key (row_degree: global degree, or in-degree of a directed graph) and the length of the
+  // row this context holds
+  const std::vector<uint32_t>& key_degrees() const { return rdeg_host.empty() ? deg_host : rdeg_host; }
+  const std::vector<uint32_t>& held_degrees() const { return ldeg_host.empty() ? key_degrees() : ldeg_host; }
   uint64_t nq = 0;                // padded slots (label independent)
   uint64_t* d_offp = nullptr;     // label-major padded row starts, V+1
   uint64_t* d_offr = nullptr;     // label-major unpadded offsets (degree sums), V+1
   uint32_t* d_colp = nullptr;     // padded adjacency (neighbour positions, kNone pad), nq
   uint32_t* d_perm = nullptr;     // position -> vertex id
   uint32_t* d_pos = nullptr;      // vertex id -> position
-  uint64_t* d_labs = nullptr;     // labels in position order
+  uint64_t* d_labs = nullptr;     // labels in position order (kept only when a line has selected vertices)
   std::vector<uint32_t> perm_host;
   LabelRuns lr{};
-  uint64_t* d_labels = nullptr;   // labels by vertex id
   uint64_t* d_hubs = nullptr;
-  std::vector<uint64_t> labels_host;  // for result files
+  std::vector<uint64_t> labels_host;  // labels by vertex id (layout input, result files)
 
   // superstep-0 tiling for the current labels and pattern
   std::vector<KRange> ktab;
@@ -297,6 +315,12 @@ struct Ctx {
   // (shard_replicate): the rest of the search -- later supersteps, NLC lines,
   // later LCC calls -- runs on the replica exactly as on one GPU.
   uint32_t nshards = 1, shard = 0;
+  uint64_t held_rows = 0;         // nonempty rows this context holds (a shard: owned rows + delegate shares)
+  uint64_t held_hub_entries = 0;  // entries of the delegate shares it holds
+  hipEvent_t ev_handoff = nullptr;  // sharded: recorded when the state became the replica (sharded_ms)
+  float sharded_ms = 0.f;         // device time of the last search's sharded part (search start -> replica)
+  double comm_wall0 = 0.0, comm_wall_handoff = 0.0;  // Comm::wall at the search start / at the hand-off
+  uint64_t replica_rows = 0, replica_entries = 0;
   Comm* comm = nullptr;
   Comm* comm_owned = nullptr;     // deleted with the context
   uint64_t mcap = 0;              // capacity (entries) of d_colp and d_mcol (nq; + kTileEntries tail padding)
@@ -440,6 +464,8 @@ struct Ctx {
   unsigned long long* d_hval = nullptr;
   uint64_t hcap = 0;
   bool hash_regrown = false;
+  uint64_t hash_slots = 0;        // PM_HASH_SLOTS (diagnostics): size of the context's first table (0: from |S|)
+  int64_t nogrow_shard = -1;      // PM_DEBUG_NOGROW_SHARD (diagnostics): that shard reports no room to grow it
   bool no_row_compaction = false;
   uint32_t lcc_calls = 0;  // stamp of the LCC calls (the compaction's long-row word)
   bool push_long = true;   // some row of S may be longer than a push-form piece (unknown: true)  // PM_ROW_COMPACTION=0 (diagnostics): rows keep their dead entries  // the last fused launch overflowed the table and grew it (rerun the line fused)
@@ -489,11 +515,11 @@ inline uint32_t* m_col(const Ctx& c) { return c.replicated ? c.d_rmcol : c.d_mco
 inline uint64_t m_cap(const Ctx& c) { return c.replicated ? c.rmcap : c.mcap; }
 
 // Kernel launchers (pm_kernels.hip).
-void launch_degree_labels(Ctx& c);
 // Label-major layout: sorts the vertices by (label, degree, id) and writes the
-// renumbered adjacency into dst (E entries).  src_col holds neighbour ids at
-// src_start[id] (the id-major input), or, when relabelling, is the current
-// d_colp (neighbour positions, translated in place first).
+// renumbered adjacency into dst (E entries).  src_col holds the id-major input
+// (each held row at the prefix sum of held_degrees()), or, when relabelling, is
+// the current d_colp (neighbour positions, translated in place first).  Its
+// scratch (~64 B per vertex) is allocated for the call and freed after it.
 void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst);
 void build_tiling(Ctx& c);
 // Counter slots: W = slot_words(c) u64 = [vertices per rank | edges per rank |
@@ -587,6 +613,10 @@ void shard_hub_combine(Ctx& c, uint64_t* d_slot);
 void shard_codes_after_first(Ctx& c);  // after superstep 0: every shard's survivors' T_pub codes
 void shard_replicate(Ctx& c);          // the state of S of every shard -> the replica (collective)
 std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  // host vector, sum
+// The minimum of v over the shards (v itself without a communicator): capacities that steer the replicated
+// part of a sharded search (arena, line hash table) must be the same on every shard, or an overflow -- and the
+// collectives of the path it takes -- could happen on some shards only.
+uint64_t shard_agree_min(Ctx& c, uint64_t v);
 // S rows of the current state (slist entries with T_pub != 0) packed on the device: per row
 // {position, T_pub | T_state << 16, |M|, first entry} (4 u32) and its alive M entries; counts[0..1] =
 // rows, entries (device).  rec / ent hold nS_host rows / the caller's entry bound.

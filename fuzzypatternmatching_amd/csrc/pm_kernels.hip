@@ -38,27 +38,18 @@ namespace pm {
 
 
 // ---------------------------------------------------------------------------
-// K0: labels.
-// vertex_data_db_degree.hpp:109  label = ceil(log2(degree + 1)) == bit_width(degree)
-__global__ void k_degree_labels(const uint64_t* __restrict__ off, uint64_t n, uint64_t* __restrict__ labels) {
-  for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < n; v += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t d = off[v + 1] - off[v];
-    labels[v] = d ? static_cast<uint64_t>(64 - __clzll(static_cast<long long>(d))) : 0;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Label-major padded layout (built when the labels change, outside any search).
 //
 // Vertices are stably sorted by (label, degree); rows of degree <= kHeavyDeg
 // get padded_degree() slots (kNone fill), so every (label, degree class) run
 // is a dense rows x G array whose slot addresses follow from the tile index
 // alone: superstep 0 needs no row-offset loads, one round trip per tile.
-__global__ void k_layout_keys(const uint64_t* __restrict__ off, uint64_t n, uint32_t* __restrict__ dkey,
+// (Degree labels, vertex_data_db_degree.hpp:109 label = bit_width(degree), are
+// computed on the host: the device holds no id-major degree array.)
+__global__ void k_layout_keys(const uint32_t* __restrict__ deg, uint64_t n, uint32_t* __restrict__ dkey,
                               uint32_t* __restrict__ ids) {
   for (uint64_t v = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; v < n; v += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t d = off[v + 1] - off[v];
-    dkey[v] = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
+    dkey[v] = deg[v];
     ids[v] = static_cast<uint32_t>(v);
   }
 }
@@ -70,11 +61,11 @@ __global__ void k_gather_labels(const uint64_t* __restrict__ labels, const uint3
 }
 
 // Degrees in position order: padded (pad) and real (real).
-__global__ void k_perm_degrees(const uint64_t* __restrict__ off, const uint32_t* __restrict__ perm, uint64_t n,
+__global__ void k_perm_degrees(const uint32_t* __restrict__ deg, const uint32_t* __restrict__ perm, uint64_t n,
                                uint64_t* __restrict__ pad, uint64_t* __restrict__ real) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = perm[i];
-    const uint64_t d = off[u + 1] - off[u];
+    const uint64_t d = deg[u];
     pad[i] = padded_degree(d);
     real[i] = d;
   }
@@ -104,7 +95,7 @@ __global__ void k_to_ids(uint32_t* __restrict__ col, uint64_t nq, const uint32_t
 // the padding kNone.
 __global__ __launch_bounds__(kBlock) void k_copy_rows(const uint32_t* __restrict__ src,
                                                       const uint64_t* __restrict__ src_start,
-                                                      const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ deg,
                                                       const uint64_t* __restrict__ offp,
                                                       const uint32_t* __restrict__ perm,
                                                       const uint32_t* __restrict__ pos, uint64_t n,
@@ -114,9 +105,9 @@ __global__ __launch_bounds__(kBlock) void k_copy_rows(const uint32_t* __restrict
   for (uint64_t i = blockIdx.x * uint64_t(kWpb) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave); i < n; i += nw) {
     const uint64_t d0 = offp[i], slots = offp[i + 1] - d0;
     const uint32_t u = perm[i];
-    const uint64_t deg = off[u + 1] - off[u];
+    const uint64_t du = deg[u];
     const uint64_t s0 = src_start[u];
-    for (uint64_t j = lane; j < slots; j += kWave) dst[d0 + j] = j < deg ? pos[src[s0 + j]] : kNone;
+    for (uint64_t j = lane; j < slots; j += kWave) dst[d0 + j] = j < du ? pos[src[s0 + j]] : kNone;
   }
 }
 
@@ -1646,12 +1637,6 @@ static OwnerArgs owner_args(const Ctx& c) {
   return oa;
 }
 
-void launch_degree_labels(Ctx& c) {
-  hipLaunchKernelGGL(k_degree_labels, dim3(grid_for(c.n, kBlock, 8192)), dim3(kBlock), 0, c.stream, c.d_off, c.n,
-                     c.d_labels);
-  PM_HIP_CHECK(hipGetLastError());
-}
-
 uint32_t slot_words(const Ctx& c) { return 2 * (c.nranks <= 1 ? 1 : c.nranks) + 4; }
 
 static Partials partials(Ctx& c, uint64_t* d_slot) {
@@ -1666,8 +1651,8 @@ static void reduce_into(Ctx&, unsigned, uint64_t*) {}
 // (nshards > 1): by (label, degree class, owner, degree, id) -- two more
 // passes (owner, class) between them -- so every (label, class) run of the
 // tiling splits into one contiguous sub-run per shard while the label runs
-// stay whole.  Keys use the global degrees (d_off); slots and copied rows the
-// shard's own rows (d_offl: other shards' rows are empty here).
+// stay whole.  Keys use the global degrees (key_degrees); slots and copied rows
+// the shard's own rows (held_degrees: other shards' rows are empty here).
 __global__ void k_owner_keys(const uint32_t* __restrict__ ids, uint64_t n, uint32_t nshards,
                              uint32_t* __restrict__ key) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
@@ -1684,11 +1669,11 @@ __host__ __device__ inline uint32_t degree_class(uint64_t d) {
 
 // hub_thr (sharded searches with delegates): a delegate's share is a heavy row on every shard
 // whatever its length there, so every delegate sorts into the heavy class
-__global__ void k_class_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ ids, uint64_t n,
+__global__ void k_class_keys(const uint32_t* __restrict__ deg, const uint32_t* __restrict__ ids, uint64_t n,
                              uint64_t hub_thr, uint32_t* __restrict__ key) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t u = ids[i];
-    const uint64_t d = off[u + 1] - off[u];
+    const uint64_t d = deg[u];
     key[i] = d >= hub_thr ? kHeavyKind + 1 : degree_class(d);
   }
 }
@@ -1704,32 +1689,72 @@ __global__ void k_patch_moff(const HubInfo* __restrict__ info, uint32_t nh, uint
     if (info[j].moff != ~0ull) moff[info[j].pos] = info[j].moff;
 }
 
+// Scratch of one call: device allocations freed with the object.
+namespace {
+struct Scratch {
+  std::vector<void*> ps;
+  ~Scratch() {
+    for (void* p : ps) (void)hipFree(p);
+  }
+  template <typename T>
+  T* get(uint64_t n) {
+    void* p = nullptr;
+    PM_HIP_CHECK(hipMalloc(&p, std::max<uint64_t>(n, 1) * sizeof(T)));
+    ps.push_back(p);
+    return static_cast<T*>(p);
+  }
+};
+}  // namespace
+
 void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst) {
   const uint64_t n = c.n;
-  c.arena.reset();
   if (n) {
+    Scratch sc;
     const unsigned g = grid_for(n, kBlock, 8192);
-    auto* src_start = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
+    // the layout's inputs by vertex id, from the host: sort-key degrees, held-row lengths, labels
+    const std::vector<uint32_t>& kd = c.key_degrees();
+    const std::vector<uint32_t>& hd = c.held_degrees();
+    auto* kdeg = sc.get<uint32_t>(n);
+    PM_HIP_CHECK(hipMemcpyAsync(kdeg, kd.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+    uint32_t* hdeg = kdeg;
+    if (&hd != &kd) {
+      hdeg = sc.get<uint32_t>(n);
+      PM_HIP_CHECK(hipMemcpyAsync(hdeg, hd.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, c.stream));
+    }
+    auto* labels = sc.get<uint64_t>(n);
+    PM_HIP_CHECK(hipMemcpyAsync(labels, c.labels_host.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+    auto* src_start = sc.get<uint64_t>(n);
+    rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> hw(hdeg, Widen());
     if (src_is_layout) {
       hipLaunchKernelGGL(k_row_starts_by_id, dim3(g), dim3(kBlock), 0, c.stream, c.d_offp, c.d_perm, n, src_start);
       hipLaunchKernelGGL(k_to_ids, dim3(grid_for(c.nq, kBlock, 65535)), dim3(kBlock), 0, c.stream, src_col, c.nq,
                          c.d_perm);
-    } else {
-      PM_HIP_CHECK(hipMemcpyAsync(src_start, c.d_offl, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, c.stream));
     }
-    auto* dkey = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
-    auto* dkey2 = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
-    auto* ids = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
-    auto* ids2 = static_cast<uint32_t*>(c.arena.get(n * sizeof(uint32_t)));
-    auto* lkey = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
-    hipLaunchKernelGGL(k_layout_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, n, dkey, ids);
-    size_t tmp = 0, tmp2 = 0;
+    auto* dkey = sc.get<uint32_t>(n);
+    auto* dkey2 = sc.get<uint32_t>(n);
+    auto* ids = sc.get<uint32_t>(n);
+    auto* ids2 = sc.get<uint32_t>(n);
+    auto* lkey = sc.get<uint64_t>(n);
+    // labels in position order: kept for selected-vertices lines only (their destination filter)
+    if (c.any_sv && !c.d_labs) PM_HIP_CHECK(hipMalloc(&c.d_labs, n * sizeof(uint64_t)));
+    uint64_t* labs = c.any_sv ? c.d_labs : sc.get<uint64_t>(n);
+    hipLaunchKernelGGL(k_layout_keys, dim3(g), dim3(kBlock), 0, c.stream, kdeg, n, dkey, ids);
+    size_t tmp = 0, tmp2 = 0, tmp3 = 0, tmp4 = 0;
     PM_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 32,
                                                     c.stream));
-    PM_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp2, lkey, c.d_labs, ids2, c.d_perm, size_t(n),
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, tmp2, lkey, labs, ids2, c.d_perm, size_t(n),
                                                     0, 64, c.stream));
-    tmp = std::max(tmp, tmp2);
-    void* d_tmp = c.arena.get(tmp);
+    PM_HIP_CHECK(rocprim::inclusive_scan(nullptr, tmp3, lkey, c.d_offp + 1, size_t(n), rocprim::plus<uint64_t>(),
+                                         c.stream));
+    PM_HIP_CHECK(rocprim::exclusive_scan(nullptr, tmp4, hw, src_start, uint64_t(0), size_t(n),
+                                         rocprim::plus<uint64_t>(), c.stream));
+    tmp = std::max(std::max(tmp, tmp2), std::max(tmp3, tmp4));
+    void* d_tmp = sc.get<char>(tmp);
+    if (!src_is_layout) {  // the id-major input: held rows one after the other
+      size_t t4 = tmp;
+      PM_HIP_CHECK(rocprim::exclusive_scan(d_tmp, t4, hw, src_start, uint64_t(0), size_t(n),
+                                           rocprim::plus<uint64_t>(), c.stream));
+    }
     PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 32,
                                                     c.stream));
     if (c.nshards > 1) {
@@ -1738,37 +1763,37 @@ void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t*
       hipLaunchKernelGGL(k_owner_keys, dim3(g), dim3(kBlock), 0, c.stream, ids2, n, c.nshards, dkey);
       PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids2, ids, size_t(n), 0,
                                                       obits, c.stream));
-      hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, c.d_off, ids, n,
+      hipLaunchKernelGGL(k_class_keys, dim3(g), dim3(kBlock), 0, c.stream, kdeg, ids, n,
                          c.split_hubs ? c.hub_threshold : ~0ull, dkey);
       PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, dkey, dkey2, ids, ids2, size_t(n), 0, 6,
                                                       c.stream));
     }
-    hipLaunchKernelGGL(k_gather_labels, dim3(g), dim3(kBlock), 0, c.stream, c.d_labels, ids2, n, lkey);
-    PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, lkey, c.d_labs, ids2, c.d_perm, size_t(n), 0,
+    hipLaunchKernelGGL(k_gather_labels, dim3(g), dim3(kBlock), 0, c.stream, labels, ids2, n, lkey);
+    PM_HIP_CHECK(rocprim::radix_sort_pairs(d_tmp, tmp, lkey, labs, ids2, c.d_perm, size_t(n), 0,
                                                     64, c.stream));
     hipLaunchKernelGGL(k_inverse_perm, dim3(g), dim3(kBlock), 0, c.stream, c.d_perm, n, c.d_pos);
     // label-major offsets of this shard's rows: padded (slots) and real (degree sums)
     auto* pdeg = lkey;  // reuse
-    auto* rdeg = static_cast<uint64_t*>(c.arena.get(n * sizeof(uint64_t)));
-    hipLaunchKernelGGL(k_perm_degrees, dim3(g), dim3(kBlock), 0, c.stream, c.d_offl, c.d_perm, n, pdeg, rdeg);
-    size_t tmp3 = 0;
-    PM_HIP_CHECK(rocprim::inclusive_scan(nullptr, tmp3, pdeg, c.d_offp + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
-    void* d_tmp3 = c.arena.get(tmp3);
-    PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp3, tmp3, pdeg, c.d_offp + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
-    PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp3, tmp3, rdeg, c.d_offr + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
+    auto* rdeg = sc.get<uint64_t>(n);
+    hipLaunchKernelGGL(k_perm_degrees, dim3(g), dim3(kBlock), 0, c.stream, hdeg, c.d_perm, n, pdeg, rdeg);
+    size_t t3 = tmp;
+    PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp, t3, pdeg, c.d_offp + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
+    t3 = tmp;
+    PM_HIP_CHECK(rocprim::inclusive_scan(d_tmp, t3, rdeg, c.d_offr + 1, size_t(n), rocprim::plus<uint64_t>(), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_offr, 0, sizeof(uint64_t), c.stream));
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(n, kWpb, 65535)), dim3(kBlock), 0, c.stream, src_col, src_start,
-                       c.d_offl, c.d_offp, c.d_perm, c.d_pos, n, dst);
+                       hdeg, c.d_offp, c.d_perm, c.d_pos, n, dst);
     PM_HIP_CHECK(hipGetLastError());
+    c.perm_host.resize(n);
+    PM_HIP_CHECK(hipMemcpyAsync(c.perm_host.data(), c.d_perm, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));  // (the scratch is freed on return)
   } else {
     PM_HIP_CHECK(hipMemsetAsync(c.d_offp, 0, sizeof(uint64_t), c.stream));
     PM_HIP_CHECK(hipMemsetAsync(c.d_offr, 0, sizeof(uint64_t), c.stream));
+    c.perm_host.clear();
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
   }
-  c.perm_host.resize(n);
-  if (n) PM_HIP_CHECK(hipMemcpyAsync(c.perm_host.data(), c.d_perm, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  c.arena.reset();
 }
 
 // Superstep-0 tiling for the current layout and pattern (host-side table).
@@ -2234,8 +2259,10 @@ __global__ void k_slist_heavy(const uint4* __restrict__ hrec, uint32_t nheavy, c
 // Records in place (one context): the slice holding the first record of each 64-record chunk of the slices'
 // concatenation, rofs[W] = the number of light records, and the list count (the heavy survivors are appended
 // after them by k_slist_heavy).
-__global__ void k_chunk_slices(const uint64_t* __restrict__ rofs_in, const uint32_t* __restrict__ rcnt,
-                               const uint64_t* __restrict__ rbase, uint32_t W, uint64_t* __restrict__ rofs,
+// (rofs_in and rofs are the same array -- thread 0 writes rofs[W], which no thread reads -- so neither is
+// declared __restrict__)
+__global__ void k_chunk_slices(const uint64_t* rofs_in, const uint32_t* __restrict__ rcnt,
+                               const uint64_t* __restrict__ rbase, uint32_t W, uint64_t* rofs,
                                uint4* __restrict__ cdesc, uint32_t* __restrict__ nS) {
   const uint64_t total = rofs_in[W - 1] + rcnt[W - 1];
   const uint64_t nch = (total + kWave - 1) / kWave;
@@ -2365,6 +2392,9 @@ void launch_lcc_push(Ctx& c, uint64_t* d_slot) {
   // no row of S longer than a piece (the last row compaction says so, c.push_long): no piece lists
   const bool pieces = c.push_long;
   if (pieces) PM_HIP_CHECK(hipMemsetAsync(c.d_push, 0, 2 * sizeof(unsigned long long), c.stream));
+  // without the piece launches a long row must be walked by its own wave: no capacity, so push_pieces always
+  // reports the list full (should the no-long-row stamp ever be wrong, the row is still sent and verified)
+  if (!pieces) a.piece_cap = av.piece_cap = 0;
   const unsigned grid = grid_for((uint64_t(c.nS_host) + kWave - 1) / kWave, kWpb, 16384);
   auto* trav = reinterpret_cast<unsigned long long*>(d_slot + 2 * P);
   const OwnerArgs oa = owner_args(c);
@@ -2940,32 +2970,39 @@ __global__ void k_tp_terminal_sv(const uint32_t* __restrict__ tu, const uint32_t
   }
 }
 
+// Position-1 walks of the sources; only each source's walks [clo, chi) are written (a source with more walks
+// than a chunk holds is enumerated in windows of its walks).
 __global__ void k_tds_init(const uint32_t* __restrict__ sources, uint64_t nsrc, const uint64_t* __restrict__ obase,
                            uint64_t obase0, const uint64_t* __restrict__ offp, const uint32_t* __restrict__ mcol,
                            const uint32_t* __restrict__ mlen, int stride,
-                           uint32_t* __restrict__ walks) {
+                           uint32_t* __restrict__ walks, uint64_t clo, uint64_t chi) {
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nsrc; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t s = sources[i];
-    uint64_t o = obase[i] - obase0;
+    uint64_t o = obase[i] - obase0, j = 0;
     const uint64_t b = offp[s], L = mlen[s];
     for (uint64_t e = b; e < b + L; ++e) {
       if (!(mcol[e] & kAlive)) continue;
-      walks[o * stride + 0] = s;
-      walks[o * stride + 1] = mcol[e] & kPosMask;
-      ++o;
+      if (j >= clo && j < chi) {
+        walks[o * stride + 0] = s;
+        walks[o * stride + 1] = mcol[e] & kPosMask;
+        ++o;
+      }
+      ++j;
     }
   }
 }
 
 // Non-terminal position k: receiver checks, then sender-side filter per
-// neighbour.  pass 0 counts, pass 1 writes.
+// neighbour.  pass 0 counts, pass 1 writes each walk's children [clo, chi)
+// (a walk with more children than a chunk holds is expanded in windows).
 template <int PASS>
 __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int k, int stride, LineArgs la,
                              const uint16_t* __restrict__ tpub, const uint64_t* __restrict__ offp,
                              const uint32_t* __restrict__ mcol,
                              const uint32_t* __restrict__ mlen, const uint32_t* __restrict__ malive,
                              uint32_t* __restrict__ cnt, const uint64_t* __restrict__ obase, uint64_t obase0,
-                             uint32_t* __restrict__ wout, unsigned long long* __restrict__ trav) {
+                             uint32_t* __restrict__ wout, unsigned long long* __restrict__ trav, uint64_t clo = 0,
+                             uint64_t chi = ~0ull) {
   uint64_t t = 0;
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < nw; i += uint64_t(gridDim.x) * blockDim.x) {
     const uint32_t* w = win + i * stride;
@@ -2988,7 +3025,7 @@ __global__ void k_tds_expand(const uint32_t* __restrict__ win, uint64_t nw, int 
         } else {
           if (!enum_ok(w, k + 1, nb, la)) continue;
         }
-        if (PASS) {
+        if (PASS && c >= clo && c < chi) {
           uint32_t* d = wout + o * stride;
           for (int p = 0; p <= k; ++p) d[p] = w[p];
           d[k + 1] = nb;
@@ -3298,7 +3335,9 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
 // expanded.  Device memory is then bounded by (C + 1) levels of at most cap walks, whatever the total
 // frontier; a level's pass-0 count (and its traversed-edge counter) still covers the level's whole walk set,
 // and the kept walks come out in the order of the unbatched enumeration (lexicographic by the children's
-// indices), for every cap.  PM_TDS_CAP=<walks> forces a small cap (tests).
+// indices), for every cap.  A single walk (or source) with more than cap children is expanded in windows of
+// cap of its children, so the bound holds for hubs at any position too.  PM_TDS_CAP=<walks> forces a small cap
+// (tests).
 namespace {
 struct TdsRun {
   Ctx& c;
@@ -3318,7 +3357,8 @@ struct TdsRun {
     auto* wc = arena_alloc<uint32_t>(c, nw);
     hipLaunchKernelGGL(k_tds_expand<0>, dim3(grid_for(nw, kBlock, 1024)), dim3(kBlock), 0, c.stream, walks, nw, k,
                        stride, la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_malive, wc,
-                       static_cast<const uint64_t*>(nullptr), uint64_t(0), static_cast<uint32_t*>(nullptr), d_trav);
+                       static_cast<const uint64_t*>(nullptr), uint64_t(0), static_cast<uint32_t*>(nullptr), d_trav,
+                       uint64_t(0), ~0ull);
     auto* wb = arena_alloc<uint64_t>(c, nw + 1);
     const uint64_t nnext = exclusive_scan_u32_to_u64(c, wc, wb, nw);
     res.tokens += nnext;
@@ -3337,15 +3377,17 @@ struct TdsRun {
           i1 = std::max(i1, i0 + 1);
           n = hb[i1] - b0;
         }
-        if (n) {
+        // (one walk with more than cap children, i1 == i0 + 1: its children in windows of cap, in order)
+        for (uint64_t c0 = 0; c0 < n; c0 += cap) {
+          const uint64_t nn = std::min(cap, n - c0);
           const size_t cm = c.arena.used;
-          auto* child = arena_alloc<uint32_t>(c, n * stride);
+          auto* child = arena_alloc<uint32_t>(c, nn * stride);
           hipLaunchKernelGGL(k_tds_expand<1>, dim3(grid_for(i1 - i0, kBlock, 1024)), dim3(kBlock), 0, c.stream,
                              walks + i0 * stride, i1 - i0, k, stride, la, tpub, m_off(c), m_col(c), c.d_mlen,
-                             c.d_malive, wc + i0, wb + i0, b0, child, d_trav);
+                             c.d_malive, wc + i0, wb + i0, b0, child, d_trav, c0, n > cap ? c0 + nn : ~0ull);
           PM_HIP_CHECK(hipGetLastError());
           ++chunks;
-          expand(k + 1, child, n);
+          expand(k + 1, child, nn);
           c.arena.used = cm;
         }
         i0 = i1;
@@ -3425,14 +3467,17 @@ TpResult run_tds_line(Ctx& c, const NlcLine& line, uint32_t& stride_out, const T
       i1 = std::max(i1, i0 + 1);
       n = hb[i1] - b0;
     }
-    if (n) {
+    // (one source with more than cap walks, i1 == i0 + 1: its walks in windows of cap, in order)
+    for (uint64_t c0 = 0; c0 < n; c0 += run.cap) {
+      const uint64_t nn = std::min(run.cap, n - c0);
       const size_t mark = c.arena.used;
-      auto* walks = arena_alloc<uint32_t>(c, n * stride);
+      auto* walks = arena_alloc<uint32_t>(c, nn * stride);
       hipLaunchKernelGGL(k_tds_init, dim3(grid_for(i1 - i0, kBlock, 4096)), dim3(kBlock), 0, c.stream,
-                         c.d_sources + i0, i1 - i0, obase + i0, b0, m_off(c), m_col(c), c.d_mlen, stride, walks);
+                         c.d_sources + i0, i1 - i0, obase + i0, b0, m_off(c), m_col(c), c.d_mlen, stride, walks, c0,
+                         n > run.cap ? c0 + nn : ~0ull);
       PM_HIP_CHECK(hipGetLastError());
       ++run.chunks;
-      run.expand(1, walks, n);
+      run.expand(1, walks, nn);
       c.arena.used = mark;
     }
     i0 = i1;

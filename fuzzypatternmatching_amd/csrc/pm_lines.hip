@@ -1119,7 +1119,7 @@ static T* dmalloc(uint64_t n) {
 }
 
 static void ensure_hash(Ctx& c, uint64_t want) {
-  uint64_t cap = 1ull << 16;
+  uint64_t cap = 1ull << 10;
   while (cap < want && cap < (1ull << 31)) cap <<= 1;
   if (c.hcap >= cap) return;
   if (c.d_hkey) (void)hipFree(c.d_hkey);
@@ -1136,6 +1136,9 @@ static void ensure_hash(Ctx& c, uint64_t want) {
 // After a path / cycle line overflowed the (source, vertex) table: partial inserts are not all recorded in the
 // frontier list, so the table is cleared; it grows 4x while the device has room (c.hash_regrown: the caller
 // reruns the line on the fused path), else the line goes to the exact per-position path.
+// Sharded replica: every shard overflows the same line (the table and the arena have one size on every shard and
+// the frontier count that overflows is order independent), so every shard is here; the room is agreed over the
+// shards, so that all of them rerun the line fused (a split line: its collectives) or all take the exact path.
 static void regrow_hash(Ctx& c) {
   PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
   PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
@@ -1143,7 +1146,10 @@ static void regrow_hash(Ctx& c) {
   constexpr uint64_t kSlotBytes = 2 * sizeof(unsigned long long) + sizeof(uint32_t) / 2;  // key, value, frontier
   size_t free_b = 0, total_b = 0;
   PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-  if (grow > (1ull << 31) || grow * kSlotBytes + (size_t(2) << 30) > free_b + c.hcap * kSlotBytes) return;
+  bool room = grow <= (1ull << 31) && grow * kSlotBytes + (size_t(2) << 30) <= free_b + c.hcap * kSlotBytes;
+  if (c.comm && c.nogrow_shard == static_cast<int64_t>(c.shard)) room = false;  // (PM_DEBUG_NOGROW_SHARD, tests)
+  room = shard_agree_min(c, room ? 1 : 0) != 0;
+  if (!room) return;
   ensure_hash(c, grow);
   c.hash_regrown = true;
 }
@@ -1215,7 +1221,9 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   }
   // the table is sized from the superstep-0 matching rows (upper bound of |S|); a replica by its rows, the same
   // on every shard
-  ensure_hash(c, std::max<uint64_t>(1ull << 20, 4 * (c.replicated ? uint64_t(c.nS_host) : c.ss0_rows)));
+  // (PM_HASH_SLOTS, diagnostics: the first table of the context has that many slots -- tests force overflows)
+  ensure_hash(c, c.hash_slots ? c.hash_slots
+                              : std::max<uint64_t>(1ull << 20, 4 * (c.replicated ? uint64_t(c.nS_host) : c.ss0_rows)));
   unsigned* d_done = c.d_gbar + kGbarWords;                                   // [0] lines done
   auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
   const size_t ctl_bytes = 64 * sizeof(unsigned) + nl * sizeof(LineStats);  // control words + stats of lines < nl

@@ -61,21 +61,31 @@ class RcclComm : public Comm {
   // ::test_rccl_shard_single_rank exercises the communicator); zero-sized calls
   // are skipped on the host.
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    Timer timer(this);
+    count(bytes);
     if (!bytes) return;
     PM_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    Timer timer(this);
+    Comm::count(count * 8);
     if (!count) return;
     PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm_, s));
   }
   void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    Timer timer(this);
+    Comm::count(count * 4);
     if (!count) return;
     PM_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, comm_, s));
   }
   // grouped point-to-point sends / receives over xGMI (one pair per peer)
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                  hipStream_t s) override {
+    Timer timer(this);
     uint64_t so = 0, ro = 0;
+    for (int g = 0; g < nranks_; ++g) so += sbytes[g];
+    count(so);
+    so = 0;
     PM_NCCL_CHECK(ncclGroupStart());
     for (int g = 0; g < nranks_; ++g) {
       if (sbytes[g]) PM_NCCL_CHECK(ncclSend(static_cast<const char*>(send) + so, sbytes[g], ncclUint8, g, comm_, s));
@@ -132,6 +142,99 @@ size_t rccl_unique_id(void* out, size_t len) {
 }
 
 // ---------------------------------------------------------------------------
+// Host-staged collectives of the caller (include/pm_abi.h pm_host_comm): the exchange the reference makes
+// over MPI (new_mailbox.hpp:358-405, impl/vertex_data.hpp:114-126), with the transport left to the host --
+// an MPI communicator, torch.distributed gloo (tests/test_gpu_multiprocess.py), any process group.  Every
+// call synchronises the stream, copies the device buffer to pinned host staging, calls the caller's
+// collective and copies the result back; the processes may share one device or use one each.
+class HostComm : public Comm {
+ public:
+  explicit HostComm(const pm_host_comm& h) : h_(h) {
+    if (!h.allgather || !h.allreduce_sum_u64 || !h.allreduce_sum_u32 || !h.alltoallv)
+      throw std::runtime_error("pm_host_comm: every collective must be given");
+  }
+  ~HostComm() override {
+    for (auto& b : buf_)
+      if (b.p) (void)hipHostFree(b.p);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    Timer timer(this);
+    count(bytes);
+    const int G = size();
+    char* hs = stage(0, bytes);
+    char* hr = stage(1, bytes * G);
+    to_host(hs, send, bytes, s);
+    check(h_.allgather(h_.user, hs, hr, bytes), "allgather");
+    to_device(recv, hr, bytes * G, s);
+  }
+  void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    Timer timer(this);
+    Comm::count(count * 8);
+    auto* h = reinterpret_cast<uint64_t*>(stage(0, count * 8));
+    to_host(h, buf, count * 8, s);
+    check(h_.allreduce_sum_u64(h_.user, h, count), "allreduce_sum_u64");
+    to_device(buf, h, count * 8, s);
+  }
+  void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    Timer timer(this);
+    Comm::count(count * 4);
+    auto* h = reinterpret_cast<uint32_t*>(stage(0, count * 4));
+    to_host(h, buf, count * 4, s);
+    check(h_.allreduce_sum_u32(h_.user, h, count), "allreduce_sum_u32");
+    to_device(buf, h, count * 4, s);
+  }
+  void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
+                 hipStream_t s) override {
+    Timer timer(this);
+    const int G = size();
+    uint64_t so = 0, ro = 0;
+    for (int g = 0; g < G; ++g) {
+      so += sbytes[g];
+      ro += rbytes[g];
+    }
+    count(so);
+    char* hs = stage(0, so);
+    char* hr = stage(1, ro);
+    to_host(hs, send, so, s);
+    check(h_.alltoallv(h_.user, hs, sbytes, hr, rbytes), "alltoallv");
+    to_device(recv, hr, ro, s);
+  }
+
+ private:
+  struct Buf {
+    char* p = nullptr;
+    size_t cap = 0;
+  };
+  int size() const { return static_cast<int>(h_.nshards); }
+  char* stage(int k, size_t bytes) {
+    Buf& b = buf_[k];
+    if (b.cap < bytes || !b.p) {
+      if (b.p) (void)hipHostFree(b.p);
+      b.p = nullptr;
+      const size_t cap = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+      PM_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.p), cap, hipHostMallocDefault));
+      b.cap = cap;
+    }
+    return b.p;
+  }
+  static void to_host(void* h, const void* d, size_t bytes, hipStream_t s) {
+    if (bytes) PM_HIP_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (also orders the caller's kernels before the exchange)
+  }
+  static void to_device(void* d, const void* h, size_t bytes, hipStream_t s) {
+    if (bytes) PM_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the staging buffer is reused by the next call)
+  }
+  static void check(int rc, const char* what) {
+    if (rc != 0) throw std::runtime_error(std::string("pm_host_comm ") + what + " failed (" + std::to_string(rc) + ")");
+  }
+  pm_host_comm h_;
+  Buf buf_[2];
+};
+
+Comm* make_host_comm(const pm_host_comm& h) { return new HostComm(h); }
+
+// ---------------------------------------------------------------------------
 // Threads of one process, all shards on one device (parity tests on a
 // one-GPU box).  Shards compute one at a time (ThreadGroup::device is held
 // outside collectives), so their kernels never share the chip; a collective
@@ -170,6 +273,8 @@ class ThreadComm : public Comm {
  public:
   ThreadComm(ThreadGroup* g, int rank) : g_(g), rank_(rank) {}
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    Timer timer(this);
+    count(bytes);
     PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     g_->ptrs[rank_] = send;
@@ -185,6 +290,8 @@ class ThreadComm : public Comm {
     g_->barrier();
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    Timer timer(this);
+    Comm::count(count * 8);
     PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     std::vector<uint64_t> h(count), sum(count, 0);
@@ -199,6 +306,8 @@ class ThreadComm : public Comm {
     PM_HIP_CHECK(hipStreamSynchronize(s));
   }
   void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    Timer timer(this);
+    Comm::count(count * 4);
     PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     std::vector<uint32_t> h(count);
@@ -217,6 +326,10 @@ class ThreadComm : public Comm {
   }
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                  hipStream_t s) override {
+    Timer timer(this);
+    uint64_t sent = 0;
+    for (int q = 0; q < g_->n; ++q) sent += sbytes[q];
+    count(sent);
     PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     const int G = g_->n;
@@ -572,6 +685,14 @@ static void ensure_xcnt(Ctx& c) {
   if (!c.d_xcnt) PM_HIP_CHECK(hipMalloc(&c.d_xcnt, (64 + 4 * 64) * sizeof(uint64_t)));
 }
 
+uint64_t shard_agree_min(Ctx& c, uint64_t v) {
+  if (!c.comm || c.nshards <= 1) return v;
+  ensure_xcnt(c);
+  PM_HIP_CHECK(hipMemcpyAsync(c.d_xcnt, &v, sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
+  const std::vector<uint64_t> all = gather_counts(c, 1);  // (synchronises the stream: v may leave scope)
+  return *std::min_element(all.begin(), all.end());
+}
+
 
 void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
   if (!c.comm || !c.split_hubs) return;
@@ -859,6 +980,8 @@ void shard_replicate(Ctx& c) {
   PM_HIP_CHECK(hipGetLastError());
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));  // (nrows lives on the host stack)
   c.nS_host = nrows;
+  c.replica_rows = rows;
+  c.replica_entries = ents;
   c.slist_compacted = true;
   c.smask_valid = false;
   c.k1_dense = false;

@@ -6,6 +6,7 @@
 #include <mutex>
 #include <vector>
 
+#include "../../include/pm_abi.h"
 #include "pm_internal.hpp"
 
 namespace pm {
@@ -31,5 +32,6 @@ Comm* make_rccl_comm(const void* unique_id, int nranks, int rank);
 size_t rccl_unique_id(void* out, size_t len);
 int rccl_selftest(int device, uint64_t bytes, int op);
 Comm* make_thread_comm(ThreadGroup* g, int rank);
+Comm* make_host_comm(const pm_host_comm& h);  // host-staged collectives of the caller (pm_abi.h)
 
 }  // namespace pm

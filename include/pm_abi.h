@@ -108,6 +108,23 @@ typedef struct pm_run_stats {
   double nlcc_seconds;          /* NLC lines of the search: device time of the fused line launches (first
                                    block start to the last line's end) + host time of exact-path lines */
   uint64_t split_lines;         /* sharded: NLC lines run split by owner (sources over the shards)      */
+  uint64_t line_overflows;      /* fused NLC launches that overflowed a capacity (the line reran with a grown
+                                   table, or on the exact path)                                          */
+  uint64_t exact_lines;         /* NLC lines run on the exact per-position path                          */
+  /* This context's share of the work (a shard's own rows; the whole graph on one context):             */
+  uint64_t shard_entries;       /* adjacency entries held: owned rows + delegate shares                  */
+  uint64_t shard_rows;          /* nonempty rows held                                                     */
+  uint64_t shard_hub_entries;   /* entries of the delegate shares held                                   */
+  uint64_t shard_hubs_controlled; /* delegates whose state this shard holds (hub ordinal % nshards)      */
+  uint64_t shard_ss0_entries;   /* adjacency entries of label-matching rows superstep 0 scanned here     */
+  uint64_t shard_ss0_survivors; /* superstep-0 survivors of this shard's rows                            */
+  double shard_sharded_ms;      /* device time of the sharded part of the search (its start to the replica
+                                   hand-off) less the collectives' host time; 0 on one context            */
+  uint64_t comm_calls;          /* collectives the search issued                                          */
+  uint64_t comm_bytes;          /* bytes this shard contributed to them                                   */
+  uint64_t replica_rows;        /* rows / M entries of the replica at the hand-off                       */
+  uint64_t replica_entries;
+  double comm_seconds;          /* host time inside the collectives of the search                        */
 } pm_run_stats;
 
 /* One shard (rank) of a sharded search: the rows of ids v % nshards == shard. */
@@ -174,6 +191,30 @@ int pm_export_state(pm_ctx* ctx, uint16_t* tpub, uint32_t* mdeg, uint32_t* nbrs,
 int pm_comm_unique_id(uint8_t* out, uint64_t len);
 pm_ctx* pm_create_shard(const pm_shard_desc* shard, const char* pattern_dir, int device, const uint8_t* unique_id);
 
+/* Host-staged collectives supplied by the caller, for sharded searches whose processes exchange through
+ * the host instead of RCCL: an MPI communicator (the reference's transport, new_mailbox.hpp:358-405 and the
+ * delegate reductions of impl/vertex_data.hpp:114-126), a torch.distributed gloo group, or several processes
+ * sharing one device.  Every function is collective over the nshards processes, is called by every shard in
+ * the same order, gets host buffers and returns 0 on success:
+ *   allgather: recv receives nshards consecutive blocks of `bytes` (block g = shard g's send);
+ *   allreduce_sum_u64 / _u32: element-wise sum in place (wrapping);
+ *   alltoallv: block g of send (sbytes[g] bytes, blocks consecutive) goes to shard g; recv holds the blocks
+ *              from shards 0..nshards-1 consecutively (rbytes[g] bytes from shard g). */
+typedef struct pm_host_comm {
+  void* user;
+  uint32_t nshards;
+  uint32_t shard;
+  int (*allgather)(void* user, const void* send, void* recv, uint64_t bytes);
+  int (*allreduce_sum_u64)(void* user, uint64_t* buf, uint64_t count);
+  int (*allreduce_sum_u32)(void* user, uint32_t* buf, uint64_t count);
+  int (*alltoallv)(void* user, const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes);
+} pm_host_comm;
+
+/* pm_create_shard with the exchanges through `comm` (copied; its functions and user pointer must stay valid
+ * for the context's lifetime).  comm->nshards / comm->shard must equal shard->nshards / shard->shard. */
+pm_ctx* pm_create_shard_host_comm(const pm_shard_desc* shard, const char* pattern_dir, int device,
+                                  const pm_host_comm* comm);
+
 /* nshards shards of one search run by threads of this process on one device (the
  * partitioning of pm_create_shard with an in-process exchange): parity of the sharded
  * path on a single GPU.  labels may be NULL (degree labels). */
@@ -196,6 +237,12 @@ pm_ctx* pm_create_rmat_shard(uint64_t scale, uint64_t p_gen, const char* pattern
 int pm_run_rmat_local_shards(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
                              uint32_t nranks, uint64_t hub_threshold, const char* result_dir, uint64_t max_iterations,
                              pm_run_stats* out);
+/* The same with labels (NULL: degree labels), the search run `repeats` times (>= 1; result files from the
+ * first run, statistics from the last) and every shard's statistics: per_shard[q] for q < nshards (the
+ * partition balance and per-shard device times of the N-GPU layout, measured with the shards on one device). */
+int pm_run_rmat_local_shards2(uint64_t scale, uint64_t p_gen, const char* pattern_dir, int device, uint32_t nshards,
+                              uint32_t nranks, uint64_t hub_threshold, const uint64_t* labels, const char* result_dir,
+                              uint64_t max_iterations, uint32_t repeats, pm_run_stats* per_shard);
 
 /* Host-side input builders (no device needed). */
 /* Directed pairs (u,v),(v,u) of generator ranks first, first + stride, ... < p_gen. */

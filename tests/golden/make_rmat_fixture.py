@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--p-gen", type=int, required=True)
     ap.add_argument("--pattern", default="rmat_log2_tree_pattern")
     ap.add_argument("--nranks", type=int, default=1)
+    ap.add_argument("--labels", default="degree",
+                    help="degree (vertex_data_db_degree) or hash:<alphabet>:<salt> (pmtest.hash_labels: config C5's "
+                         "explicit labels hash32(v ^ salt) % alphabet)")
     ap.add_argument("--timing-runs", type=int, default=2, help="extra oracle runs without result files (baseline)")
     ap.add_argument("--max-iterations", type=int, default=64)
     ap.add_argument("--out", required=True)
@@ -55,18 +58,24 @@ def main():
     t0 = time.time()
     g = pm.rmat_graph(a.scale, a.p_gen, device=0)
     print(f"graph S={a.scale} P_gen={a.p_gen}: V={g.n} E={g.nnz} in {time.time() - t0:.1f}s", flush=True)
+    labels = None
+    if a.labels != "degree":
+        kind, alphabet, salt = a.labels.split(":")
+        assert kind == "hash"
+        labels = pmtest.hash_labels(g.n, int(alphabet), salt=int(salt))
     threads = oracle.default_threads()
     td = tempfile.mkdtemp(prefix="pmfix")
     try:
         rd = os.path.join(td, "oracle")
         t0 = time.time()
-        st = oracle.run(g.off, g.col, pattern, rd, nranks=a.nranks, max_iterations=a.max_iterations, threads=threads)
+        st = oracle.run(g.off, g.col, pattern, rd, labels=labels, nranks=a.nranks, max_iterations=a.max_iterations,
+                        threads=threads)
         print(f"oracle run with result files: {st['seconds']:.2f}s search, {time.time() - t0:.1f}s total", flush=True)
         dig = pmtest.result_digest(rd, a.nranks)
         secs = [st["seconds"]]
         for i in range(a.timing_runs):
-            s2 = oracle.run(g.off, g.col, pattern, None, nranks=a.nranks, max_iterations=a.max_iterations,
-                            threads=threads)
+            s2 = oracle.run(g.off, g.col, pattern, None, labels=labels, nranks=a.nranks,
+                            max_iterations=a.max_iterations, threads=threads)
             secs.append(s2["seconds"])
             assert s2["lcc_edges"] == st["lcc_edges"] and s2["final_vertices"] == st["final_vertices"]
             print(f"oracle timing run {i}: {s2['seconds']:.2f}s", flush=True)
@@ -75,9 +84,9 @@ def main():
     edges = st["lcc_edges"] + st["nlcc_edges"] + st["tds_edges"]
     med = sorted(secs)[len(secs) // 2]
     out = {
-        "what": f"oracle result digest: R-MAT S={a.scale} P_gen={a.p_gen}, degree labels, {a.pattern}, "
+        "what": f"oracle result digest: R-MAT S={a.scale} P_gen={a.p_gen}, {a.labels} labels, {a.pattern}, "
                 f"nranks={a.nranks} (tests/golden/make_rmat_fixture.py)",
-        "scale": a.scale, "p_gen": a.p_gen, "pattern": a.pattern, "nranks": a.nranks,
+        "scale": a.scale, "p_gen": a.p_gen, "pattern": a.pattern, "nranks": a.nranks, "labels": a.labels,
         "vertices": g.n, "directed_entries": g.nnz,
         "stats": {k: st[k] for k in ("iterations", "terminated", "lcc_edges", "nlcc_edges", "tds_edges", "paths",
                                      "final_vertices", "final_edges", "lcc_calls", "supersteps")},

@@ -212,7 +212,7 @@ def test_c4_s28_tree_one_gpu(tmp_path):
     print(f"S=28 parity vs the oracle fixture: {sg}")
 
 
-@pytest.mark.parametrize("nshards", [2])
+@pytest.mark.parametrize("nshards", [2, 4, 8])
 def test_c4_s28_sharded_delegates_one_gpu(nshards, tmp_path):
     """C4's sharded path at full size on one GPU: pm_run_rmat_local_shards(S=28, P_gen=8, tree, -d 1048576)
     with `nshards` shards as threads of this process (the RCCL exchanges replaced by the in-process Comm):
@@ -220,16 +220,35 @@ def test_c4_s28_sharded_delegates_one_gpu(nshards, tmp_path):
     the delegates' rows (degree >= 1048576) are split by target owner and meet at their controllers, the
     survivors' codes are all-gathered and the state is replicated.  The result must equal the oracle's S=28
     digest (LCC and TDS results are partition-independent; the fixture's result files are
-    written with one rank, so no rank attribution differs)."""
+    written with one rank, so no rank attribution differs).  nshards = 8 is BASELINE C4's partition: every
+    shard holds delegate shares and the controllers spread over the shards.  The per-shard balance (entries,
+    rows, delegate shares, superstep-0 work, device time of the sharded part, exchanged bytes) goes to
+    $PM_STATS_DIR/c4_s28_shards<N>.json when that is set."""
     fixture = os.path.join(pmtest.ROOT, "tests", "golden", "rmat_s28_p8_tree.json")
     import json
     fx = json.load(open(fixture))
     _graphs.clear()
     out = tmp_path / "shards"
-    sg = pm.run_rmat_local_shards(28, 8, TREE, nshards, str(out), max_iterations=64, nranks=1,
-                                  hub_threshold=pm.DEFAULT_HUB_THRESHOLD)
+    each = pm.run_rmat_local_shards_each(28, 8, TREE, nshards, str(out), max_iterations=64, nranks=1,
+                                         hub_threshold=pm.DEFAULT_HUB_THRESHOLD, repeats=3)
+    sg = each[0]
     print(f"S=28 sharded x{nshards}: {sg['hubs']} delegates at -d {pm.DEFAULT_HUB_THRESHOLD}, {sg}")
+    keys = ("shard_entries", "shard_rows", "shard_hub_entries", "shard_hubs_controlled", "shard_ss0_entries",
+            "shard_ss0_survivors", "lcc_first_kernel_ms", "shard_sharded_ms", "comm_calls", "comm_bytes",
+            "replica_rows", "replica_entries", "nlcc_seconds", "device_seconds")
+    table = {k: [s[k] for s in each] for k in keys}
+    for k in keys[:6] + ("lcc_first_kernel_ms", "shard_sharded_ms"):
+        v = table[k]
+        print(f"  {k}: max/mean {max(v) / max(sum(v) / len(v), 1e-12):.3f}  {v}")
+    if os.environ.get("PM_STATS_DIR"):
+        os.makedirs(os.environ["PM_STATS_DIR"], exist_ok=True)
+        with open(os.path.join(os.environ["PM_STATS_DIR"], f"c4_s28_shards{nshards}.json"), "w") as f:
+            json.dump({"nshards": nshards, "per_shard": table, "stats": sg}, f, indent=1)
     assert sg["hubs"] > 0  # hubs exist at C4's threshold: the delegate split runs
+    assert sum(table["shard_entries"]) == 32 << 28  # every directed entry held by exactly one shard
+    assert all(x > 0 for x in table["shard_hub_entries"])  # every shard holds delegate shares
+    assert sum(x > 0 for x in table["shard_hubs_controlled"]) >= min(2, nshards)  # controllers spread
+    assert sum(table["shard_hubs_controlled"]) == sg["hubs"]
     diffs = pmtest.digest_diffs(fx["digest"], pmtest.result_digest(str(out), 1))
     for k_g, k_o in (("iterations", "iterations"), ("terminated", "terminated"), ("final_vertices", "final_vertices"),
                      ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"),

@@ -145,6 +145,28 @@ def test_split_lines_match_oracle(pat, scale, p_gen, alphabet, nranks, shards, t
     assert so["nlcc_edges"] + so["tds_edges"] > 0
 
 
+@pytest.mark.parametrize("nogrow", [None, 1])
+def test_split_line_overflow_agreed(nogrow, tmp_path, monkeypatch):
+    """A split line overflows a tiny (source, vertex) table on every shard (the table and the arena have one
+    size on every shard), and the shards agree whether to grow it: with room on all of them every shard reruns
+    the line fused and split (its collectives); with PM_DEBUG_NOGROW_SHARD=1 shard 1 has no room, so every
+    shard takes the exact path (no collectives) -- a shard-local decision hung the split line's all-gathers."""
+    monkeypatch.setenv("PM_SPLIT_LINES", "1")
+    monkeypatch.setenv("PM_HASH_SLOTS", "1024")
+    if nogrow is not None:
+        monkeypatch.setenv("PM_DEBUG_NOGROW_SHARD", str(nogrow))
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS["cycle"], tmp_path, 3, labels, 2)
+    assert diffs == []
+    _check(so, sg)
+    assert sg["line_overflows"] > 0
+    if nogrow is None:
+        assert sg["split_lines"] > 0
+    else:
+        assert sg["exact_lines"] > 0
+
+
 def test_sharded_exact_count_lines(tmp_path, monkeypatch):
     monkeypatch.setenv("PM_FUSED_LINES", "0")
     g = pm.rmat_graph(12, 4)
