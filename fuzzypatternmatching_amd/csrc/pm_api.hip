@@ -281,6 +281,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->any_sv = any_sv;
   if (const char* e = std::getenv("PM_SPLIT_LINES")) c->split_min = std::strtoull(e, nullptr, 10);
   if (const char* e = std::getenv("PM_HASH_SLOTS")) c->hash_slots = std::strtoull(e, nullptr, 10);
+  if (const char* e = std::getenv("PM_HANDOFF")) c->handoff_ss = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("PM_DEBUG_NOGROW_SHARD")) c->nogrow_shard = std::strtoll(e, nullptr, 10);
   // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
   // asymmetric M then aborts the search: tests use it to find such inputs)
@@ -410,6 +411,31 @@ void debug_point(Ctx& c, const char* where) {
   if (level >= 2) std::fprintf(stderr, "[pm dbg] shard %u: %s ok\n", c.shard, where);
 }
 
+// PM_DEBUG_WATCH_ID=<vertex id> (diagnostics): the vertex's state on this shard at the named point.
+static void debug_watch(Ctx& c, const char* where) {
+  static const char* e = std::getenv("PM_DEBUG_WATCH_ID");
+  if (!e || c.perm_host.empty()) return;
+  const uint64_t id = std::strtoull(e, nullptr, 10);
+  uint32_t p = 0;
+  PM_HIP_CHECK(hipMemcpy(&p, c.d_pos + id, 4, hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  uint16_t t0 = 0, t1 = 0, ts = 0;
+  uint32_t ml = 0, ma = 0, ns = 0;
+  PM_HIP_CHECK(hipMemcpy(&t0, c.d_tpub[0] + p, 2, hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(&t1, c.d_tpub[1] + p, 2, hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(&ts, c.d_tst + p, 2, hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(&ml, c.d_mlen + p, 4, hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(&ma, c.d_malive + p, 4, hipMemcpyDeviceToHost));
+  PM_HIP_CHECK(hipMemcpy(&ns, c.d_nS, 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> sl(ns);
+  if (ns) PM_HIP_CHECK(hipMemcpy(sl.data(), c.d_slist, ns * 4, hipMemcpyDeviceToHost));
+  int at = -1;
+  for (uint32_t i = 0; i < ns; ++i)
+    if (sl[i] == p) at = static_cast<int>(i);
+  std::fprintf(stderr, "[pm watch] shard %u %-22s id %llu pos %u: tpub %u/%u (cur %d) tst %u mlen %u malive %u, slist[%d] of %u\n",
+               c.shard, where, static_cast<unsigned long long>(id), p, t0, t1, c.cur, ts, ml, ma, at, ns);
+}
+
 // Pinned host staging of at least `words` u64 (read-backs of the driver loop).
 uint64_t* pinned(Ctx& c, size_t words) {
   if (c.h_pin_words < words) {
@@ -441,12 +467,16 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     c.events.push_back(e);
   }
   std::vector<hipEvent_t>& ev = c.events;  // [0..D] superstep bounds, [D+1], [D+2] superstep-0 kernel
+  // (a dense superstep-0 state is never packed: with D >= 2 the hand-off follows a later superstep)
+  const uint64_t handoff_ss = D == 1 ? 0 : std::max<uint64_t>(1, std::min<uint64_t>(c.handoff_ss, D - 1));
   zero_later(c, c.d_counts, D * W * sizeof(uint64_t));  // kernels add into the slots
   // the search's reset fills go with superstep 0's own (one launch, before the call's timing event)
   if (init_step) queue_lcc_first_fills(c);
   flush_zero(c);
   PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
   bool k_timed = false, handed_off = false;
+  // diagnostics: PM_DEBUG_LCC_STOP=k -- the first call runs supersteps 0..k-1 only
+  static const uint64_t stop_at = std::getenv("PM_DEBUG_LCC_STOP") ? std::strtoull(std::getenv("PM_DEBUG_LCC_STOP"), nullptr, 10) : 0;
   // sharded: the state became the replica (the sharded part of the search ends here)
   auto handoff = [&] {
     if (!c.comm) return;
@@ -456,11 +486,15 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     handed_off = true;
   };
   for (uint64_t ss = 0; ss < D; ++ss) {
+    if (init_step && stop_at && ss >= stop_at) {
+      PM_HIP_CHECK(hipEventRecord(ev[D], c.stream));
+      break;
+    }
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
       launch_lcc_first(c, slot, ev[D + 1], ev[D + 2]);
-      debug_point(c, "superstep 0");
+      debug_point(c, "superstep 0"); debug_watch(c, "superstep 0");
       k_timed = true;
       // |slist| is read back with the counters at the end of the call; until
       // then later supersteps size their grids by its upper bound
@@ -469,13 +503,13 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
       // sharded: the delegates' shares meet at their controllers; the survivors' codes of every shard
       // for the next superstep's pulls; a one-superstep pattern goes to the replica at once
       if (c.split_hubs) shard_hub_combine(c, slot);
-      debug_point(c, "delegate combine");
-      if (D >= 2) shard_codes_after_first(c);
+      debug_point(c, "delegate combine"); debug_watch(c, "delegate combine");
+      if (handoff_ss > 0) shard_codes_after_first(c);
       else {
         shard_replicate(c);
         handoff();
       }
-      debug_point(c, "code exchange / replica");
+      debug_point(c, "code exchange / replica"); debug_watch(c, "code exchange / replica");
     } else {
       if (!c.lcc_started) throw std::runtime_error("LCC without an initial step: state map is empty");
       // pull form while M is known symmetric (the first call on a symmetric
@@ -487,16 +521,19 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         // entries inside the superstep, one counter reservation per 64-entry chunk, measured 1.2 ms slower
         // at S=28: 153 k atomics on one address serialise.)
         launch_lcc_step(c, slot, init_step && ss == 1);
-        debug_point(c, "pull superstep");
+        debug_point(c, "pull superstep"); debug_watch(c, "pull superstep");
         if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
-        debug_point(c, "list compaction");
+        debug_point(c, "list compaction"); debug_watch(c, "list compaction");
       }
-      // sharded: after the first later superstep the state of S goes to the replica
-      if (init_step && ss == 1) {
+      // sharded: the state of S goes to the replica after superstep handoff_ss; before, the supersteps run
+      // over each shard's own rows, and after the first the shards' new T_pub are exchanged
+      if (init_step && ss == handoff_ss) {
         shard_replicate(c);
         handoff();
+      } else if (init_step && ss < handoff_ss) {
+        shard_tpub_exchange(c);
       }
-      debug_point(c, "superstep end");
+      debug_point(c, "superstep end"); debug_watch(c, "superstep end");
     }
     if (c.fine_timing || ss + 1 == D) PM_HIP_CHECK(hipEventRecord(ev[ss + 1], c.stream));
   }
@@ -510,7 +547,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));  // + stamp
   // sharded: the supersteps before the replica counted this shard's rows only: their slots are summed
   // over the shards (the replica's supersteps count the whole state on every shard)
-  const uint64_t sharded_slots = c.comm && init_step ? std::min<uint64_t>(D, 2) : 0;
+  const uint64_t sharded_slots = c.comm && init_step ? handoff_ss + 1 : 0;
   if (sharded_slots) {  // this shard's counts, then the sums over the shards
     PM_HIP_CHECK(hipMemcpyAsync(pin + 1, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.comm->allreduce_sum_u64(c.d_counts, sharded_slots * W, c.stream);
@@ -803,6 +840,22 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
       first_edges = lo.loc_edges;
     }
     record_lcc(lo, itr);
+    if (was_init && c.shard == 0 && std::getenv("PM_DEBUG_STATE_DUMP")) {  // diagnostics: the state after it
+      std::vector<uint16_t> tp;
+      std::vector<uint32_t> md, nb;
+      export_state(c, tp, md, nb);
+      std::ofstream f(std::getenv("PM_DEBUG_STATE_DUMP"));
+      uint64_t at = 0;
+      for (uint64_t v = 0; v < c.n; ++v) {
+        if (!tp[v]) continue;
+        std::vector<uint32_t> row(nb.begin() + at, nb.begin() + at + md[v]);
+        std::sort(row.begin(), row.end());
+        f << v << " " << tp[v] << " :";
+        for (auto x : row) f << " " << x;
+        f << "\n";
+        at += md[v];
+      }
+    }
     nf = nf || lo.not_finished;
     if (lines_on) f.step.push_back(std::to_string(itr) + ", LP, " + fmt_double(since(t_lp)));
     init_step = false;

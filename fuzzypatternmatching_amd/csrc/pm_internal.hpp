@@ -210,6 +210,13 @@ __host__ __device__ inline uint32_t tpub_code(uint32_t T, uint32_t tu) {
   return ((T & tu & (0u - tu)) ? 1u : 0u) | ((T & rest) ? 2u : 0u);
 }
 
+// A label on more than two template vertices: its code 3 means "read T_pub" (the position-indexed T_pub is
+// written); with one or two template vertices code 3 is just both bits, and T_pub lives in the code.
+__host__ __device__ inline bool tpub_wide(uint32_t tu) {
+  const uint32_t rest = tu & (tu - 1);
+  return (rest & (rest - 1)) != 0;
+}
+
 // The 2-bit T_pub codes are indexed by position inside the pattern's label runs (the runs packed one after
 // the other): only such positions are ever coded (members of S) or gathered (M entries), and at S=28 the
 // array is 22 MB instead of 64 MB for the first later superstep's 31 M random gathers.
@@ -242,6 +249,7 @@ struct LineStats {
   unsigned long long tstamp[4];  // s_memrealtime (100 MHz) at line start, after P1, after post, line end
   unsigned long long removed[2 * 64];  // vertices | edges per rank leaving S in post-processing
   unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)
+  unsigned long long census_tok;  // their first-position tokens (sum of |M[s]|): the line's work estimate
   unsigned long long ptime[20];  // s_memrealtime at the end of each position's phase (diagnostics, PM_PHASE_TIMES)
 };
 
@@ -325,6 +333,9 @@ struct Ctx {
   Comm* comm_owned = nullptr;     // deleted with the context
   uint64_t mcap = 0;              // capacity (entries) of d_colp and d_mcol (nq; + kTileEntries tail padding)
   bool replicated = false;        // the search state is the replica (sharded, after shard_replicate)
+  // the later superstep of the first LCC call after which the state is replicated (sharded; PM_HANDOFF, default
+  // 2: at S=28 the second superstep still has 0.8 M rows, the third 26 k); capped at diameter - 1
+  uint32_t handoff_ss = 2;
   // delegates of a sharded search (hubs_host order; the shares are rows of this shard's layout)
   bool split_hubs = false;        // nshards > 1 and some vertex has degree >= hub_threshold
   uint64_t hub_area = 0;          // entries behind the dense region: M rows of the hubs this shard controls
@@ -475,11 +486,12 @@ struct Ctx {
   uint64_t live_hint = ~0ull;     // S members on this context after the last LCC call (line grid size)
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
   bool any_sv = false;            // some line has selected_vertices (token-source sets span lines)
-  // sharded search on the replica: an NLC line whose census (sources on the replica) reaches split_min runs
-  // split by owner -- every shard passes the tokens of the sources it owns (hub ordinal % nshards, else
-  // id % nshards) -- and the shards then exchange the line's effects (pm_shard.hip split_line_finish);
-  // smaller lines run replicated (every shard all sources, no exchange).  0: never split.  PM_SPLIT_LINES.
-  uint64_t split_min = 16384;
+  // sharded search on the replica: an NLC line whose work census (first-position tokens of its sources on the
+  // replica, sum of |M[s]|) reaches split_min runs split by owner -- every shard passes the tokens of the
+  // sources it owns (hub ordinal % nshards, else id % nshards) -- and the shards then exchange the line's
+  // effects (pm_shard.hip split_line_finish); smaller lines run replicated (every shard all sources, no
+  // exchange: a split costs a launch and 2-4 all-gathers).  0: never split.  PM_SPLIT_LINES.
+  uint64_t split_min = 32768;
   unsigned long long* d_xsplit = nullptr;  // a split line's flagged M entries (replica entry indices), then
   uint64_t xsplit_cap = 0;                 // the shard's cleared sources (positions) of its post-processing
   bool force_pull = false;        // PM_FORCE_PULL=1 (diagnostics): pull-form LCC in every call
@@ -612,6 +624,8 @@ bool split_line_finish(Ctx& c, size_t pl, const LineStats& st, const uint32_t* k
 void shard_hub_combine(Ctx& c, uint64_t* d_slot);
 void shard_codes_after_first(Ctx& c);  // after superstep 0: every shard's survivors' T_pub codes
 void shard_replicate(Ctx& c);          // the state of S of every shard -> the replica (collective)
+// after the first later superstep when the replica is built after the second: every shard's S rows' T_pub
+void shard_tpub_exchange(Ctx& c);
 std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  // host vector, sum
 // The minimum of v over the shards (v itself without a communicator): capacities that steer the replicated
 // part of a sharded search (arena, line hash table) must be the same on every shard, or an overflow -- and the

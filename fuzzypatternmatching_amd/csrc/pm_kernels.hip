@@ -260,8 +260,10 @@ __device__ __forceinline__ bool k1_finish_row(uint32_t u, uint32_t cdelta, uint1
   const uint32_t ci = u + cdelta;
   atomicOr(&o.tcode[ci >> 4], tpub_code(T, tu) << ((ci & 15u) << 1));
   // dense mode: T_pub in the record (a heavy row's M stays in its padded row: no first entry); a
-  // label of more than two template vertices also keeps its position-indexed T_pub (code 3 gathers)
-  if (!o.rarea || tpub_code(T, tu) == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+  // label of more than two template vertices also keeps its position-indexed T_pub (code 3 gathers).  (Not
+  // code 3 of a two-vertex label: both bits -- the removed rows of the next superstep rely on both T_pub
+  // buffers being clean.)
+  if (!o.rarea || tpub_wide(tu)) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
   if (oa.nranks <= 1) {
     acc.vs += 1;
     acc.es += cnt;
@@ -598,7 +600,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
       // survivor lanes -- measured 1.94 / 1.89 ms per launch instead of 1.47 although it cut WRITE to 0.38 GB)
       const uint32_t ci = cstart + row;
       if (!(MODE & 1024)) atomicOr(&o.tcode[ci >> 4], code << ((ci & 15u) << 1));
-      if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + u * 2u) = T;
+      if (tpub_wide(tu)) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + u * 2u) = T;
       const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(sb >> 32),
                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(sb), 0));
       // the head's kidx: the kept entries before its row (consecutive lanes) = its first dense entry
@@ -705,7 +707,7 @@ __device__ __forceinline__ void k1_light_tile(const uint32_t (&v)[kSub], uint32_
           }
           // a label of more than two template vertices keeps its position-indexed T_pub (the next
           // superstep's code-3 gathers)
-          if (code == 3u) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
+          if (tpub_wide(tu)) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(o.tpub) + b2) = T;
           const uint64_t rslot = rcur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0));
           o.rarea[rslot] = k1_record(u, T, cnt, dense ? static_cast<uint32_t>(dpos + mrun + incl - c) : kNone,

@@ -1062,17 +1062,20 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     for (int pl = a.pl_begin; pl < a.pl_end; ++pl) {
       const LineArgs& la = a.lines[pl].la;
       const bool tds = a.lines[pl].tds != 0;
-      uint64_t cnt = 0;
+      uint64_t cnt = 0, tok = 0;
       for (uint64_t i0 = g.gw * kWave; i0 < nact; i0 += g.nw * kWave) {
         const uint64_t i = i0 + lane_id();
         if (i < nact) {
-          const uint16_t T = a.tpub[ld_dev(&a.act[i])];
+          const uint32_t s = ld_dev(&a.act[i]);
+          const uint16_t T = a.tpub[s];
           bool ok = T && pos_ok(T, 0, la);
           if (ok && !tds && !la.VC && !((T >> la.ilast) & 1u)) ok = false;
           cnt += ok ? 1u : 0u;
+          tok += ok ? a.malive[s] : 0u;
         }
       }
       wave_add(&a.st[pl].census, cnt);
+      if (a.split_min) wave_add(&a.st[pl].census_tok, tok);
     }
     tree_barrier(a.gbar);
   }
@@ -1087,7 +1090,7 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     // a split line is decided on an exact census only -- the replica's sources, identical on every shard --
     // so every shard splits the same lines: after a line of this launch changed the state the census is a
     // bound, and a line it would split ends the launch unprocessed (the next launch counts again)
-    const bool split = a.split_min && a.so.nranks > 1 && cen >= a.split_min;
+    const bool split = a.split_min && a.so.nranks > 1 && ld_dev(&a.st[pl].census_tok) >= a.split_min;
     if (split && !fresh) break;
     fresh = false;
     LineKernelArgs b = a;
@@ -1385,9 +1388,12 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   if (phase_times)
     for (unsigned j = 0; j + pl0 < done; ++j) {
       const LineStats& st = hs[j];
-      std::fprintf(stderr, "[pm] line %zu: P1 %.1f us, rest %.1f us, end barrier %.1f us (%s, %llu sources)\n",
+      std::fprintf(stderr,
+                   "[pm] line %zu: P1 %.1f us, rest %.1f us, end barrier %.1f us (%s, %llu sources, census %llu "
+                   "sources / %llu tokens%s)\n",
                    pl0 + j, (st.tstamp[1] - st.tstamp[0]) * 0.01, (st.tstamp[2] - st.tstamp[1]) * 0.01,
-                   (st.tstamp[3] - st.tstamp[2]) * 0.01, st.single ? "block 0" : "grid", st.nsrc);
+                   (st.tstamp[3] - st.tstamp[2]) * 0.01, st.single ? "block 0" : "grid", st.nsrc, st.census,
+                   st.census_tok, st.split ? ", split" : "");
       std::string pos = "[pm]   positions (walks in, us, long-row pieces):";
       unsigned long long prev = st.tstamp[1];
       for (int k = 1; k < 20 && st.ptime[k]; ++k) {

@@ -466,8 +466,8 @@ __global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t*
                              const uint16_t* __restrict__ tpub, const uint16_t* __restrict__ tst,
                              const uint32_t* __restrict__ mlen, const uint64_t* __restrict__ moff,
                              const uint32_t* __restrict__ mcol, uint32_t* __restrict__ rec, uint32_t* __restrict__ ent,
-                             uint64_t ent_cap,
-                             unsigned long long* __restrict__ totals) {
+                             uint64_t ent_cap, uint64_t nv,
+                             unsigned long long* __restrict__ totals, unsigned long long* __restrict__ err) {
   const uint64_t n = min(static_cast<uint64_t>(*nSp), cap);
   for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
     if (i == n - 1) {
@@ -488,8 +488,14 @@ __global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t*
     uint64_t k = e0;
     for (uint32_t j = 0; j < L; ++j) {
       const uint32_t m = mcol[b + j];
-      if ((m & kAlive) && k < ent_cap) ent[k++] = m;
+      if (!(m & kAlive)) continue;
+      if ((m & kPosMask) >= nv) {  // (not an M entry: the row's bounds are wrong -- reported, not packed)
+        atomicCAS(err, 0ull, (1ull << 63) | u);
+        continue;
+      }
+      if (k < ent_cap) ent[k++] = m;
     }
+    if (k - e0 != cnt[i]) atomicCAS(err, 0ull, (1ull << 62) | u);  // |M| disagrees with the alive entries
   }
   if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) totals[0] = totals[1] = 0;
 }
@@ -621,9 +627,9 @@ __global__ void k_hub_finish(HubFinishArgs a) {
       } else {
         a.tst[p] = T;
         // with superstep-0 records T_pub travels in the record (k1_finish_row's rule): the position-indexed
-        // T_pub is written only for code 3 (gathered by the next superstep), so a hub that superstep removes
-        // leaves both T_pub buffers clean
-        if (!a.srec || tpub_code(T, tu) == 3u) a.tpub[p] = T;
+        // T_pub is written only for a label on more than two template vertices (gathered by the next
+        // superstep), so a hub that superstep removes leaves both T_pub buffers clean
+        if (!a.srec || tpub_wide(tu)) a.tpub[p] = T;
         a.mlen[p] = static_cast<uint32_t>(cnt);
         a.malive[p] = static_cast<uint32_t>(cnt);
         const uint32_t ci = code_index(p, a.lr);
@@ -802,6 +808,66 @@ void shard_codes_after_first(Ctx& c) {
   PM_HIP_CHECK(hipGetLastError());
 }
 
+// After the first later superstep, when the state is replicated only after the second (Ctx::handoff_ss): the
+// second superstep pulls T_pub of its rows' M entries, which live on every shard.  Each shard's rows of S
+// (its compacted slist) go out as {position, T_pub} records; the other shards' records land in the T_pub
+// buffer that superstep reads, and are cleared from it after the superstep (shard_replicate, the code-clear
+// path) so that T_pub stays zero outside the replica's rows.  At S=28: 0.80 M records, 6.4 MB over the shards.
+__global__ void k_pack_tpub(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
+                            const uint16_t* __restrict__ tpub, unsigned long long* __restrict__ out) {
+  const uint64_t n = *nSp;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t p = slist[i];
+    out[i] = p | (static_cast<unsigned long long>(tpub[p]) << 32);
+  }
+}
+
+__global__ void k_unpack_tpub(const unsigned long long* __restrict__ in, uint64_t maxS, uint32_t G, uint32_t me,
+                              XCounts x, uint16_t* __restrict__ tpub) {
+  const uint64_t total = uint64_t(G) * maxS;
+  for (uint64_t j = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; j < total; j += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t g = static_cast<uint32_t>(j / maxS);
+    if (g == me || j % maxS >= x.n[g]) continue;
+    const unsigned long long r = in[j];
+    tpub[static_cast<uint32_t>(r & 0x3FFFFFFFull)] = static_cast<uint16_t>(r >> 32);
+  }
+}
+
+void shard_tpub_exchange(Ctx& c) {
+  if (!c.comm || c.replicated) return;
+  ensure_xcnt(c);
+  const uint32_t G = c.nshards;
+  XCounts x{};
+  // u64 code mode: the other shards' superstep-0 T_pub in the buffer the first later superstep read (the
+  // second superstep writes into it)
+  if (c.xcode_in_tpub && !c.xcode_n.empty()) {
+    for (uint32_t g = 0; g < G; ++g) x.n[g] = c.xcode_n[g];
+    hipLaunchKernelGGL(k_clear_codes, dim3(xgrid(uint64_t(G) * c.xcode_max)), dim3(kXBlock), 0, c.stream,
+                       reinterpret_cast<const unsigned long long*>(c.d_xrecv), c.xcode_max, G, c.shard, x,
+                       c.d_tpub[c.cur ^ 1]);
+  }
+  c.xcode_n.clear();
+  c.xcode_in_tpub = false;
+  hipLaunchKernelGGL(k_count_to_u64, dim3(1), dim3(1), 0, c.stream, c.d_nS, c.d_xcnt);
+  const std::vector<uint64_t> n = gather_counts(c, 1);
+  uint64_t maxS = 1;
+  for (uint32_t g = 0; g < G; ++g) maxS = std::max(maxS, n[g]);
+  c.nS_host = static_cast<uint32_t>(n[c.shard]);
+  auto* send = grow<unsigned long long>(c.d_xsend, c.xsend_cap, maxS * 8);
+  auto* recv = grow<unsigned long long>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxS * 8);
+  hipLaunchKernelGGL(k_pack_tpub, dim3(xgrid(c.nS_host)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS,
+                     c.d_tpub[c.cur], send);
+  c.comm->allgather(send, recv, maxS * 8, c.stream);
+  for (uint32_t g = 0; g < G; ++g) x.n[g] = n[g];
+  hipLaunchKernelGGL(k_unpack_tpub, dim3(xgrid(uint64_t(G) * maxS)), dim3(kXBlock), 0, c.stream, recv, maxS, G,
+                     c.shard, x, c.d_tpub[c.cur]);
+  PM_HIP_CHECK(hipGetLastError());
+  // the records stay in d_xrecv: shard_replicate clears their positions from the second superstep's input
+  c.xcode_n = n;
+  c.xcode_max = maxS;
+  c.xcode_in_tpub = true;
+}
+
 void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t* counts);
 
 // The replica's hub rows in neighbour-id order.  A delegate's M row was assembled at its controller share by
@@ -820,9 +886,9 @@ __global__ void k_hub_rows(const HubInfo* __restrict__ info, uint32_t H, const u
 }
 
 __global__ void k_hub_gather(const uint64_t* __restrict__ seg, const uint64_t* __restrict__ src, uint32_t nseg,
-                             const uint32_t* __restrict__ rmcol, const uint32_t* __restrict__ perm,
+                             const uint32_t* __restrict__ rmcol, const uint32_t* __restrict__ perm, uint64_t nv,
                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, bool back,
-                             uint32_t* __restrict__ rmcol_out) {
+                             uint32_t* __restrict__ rmcol_out, unsigned long long* __restrict__ bad) {
   // segment k: entries [seg[k], seg[k + 1]) of the temporary arrays <-> rmcol[src[k] ..]
   const int lane = threadIdx.x & 63;
   for (uint32_t k = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; k < nseg; k += gridDim.x * (blockDim.x / 64)) {
@@ -832,7 +898,13 @@ __global__ void k_hub_gather(const uint64_t* __restrict__ seg, const uint64_t* _
         rmcol_out[r + i] = vals[b + i];
       } else {
         const uint32_t m = rmcol[r + i];
-        keys[b + i] = perm[m & kPosMask];
+        const uint32_t p = m & kPosMask;
+        if (p >= nv) {  // (not an M entry: reported, the key kept in range)
+          atomicCAS(bad, 0ull, (static_cast<unsigned long long>(k) << 32) | static_cast<uint32_t>(i));
+          keys[b + i] = 0;
+        } else {
+          keys[b + i] = perm[p];
+        }
         vals[b + i] = m;
       }
     }
@@ -849,6 +921,21 @@ static void sort_hub_rows(Ctx& c) {
   PM_HIP_CHECK(hipMemcpyAsync(rows.data(), d_rows, rows.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                               c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (std::getenv("PM_DEBUG_HUB_ROWS")) {  // diagnostics: the hubs with T_pub are the replica's rows, once each
+    std::vector<uint32_t> sl(c.nS_host);
+    if (c.nS_host) PM_HIP_CHECK(hipMemcpy(sl.data(), c.d_slist, sl.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> cntp(c.n, 0);
+    for (uint32_t p : sl) ++cntp[p];
+    for (uint32_t j = 0; j < H; ++j) {
+      const uint32_t p = c.hubinfo[j].pos;
+      if ((rows[2 * j + 1] || rows[2 * j]) && cntp[p] != 1)
+        std::fprintf(stderr, "[pm dbg] shard %u: hub %u (position %u, id %u) with T_pub in the replica %u times, "
+                     "row [%llu, +%llu)\n", c.shard, j, p, c.perm_host[p], cntp[p], rows[2 * j], rows[2 * j + 1]);
+    }
+    for (size_t i = 0; i < sl.size(); ++i)
+      if (cntp[sl[i]] > 1) std::fprintf(stderr, "[pm dbg] shard %u: replica row %zu: position %u (id %u) twice\n",
+                                        c.shard, i, sl[i], c.perm_host[sl[i]]);
+  }
   std::vector<uint64_t> seg(1, 0), src;
   for (uint32_t j = 0; j < H; ++j)
     if (rows[2 * j + 1] > 1) {
@@ -858,6 +945,11 @@ static void sort_hub_rows(Ctx& c) {
   const uint32_t ns = static_cast<uint32_t>(src.size());
   const uint64_t total = seg.back();
   if (!ns) return;
+  for (uint32_t k = 0; k < ns; ++k)  // every hub row of the replica lies inside its entries
+    if (src[k] + (seg[k + 1] - seg[k]) > c.replica_entries)
+      throw std::runtime_error("internal: replica row of a delegate [" + std::to_string(src[k]) + ", +" +
+                               std::to_string(seg[k + 1] - seg[k]) + ") outside the replica's " +
+                               std::to_string(c.replica_entries) + " entries (shard " + std::to_string(c.shard) + ")");
   auto* d_seg = static_cast<uint64_t*>(c.arena.get(seg.size() * sizeof(uint64_t)));
   auto* d_src = static_cast<uint64_t*>(c.arena.get(src.size() * sizeof(uint64_t)));
   auto* k0 = static_cast<uint32_t*>(c.arena.get(total * 4));
@@ -867,8 +959,17 @@ static void sort_hub_rows(Ctx& c) {
   PM_HIP_CHECK(hipMemcpyAsync(d_seg, seg.data(), seg.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
   PM_HIP_CHECK(hipMemcpyAsync(d_src, src.data(), src.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
   const unsigned g = static_cast<unsigned>(std::min<uint64_t>(ns, 4096) + 3) / 4;
-  hipLaunchKernelGGL(k_hub_gather, dim3(g), dim3(kXBlock), 0, c.stream, d_seg, d_src, ns, c.d_rmcol, c.d_perm, k0, v0,
-                     false, c.d_rmcol);
+  auto* d_bad = static_cast<unsigned long long*>(c.arena.get(sizeof(unsigned long long)));
+  PM_HIP_CHECK(hipMemsetAsync(d_bad, 0, sizeof(unsigned long long), c.stream));
+  hipLaunchKernelGGL(k_hub_gather, dim3(g), dim3(kXBlock), 0, c.stream, d_seg, d_src, ns, c.d_rmcol, c.d_perm, c.n,
+                     k0, v0, false, c.d_rmcol, d_bad);
+  unsigned long long bad = 0;
+  PM_HIP_CHECK(hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (bad)
+    throw std::runtime_error("internal: replica row of a delegate (segment " + std::to_string(bad >> 32) +
+                             ", entry " + std::to_string(bad & 0xFFFFFFFFull) + ") holds a non-position (shard " +
+                             std::to_string(c.shard) + ")");
   size_t tmp = 0;
   PM_HIP_CHECK(rocprim::segmented_radix_sort_pairs(nullptr, tmp, k0, k1, v0, v1, size_t(total), ns, d_seg, d_seg + 1,
                                                    0, 32, c.stream));
@@ -876,7 +977,7 @@ static void sort_hub_rows(Ctx& c) {
   PM_HIP_CHECK(rocprim::segmented_radix_sort_pairs(d_tmp, tmp, k0, k1, v0, v1, size_t(total), ns, d_seg, d_seg + 1,
                                                    0, 32, c.stream));
   hipLaunchKernelGGL(k_hub_gather, dim3(g), dim3(kXBlock), 0, c.stream, d_seg, d_src, ns,
-                     static_cast<const uint32_t*>(nullptr), c.d_perm, k1, v1, true, c.d_rmcol);
+                     static_cast<const uint32_t*>(nullptr), c.d_perm, c.n, k1, v1, true, c.d_rmcol, d_bad);
   PM_HIP_CHECK(hipGetLastError());
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));  // (seg / src live on the host stack)
 }
@@ -895,6 +996,7 @@ void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t
   const uint64_t cap = c.nS_host;
   // (the state right after superstep 0 is never packed: with dense M the first later superstep follows)
   if (c.k1_dense) throw std::runtime_error("internal: pack_state of a dense superstep-0 state");
+  ensure_xcnt(c);
   c.arena.reset();
   auto* keep = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
   auto* cnt = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
@@ -914,10 +1016,21 @@ void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t
   PM_HIP_CHECK(rocprim::exclusive_scan(tmp, t2, wc, eoff, uint64_t(0), size_t(cap), rocprim::plus<uint64_t>(),
                                        c.stream));
   // rec == nullptr: totals only (the rows are not written)
+  auto* err = reinterpret_cast<unsigned long long*>(c.d_xcnt + 60);
+  if (rec) PM_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), c.stream));
   hipLaunchKernelGGL(k_pack_write, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap, keep,
                      ridx, cnt, eoff, c.d_tpub[c.cur], c.d_tst, c.d_mlen, m_off(c), m_col(c), rec, ent,
-                     rec ? ent_cap : 0, reinterpret_cast<unsigned long long*>(counts));
+                     rec ? ent_cap : 0, c.n, reinterpret_cast<unsigned long long*>(counts), err);
   PM_HIP_CHECK(hipGetLastError());
+  if (rec && c.comm) {  // (a wrong row would corrupt every replica: checked before it is sent)
+    unsigned long long e = 0;
+    PM_HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(e), hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    if (e)
+      throw std::runtime_error(std::string("internal: state row of position ") + std::to_string(e & 0x3FFFFFFFull) +
+                               ((e >> 63) ? " holds a non-position entry" : " has |M| != its alive entries") +
+                               " (shard " + std::to_string(c.shard) + (c.replicated ? ", replica)" : ")"));
+  }
 }
 
 void shard_replicate(Ctx& c) {
@@ -986,7 +1099,7 @@ void shard_replicate(Ctx& c) {
   c.smask_valid = false;
   c.k1_dense = false;
   c.replicated = true;
-  if (c.split_hubs) {
+  if (c.split_hubs && !std::getenv("PM_DEBUG_NO_HUB_SORT")) {
     c.arena.reset();
     sort_hub_rows(c);
   }
