@@ -2323,9 +2323,9 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
     size_t tb = c.rscan_tmp_bytes;
     PM_HIP_CHECK(rocprim::exclusive_scan(c.d_rscan_tmp, tb, rit, c.d_rofs, uint64_t(0), size_t(c.rwaves),
                                          rocprim::plus<uint64_t>(), c.stream));
-    // one context: the first later superstep reads the records in place (no copy); a sharded context packs the
-    // survivors' codes from slist before that superstep, so it copies
-    c.records_in_place = !c.comm;
+    // the first later superstep reads the records in place (no copy); a sharded context whose labels need the
+    // wide code exchange packs every survivor's T_pub from the records before that superstep, so it copies
+    c.records_in_place = !c.comm || !c.xcode_wide;
     if (c.records_in_place) {
       if (!c.d_cdesc) PM_HIP_CHECK(hipMalloc(&c.d_cdesc, (c.rarea_cap / kWave + 2) * sizeof(uint4)));
       hipLaunchKernelGGL(k_chunk_slices, dim3(grid_for(c.rarea_cap / kWave + 1, kBlock, 1024)), dim3(kBlock), 0,

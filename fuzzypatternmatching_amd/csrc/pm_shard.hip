@@ -158,6 +158,7 @@ class HostComm : public Comm {
       if (b.p) (void)hipHostFree(b.p);
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     count(bytes);
     const int G = size();
@@ -168,6 +169,7 @@ class HostComm : public Comm {
     to_device(recv, hr, bytes * G, s);
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     Comm::count(count * 8);
     auto* h = reinterpret_cast<uint64_t*>(stage(0, count * 8));
@@ -176,6 +178,7 @@ class HostComm : public Comm {
     to_device(buf, h, count * 8, s);
   }
   void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     Comm::count(count * 4);
     auto* h = reinterpret_cast<uint32_t*>(stage(0, count * 4));
@@ -185,6 +188,7 @@ class HostComm : public Comm {
   }
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                  hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     const int G = size();
     uint64_t so = 0, ro = 0;
@@ -273,9 +277,9 @@ class ThreadComm : public Comm {
  public:
   ThreadComm(ThreadGroup* g, int rank) : g_(g), rank_(rank) {}
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     count(bytes);
-    PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     g_->ptrs[rank_] = send;
     g_->barrier();
@@ -290,9 +294,9 @@ class ThreadComm : public Comm {
     g_->barrier();
   }
   void allreduce_sum_u64(uint64_t* buf, size_t count, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     Comm::count(count * 8);
-    PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     std::vector<uint64_t> h(count), sum(count, 0);
     if (count) PM_HIP_CHECK(hipMemcpyAsync(h.data(), buf, count * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -306,9 +310,9 @@ class ThreadComm : public Comm {
     PM_HIP_CHECK(hipStreamSynchronize(s));
   }
   void allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     Comm::count(count * 4);
-    PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     std::vector<uint32_t> h(count);
     std::vector<uint64_t> hv(count);
@@ -326,11 +330,11 @@ class ThreadComm : public Comm {
   }
   void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                  hipStream_t s) override {
+    PM_HIP_CHECK(hipStreamSynchronize(s));  // (the shard's own work: not collective time)
     Timer timer(this);
     uint64_t sent = 0;
     for (int q = 0; q < g_->n; ++q) sent += sbytes[q];
     count(sent);
-    PM_HIP_CHECK(hipStreamSynchronize(s));
     DeviceReleased rel(g_);
     const int G = g_->n;
     g_->ptrs[rank_] = send;
@@ -459,7 +463,10 @@ __global__ void k_pack_count(const uint32_t* __restrict__ slist, const uint32_t*
   }
 }
 
-// pass 2: rows {position, T_pub | T_state << 16, |M|, first entry} and their alive entries.
+// pass 2: rows {position, T_pub | T_state << 16, |M|, first entry} and their alive entries.  A wave per 64
+// rows: rows of up to kPackShort entries are walked by their lane, longer ones (delegates: 10^5 entries at C5's
+// scale) by the whole wave in turn (a lane walking a hub row took 0.1 s).
+static constexpr uint32_t kPackShort = 32;
 __global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp, uint64_t cap,
                              const uint32_t* __restrict__ keep, const uint32_t* __restrict__ ridx,
                              const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ eoff,
@@ -469,33 +476,66 @@ __global__ void k_pack_write(const uint32_t* __restrict__ slist, const uint32_t*
                              uint64_t ent_cap, uint64_t nv,
                              unsigned long long* __restrict__ totals, unsigned long long* __restrict__ err) {
   const uint64_t n = min(static_cast<uint64_t>(*nSp), cap);
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-    if (i == n - 1) {
-      totals[0] = ridx[i] + keep[i];
-      totals[1] = eoff[i] + cnt[i];
-    }
-    if (!keep[i] || !rec) continue;
-    const uint32_t u = slist[i];
-    const uint64_t b = moff[u];
-    const uint32_t L = mlen[u];
-    const uint16_t T = tpub[u];
-    const uint64_t e0 = eoff[i];
-    uint32_t* r = rec + 4 * uint64_t(ridx[i]);
-    r[0] = u;
-    r[1] = T | (static_cast<uint32_t>(tst[u]) << 16);
-    r[2] = cnt[i];
-    r[3] = static_cast<uint32_t>(e0);
-    uint64_t k = e0;
-    for (uint32_t j = 0; j < L; ++j) {
-      const uint32_t m = mcol[b + j];
-      if (!(m & kAlive)) continue;
-      if ((m & kPosMask) >= nv) {  // (not an M entry: the row's bounds are wrong -- reported, not packed)
-        atomicCAS(err, 0ull, (1ull << 63) | u);
-        continue;
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = uint64_t(gridDim.x) * (blockDim.x / 64);
+  for (uint64_t ch = blockIdx.x * uint64_t(blockDim.x / 64) + threadIdx.x / 64; ch * 64 < n; ch += nw) {
+    const uint64_t i = ch * 64 + lane;
+    bool mine = false;
+    uint32_t u = 0, L = 0, c = 0;
+    uint64_t b = 0, e0 = 0;
+    if (i < n) {
+      if (i == n - 1) {
+        totals[0] = ridx[i] + keep[i];
+        totals[1] = eoff[i] + cnt[i];
       }
-      if (k < ent_cap) ent[k++] = m;
+      if (keep[i] && rec) {
+        u = slist[i];
+        b = moff[u];
+        L = mlen[u];
+        c = cnt[i];
+        e0 = eoff[i];
+        uint32_t* r = rec + 4 * uint64_t(ridx[i]);
+        r[0] = u;
+        r[1] = tpub[u] | (static_cast<uint32_t>(tst[u]) << 16);
+        r[2] = c;
+        r[3] = static_cast<uint32_t>(e0);
+        mine = true;
+      }
     }
-    if (k - e0 != cnt[i]) atomicCAS(err, 0ull, (1ull << 62) | u);  // |M| disagrees with the alive entries
+    if (mine && L <= kPackShort) {
+      uint64_t k = e0;
+      for (uint32_t j = 0; j < L; ++j) {
+        const uint32_t m = mcol[b + j];
+        if (!(m & kAlive)) continue;
+        if ((m & kPosMask) >= nv) {  // (not an M entry: the row's bounds are wrong -- reported, not packed)
+          atomicCAS(err, 0ull, (1ull << 63) | u);
+          continue;
+        }
+        if (k < ent_cap) ent[k++] = m;
+      }
+      if (k - e0 != c && e0 + c <= ent_cap) atomicCAS(err, 0ull, (1ull << 62) | u);  // |M| != alive entries
+    }
+    uint64_t lb = __ballot(mine && L > kPackShort);
+    while (lb) {
+      const int q = __ffsll(static_cast<long long>(lb)) - 1;
+      lb &= lb - 1;
+      const uint32_t uq = __shfl(u, q, 64), Lq = __shfl(L, q, 64), cq = __shfl(c, q, 64);
+      const uint64_t bq = __shfl(b, q, 64);
+      const uint64_t e0q = __shfl(e0, q, 64);
+      uint64_t k = e0q;
+      for (uint32_t j0 = 0; j0 < Lq; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const uint32_t m = j < Lq ? mcol[bq + j] : 0u;
+        const bool bad = (m & kAlive) && (m & kPosMask) >= nv;
+        if (bad) atomicCAS(err, 0ull, (1ull << 63) | uq);
+        const bool ok = (m & kAlive) && !bad;
+        const uint64_t bal = __ballot(ok);
+        const uint64_t at = k + __builtin_popcountll(bal & ((1ull << lane) - 1));
+        if (ok && at < ent_cap) ent[at] = m;
+        k += __builtin_popcountll(bal);
+      }
+      if (lane == 0 && k - e0q != cq && e0q + cq <= ent_cap) atomicCAS(err, 0ull, (1ull << 62) | uq);
+    }
   }
   if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) totals[0] = totals[1] = 0;
 }
@@ -781,6 +821,15 @@ void shard_hub_combine(Ctx& c, uint64_t* d_slot) {
 
 void shard_codes_after_first(Ctx& c) {
   if (!c.comm || c.replicated) return;
+  if (!c.xcode_wide) {
+    // a position's 2-bit code is set only by the shard that holds its row (a delegate's by its controller):
+    // the shards' code arrays have disjoint fields, and their word-wise sum is their union -- one all-reduce
+    // of the code words (22 MB at S=28) instead of packing, gathering and unpacking every survivor's record
+    c.comm->allreduce_sum_u32(c.d_tcode, tcode_words(c.lr), c.stream);
+    c.xcode_n.clear();
+    c.xcode_in_tpub = false;
+    return;
+  }
   ensure_xcnt(c);
   const uint32_t G = c.nshards;
   hipLaunchKernelGGL(k_count_to_u64, dim3(1), dim3(1), 0, c.stream, c.d_nS, c.d_xcnt);
@@ -1002,7 +1051,7 @@ void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t
   auto* cnt = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
   auto* ridx = static_cast<uint32_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint32_t)));
   auto* eoff = static_cast<uint64_t*>(c.arena.get(std::max<uint64_t>(cap, 1) * sizeof(uint64_t)));
-  PM_HIP_CHECK(hipMemsetAsync(counts, 0, 2 * sizeof(uint64_t), c.stream));
+  PM_HIP_CHECK(hipMemsetAsync(counts, 0, 3 * sizeof(uint64_t), c.stream));  // rows, entries, error word
   if (!cap) return;
   hipLaunchKernelGGL(k_pack_count, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap,
                      c.d_tpub[c.cur], c.d_malive, keep, cnt);
@@ -1015,22 +1064,13 @@ void pack_state(Ctx& c, uint32_t* rec, uint32_t* ent, uint64_t ent_cap, uint64_t
   PM_HIP_CHECK(rocprim::exclusive_scan(tmp, t1, keep, ridx, 0u, size_t(cap), rocprim::plus<uint32_t>(), c.stream));
   PM_HIP_CHECK(rocprim::exclusive_scan(tmp, t2, wc, eoff, uint64_t(0), size_t(cap), rocprim::plus<uint64_t>(),
                                        c.stream));
-  // rec == nullptr: totals only (the rows are not written)
-  auto* err = reinterpret_cast<unsigned long long*>(c.d_xcnt + 60);
-  if (rec) PM_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), c.stream));
+  // rec == nullptr: totals only (the rows are not written); counts[2]: a row the pack found inconsistent
+  // (shard_replicate gathers it with the counts: a wrong row would corrupt every replica)
   hipLaunchKernelGGL(k_pack_write, dim3(xgrid(cap)), dim3(kXBlock), 0, c.stream, c.d_slist, c.d_nS, cap, keep,
                      ridx, cnt, eoff, c.d_tpub[c.cur], c.d_tst, c.d_mlen, m_off(c), m_col(c), rec, ent,
-                     rec ? ent_cap : 0, c.n, reinterpret_cast<unsigned long long*>(counts), err);
+                     rec ? ent_cap : 0, c.n, reinterpret_cast<unsigned long long*>(counts),
+                     reinterpret_cast<unsigned long long*>(counts + 2));
   PM_HIP_CHECK(hipGetLastError());
-  if (rec && c.comm) {  // (a wrong row would corrupt every replica: checked before it is sent)
-    unsigned long long e = 0;
-    PM_HIP_CHECK(hipMemcpyAsync(&e, err, sizeof(e), hipMemcpyDeviceToHost, c.stream));
-    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-    if (e)
-      throw std::runtime_error(std::string("internal: state row of position ") + std::to_string(e & 0x3FFFFFFFull) +
-                               ((e >> 63) ? " holds a non-position entry" : " has |M| != its alive entries") +
-                               " (shard " + std::to_string(c.shard) + (c.replicated ? ", replica)" : ")"));
-  }
 }
 
 void shard_replicate(Ctx& c) {
@@ -1048,13 +1088,23 @@ void shard_replicate(Ctx& c) {
   }
   c.xcode_n.clear();
   debug_point(c, "replica: code clear");
-  // this shard's rows of S: counts first, then one gather of every shard's counts (one host sync)
-  pack_state(c, nullptr, nullptr, 0, c.d_xcnt);
-  const std::vector<uint64_t> cn = gather_counts(c, 2);
+  // this shard's rows of S, packed once into the send buffers as they stand (grown to the largest shard's
+  // block by the previous search), and one gather of every shard's counts and pack error word (one host
+  // sync); a shard whose buffers are smaller than the largest block -- the all-gathers read that much from
+  // every shard -- grows them and packs again
+  auto* rsend = grow<uint32_t>(c.d_xsend, c.xsend_cap, std::max<uint64_t>(c.nS_host, 1) * 16);
+  auto* esend = grow<uint32_t>(c.d_xent_send, c.xent_send_cap, std::max<size_t>(c.xent_send_cap, size_t(1) << 18));
+  pack_state(c, rsend, esend, c.xent_send_cap / 4, c.d_xcnt);
+  const std::vector<uint64_t> cn = gather_counts(c, 3);
+  for (uint32_t g = 0; g < G; ++g)
+    if (const uint64_t e = cn[3 * g + 2])
+      throw std::runtime_error("internal: state row of position " + std::to_string(e & 0x3FFFFFFFull) + " on shard " +
+                               std::to_string(g) + ((e >> 63) ? " holds a non-position entry" :
+                                                                " has |M| != its alive entries"));
   uint64_t maxR = 1, maxE = 1, rows = 0, ents = 0;
   for (uint32_t g = 0; g < G; ++g) {
-    x.n[g] = cn[2 * g];
-    x.m[g] = cn[2 * g + 1];
+    x.n[g] = cn[3 * g];
+    x.m[g] = cn[3 * g + 1];
     x.base[g] = rows;
     x.ebase[g] = ents;
     rows += x.n[g];
@@ -1065,9 +1115,11 @@ void shard_replicate(Ctx& c) {
   if (x.m[c.shard] >= (1ull << 32)) throw std::runtime_error("replica: more than 2^32 M entries on one shard");
   if (rows > c.n) throw std::runtime_error("internal: replica larger than the vertex set");
   // every shard's send block is read up to the largest count
-  auto* rsend = grow<uint32_t>(c.d_xsend, c.xsend_cap, maxR * 16);
-  auto* esend = grow<uint32_t>(c.d_xent_send, c.xent_send_cap, maxE * 4);
-  pack_state(c, rsend, esend, maxE, c.d_xcnt + 2);
+  if (c.xsend_cap < maxR * 16 || c.xent_send_cap < maxE * 4) {
+    rsend = grow<uint32_t>(c.d_xsend, c.xsend_cap, maxR * 16);
+    esend = grow<uint32_t>(c.d_xent_send, c.xent_send_cap, maxE * 4);
+    pack_state(c, rsend, esend, c.xent_send_cap / 4, c.d_xcnt);
+  }
   auto* rrecv = grow<uint32_t>(c.d_xrecv, c.xrecv_cap, uint64_t(G) * maxR * 16);
   auto* erecv = grow<uint32_t>(c.d_xent_recv, c.xent_recv_cap, uint64_t(G) * maxE * 4);
   c.comm->allgather(rsend, rrecv, maxR * 16, c.stream);
