@@ -145,6 +145,8 @@ SIGNATURES = [
                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_u32), ctypes.POINTER(c_u64)]),
     ("pm_pattern_summary", ctypes.c_int, [c_char_p, c_char_p, c_u64]),
     ("pm_debug_time_lcc_first", ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
+    ("pm_debug_gather_floor", ctypes.c_int,
+     [c_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint64)]),
     ("pm_debug_layout_stats", ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64]),
     ("pm_debug_tpub_census", ctypes.c_int, [c_vp, ctypes.c_int, c_vp]),
     ("pm_write_rmat_text", ctypes.c_int, [c_u64, c_u64, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(c_u64)]),

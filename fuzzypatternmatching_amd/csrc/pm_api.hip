@@ -26,6 +26,7 @@
 #include "../../include/pm_abi.h"
 #include "host/graph_store.hpp"
 #include "host/mt_jump.hpp"
+#include "pm_device.hpp"
 #include "pm_internal.hpp"
 #include "pm_ingest.hpp"
 #include "pm_rmat.hpp"
@@ -1982,19 +1983,20 @@ int pm_write_label_text(const uint64_t* labels, uint64_t n, const char* prefix, 
 }
 
 // Diagnostics: times `reps` launches of the superstep-0 kernel on the current
-// labels (state is reset first).  variant < 65536: diagnostic MODE of the
-// kernel on the default grid (dense M whenever light tiles run, as in the
-// product); variant >= 65536: the product kernel on a grid of variant - 65536
-// blocks.
+// labels (state is reset first).  variant & 0xFFFF: the kernel variant (0 the
+// product; diagnostic MODEs and register / pairing variants in libpm_diag.so),
+// dense M whenever light tiles run, as in the product; variant >> 16: the grid
+// in blocks (0: the product grid).
 int pm_debug_time_lcc_first(pm_ctx* ctx, int variant, int reps, float* ms_out) {
   PM_API_BODY(ctx, {
     pm::reset_state(*ctx);
     hipEvent_t a, b;
     PM_HIP_CHECK(hipEventCreate(&a));
     PM_HIP_CHECK(hipEventCreate(&b));
-    const unsigned grid = variant >= 65536 ? std::min<unsigned>(static_cast<unsigned>(variant - 65536), pm::kPartGridMax)
-                                           : ctx->k1_grid;
-    const int mode = variant >= 65536 ? 0 : variant;
+    // variant = kernel variant | grid << 16 (grid 0: the product grid)
+    const unsigned grid = (variant >> 16) ? std::min<unsigned>(static_cast<unsigned>(variant >> 16), pm::kPartGridMax)
+                                          : ctx->k1_grid;
+    const int mode = variant & 0xFFFF;
     const bool dense = !(mode & 2);
     pm::ensure_counts(*ctx, 1);
     pm::lcc_first_prepare(*ctx);
@@ -2116,3 +2118,311 @@ int pm_pattern_summary(const char* pattern_dir, char* buf, uint64_t buflen) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------------
+// Diagnostics: the floor of the first later superstep's neighbour-T_pub gathers.  The gathers
+// of the S=28 first later superstep: one 2-bit code per alive M entry of the superstep-0 survivors, read from the
+// code array (tcode, ~22 MB) at the entry's code index.  pm_debug_gather_floor runs superstep 0 (product kernel,
+// dense M + records), collects the light survivors' M entries as code indices in record order (the order the
+// superstep reads them), and times gather-only kernels over them:
+//   0  record order: the entry's index read (coalesced) + its code word gathered, 4 entries in flight per lane
+//   1  the index stream alone (no gather)
+//   2  XCD-sliced: entries bucketed (untimed) into eight code ranges of an eighth of the entries each; workgroup b
+//      takes bucket b % 8 (workgroups are dealt to the 8 XCDs round-robin), so each XCD's gathers stay inside its
+//      own range of the code array
+//   3  the same buckets, each spread over every XCD (bucket (b / 8) % 8): the XCD placement alone
+//   4  the same number of gathers, uniformly random over the code array (index hashed, no index stream)
+//   5  the entries sorted by code index (every line fetched once, in order)
+//   6  calibration: one 4-B load from each of n distinct 128-B lines of a 4 GiB buffer (every load a miss beyond
+//      the Infinity Cache), for FETCH_SIZE per narrow gather
+//   7  a bucketing pass (the preparation a sliced gather needs on the device; eight equal code ranges): per
+//      workgroup LDS counts, one reservation per bucket and workgroup, every entry written to its bucket
+// info[0] entries (heavy rows' entries, read from their padded rows by the superstep, are not collected),
+// [1] checksum of the gathered codes (equal for 0, 2, 3, 5), [2] code array bytes.
+namespace pm {
+template <int V>
+__global__ __launch_bounds__(256) void k_gather_floor(const uint32_t* __restrict__ idx, uint64_t n,
+                                                      const uint32_t* __restrict__ tab, uint64_t ncode,
+                                                      const uint64_t* __restrict__ boff,
+                                                      unsigned long long* __restrict__ sink,
+                                                      uint32_t* __restrict__ bout, unsigned int* __restrict__ bcnt) {
+  uint64_t lo = 0, hi = n, start, stride;
+  if (V == 2 || V == 3) {
+    // 2: bucket b % 8 on XCD b % 8 (member b / 8); 3: bucket (b / 8) % 8, its members on every XCD
+    const uint32_t b = V == 2 ? (blockIdx.x & 7u) : ((blockIdx.x >> 3) & 7u);
+    const uint32_t mem = V == 2 ? (blockIdx.x >> 3) : ((blockIdx.x & 7u) | ((blockIdx.x >> 6) << 3));
+    lo = boff[b];
+    hi = boff[b + 1];
+    start = lo + (uint64_t(mem) * blockDim.x + threadIdx.x);
+    stride = uint64_t(gridDim.x >> 3) * blockDim.x;
+  } else {
+    start = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    stride = uint64_t(gridDim.x) * blockDim.x;
+  }
+  uint64_t acc = 0;
+  for (uint64_t i0 = start; i0 < hi; i0 += 4 * stride) {
+    uint32_t ci[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t i = i0 + q * stride;
+      ok[q] = i < hi;
+      if (V == 4) ci[q] = ok[q] ? static_cast<uint32_t>((i * 0x9E3779B97F4A7C15ull >> 29) % ncode) : 0u;
+      else if (V == 6) ci[q] = ok[q] ? static_cast<uint32_t>(((i * 2654435761ull) & (ncode - 1)) << 5) : 0u;
+      else ci[q] = ok[q] ? idx[i] : 0u;
+    }
+    if (V == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc += ci[q];
+    } else if (V == 7) {
+      // (the bucketing pass is k_bucket_floor)
+    } else if (V == 6) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = ok[q] ? tab[ci[q]] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc += w[q];
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = ok[q] ? tab[ci[q] >> 4] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc += (w[q] >> ((ci[q] & 15u) << 1)) & 3u;
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane_id() == 0) atomicAdd(sink, static_cast<unsigned long long>(acc));
+}
+
+// the light survivors' alive M entries as code indices, in record order: pass 0 counts per wave slice, pass 1
+// writes at the slice's offset (one thread per superstep-0 wave slice)
+template <int PASS>
+__global__ __launch_bounds__(256) void k_collect_entries(const uint4* __restrict__ rarea,
+                                                         const uint64_t* __restrict__ rbase,
+                                                         const uint32_t* __restrict__ rcnt, uint32_t nw,
+                                                         const uint32_t* __restrict__ mcol, uint64_t dbase,
+                                                         LabelRuns lr, uint64_t* __restrict__ cnt,
+                                                         uint32_t* __restrict__ out) {
+  const uint32_t gw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gw >= nw) return;
+  uint64_t k = PASS ? cnt[gw] : 0;
+  for (uint32_t r = 0; r < rcnt[gw]; ++r) {
+    const uint4 rec = rarea[rbase[gw] + r];
+    if (rec.z == kNone) continue;
+    const uint32_t len = (rec.y >> 16) & 0x1FFu;
+    for (uint32_t j = 0; j < len; ++j) {
+      const uint32_t m = mcol[dbase + rec.z + j];
+      if (!(m & kAlive)) continue;
+      const uint32_t p = m & kPosMask;
+      uint32_t ci = kNone;
+      for (int l = 0; l < lr.n; ++l)
+        if (p - lr.lo[l] < lr.len[l]) ci = p + lr.cd[l];
+      if (ci == kNone) continue;
+      if (PASS) out[k] = ci;
+      ++k;
+    }
+  }
+  if (!PASS) cnt[gw] = k;
+}
+
+// a bucketing pass (variant 7): each workgroup takes a contiguous range of the index stream, counts its entries
+// per bucket in LDS, reserves its bucket ranges with one global atomic per bucket, then re-reads the range and
+// writes every entry to its bucket (two reads and one write of the stream)
+__global__ __launch_bounds__(256) void k_bucket_floor(const uint32_t* __restrict__ idx, uint64_t n, uint64_t ncode,
+                                                      const uint64_t* __restrict__ boff, uint32_t* __restrict__ bout,
+                                                      unsigned int* __restrict__ bcnt) {
+  __shared__ unsigned int s_cnt[8], s_at[8];
+  if (threadIdx.x < 8) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = min<uint64_t>(n, uint64_t(blockIdx.x) * per), hi = min<uint64_t>(n, lo + per);
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+    atomicAdd(&s_cnt[(uint64_t(idx[i]) * 8) / ncode], 1u);
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    s_at[threadIdx.x] = atomicAdd(&bcnt[threadIdx.x], s_cnt[threadIdx.x]);
+    s_cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t ci = idx[i];
+    const uint32_t b = static_cast<uint32_t>((uint64_t(ci) * 8) / ncode);
+    const unsigned k = atomicAdd(&s_cnt[b], 1u);
+    const uint64_t at = boff[b] + s_at[b] + k;
+    if (at < boff[b + 1]) bout[at] = ci;
+  }
+}
+
+struct GfArgs {
+  const uint32_t* idx;
+  uint64_t n;
+  const uint32_t* tab;
+  uint64_t ncode;
+  const uint64_t* boff;
+  unsigned long long* sink;
+  uint32_t* bout;
+  unsigned int* bcnt;
+};
+template <int V>
+static void launch_gather_floor(const GfArgs& g, unsigned grid, hipStream_t s) {
+  if (V == 7) {
+    hipLaunchKernelGGL(k_bucket_floor, dim3(grid), dim3(256), 0, s, g.idx, g.n, g.ncode, g.boff, g.bout, g.bcnt);
+    return;
+  }
+  hipLaunchKernelGGL(k_gather_floor<V>, dim3(grid), dim3(256), 0, s, g.idx, g.n, g.tab, g.ncode, g.boff, g.sink,
+                     g.bout, g.bcnt);
+}
+
+struct GatherFloor {
+  const void* owner = nullptr;
+  uint64_t n = 0;
+  uint32_t *d_idx = nullptr, *d_bkt = nullptr, *d_sorted = nullptr, *d_big = nullptr, *d_bout = nullptr;
+  uint64_t* d_boff = nullptr;
+  unsigned long long* d_sink = nullptr;
+  unsigned int* d_bcnt = nullptr;
+  void release() {
+    for (void* p : {static_cast<void*>(d_idx), static_cast<void*>(d_bkt), static_cast<void*>(d_sorted),
+                    static_cast<void*>(d_big), static_cast<void*>(d_bout), static_cast<void*>(d_boff),
+                    static_cast<void*>(d_sink), static_cast<void*>(d_bcnt)})
+      if (p) (void)hipFree(p);
+    *this = GatherFloor{};
+  }
+};
+static GatherFloor g_gather;
+
+static void gather_floor_build(Ctx& c) {
+  g_gather.release();
+  reset_state(c);
+  ensure_counts(c, 1);
+  lcc_first_prepare(c);
+  lcc_first_set_dense(c);
+  if (!c.k1_dense || !c.d_rarea) throw std::runtime_error("gather floor: superstep 0 writes no dense M records here");
+  launch_lcc_first_kernel(c, 0, c.k1_grid, c.d_counts);
+  const uint32_t nw = c.rwaves;
+  uint64_t* d_cnt = dalloc<uint64_t>(nw + 1);
+  const unsigned g = (nw + 255) / 256;
+  hipLaunchKernelGGL(k_collect_entries<0>, dim3(g), dim3(256), 0, c.stream, c.d_rarea, c.d_rbase, c.d_rcnt, nw,
+                     c.d_mcol, c.dbase, c.lr, d_cnt, nullptr);
+  std::vector<uint64_t> cnt(nw);
+  PM_HIP_CHECK(hipMemcpyAsync(cnt.data(), d_cnt, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  uint64_t n = 0;
+  for (auto& x : cnt) {
+    const uint64_t v = x;
+    x = n;
+    n += v;
+  }
+  PM_HIP_CHECK(hipMemcpy(d_cnt, cnt.data(), nw * sizeof(uint64_t), hipMemcpyHostToDevice));
+  g_gather.d_idx = dalloc<uint32_t>(n + 1);
+  hipLaunchKernelGGL(k_collect_entries<1>, dim3(g), dim3(256), 0, c.stream, c.d_rarea, c.d_rbase, c.d_rcnt, nw,
+                     c.d_mcol, c.dbase, c.lr, d_cnt, g_gather.d_idx);
+  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  (void)hipFree(d_cnt);
+  std::vector<uint32_t> idx(n);
+  PM_HIP_CHECK(hipMemcpy(idx.data(), g_gather.d_idx, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  // buckets: eight code ranges holding an eighth of the entries each (the R-MAT skew puts most entries on low
+  // positions), entries in record order inside a bucket; and a fully sorted copy
+  std::vector<uint32_t> sorted(idx);
+  std::sort(sorted.begin(), sorted.end());
+  uint32_t cut[8];
+  for (int b = 0; b < 8; ++b) cut[b] = n ? sorted[std::min<uint64_t>(n - 1, (uint64_t(b) + 1) * n / 8)] : 0u;
+  cut[7] = kNone;
+  auto bucket = [&](uint32_t ci) {
+    int b = 0;
+    while (b < 7 && ci >= cut[b]) ++b;
+    return b;
+  };
+  std::vector<uint64_t> roff(9, 0);  // (variant 7: eight equal code ranges)
+  for (uint32_t ci : idx) ++roff[(uint64_t(ci) * 8) / c.lr.ncode + 1];
+  for (int b = 0; b < 8; ++b) roff[b + 1] += roff[b];
+  std::vector<uint64_t> boff(9, 0);
+  for (uint32_t ci : idx) ++boff[bucket(ci) + 1];
+  for (int b = 0; b < 8; ++b) boff[b + 1] += boff[b];
+  std::vector<uint32_t> bkt(n);
+  {
+    std::vector<uint64_t> at(boff.begin(), boff.end() - 1);
+    for (uint32_t ci : idx) bkt[at[bucket(ci)]++] = ci;
+  }
+  idx.swap(sorted);
+  g_gather.d_bkt = dalloc<uint32_t>(n + 1);
+  g_gather.d_sorted = dalloc<uint32_t>(n + 1);
+  g_gather.d_bout = dalloc<uint32_t>(n + 1);
+  g_gather.d_boff = dalloc<uint64_t>(18);
+  g_gather.d_sink = dalloc<unsigned long long>(1);
+  g_gather.d_bcnt = dalloc<unsigned int>(8);
+  PM_HIP_CHECK(hipMemcpy(g_gather.d_bkt, bkt.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMemcpy(g_gather.d_sorted, idx.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMemcpy(g_gather.d_boff, boff.data(), 9 * sizeof(uint64_t), hipMemcpyHostToDevice));
+  PM_HIP_CHECK(hipMemcpy(g_gather.d_boff + 9, roff.data(), 9 * sizeof(uint64_t), hipMemcpyHostToDevice));
+  // 4 GiB calibration buffer: 2^25 lines of 128 B
+  g_gather.d_big = dalloc<uint32_t>(uint64_t(1) << 30);
+  PM_HIP_CHECK(hipMemset(g_gather.d_big, 1, uint64_t(4) << 30));
+  g_gather.n = n;
+  g_gather.owner = &c;
+  reset_state(c);
+  c.k1_dense = false;
+  c.tpub_clean = false;
+}
+}  // namespace pm
+
+extern "C" int pm_debug_gather_floor(pm_ctx* ctx, int variant, int reps, float* ms_out, uint64_t* info) {
+  PM_API_BODY(ctx, {
+    if (variant < 0 || variant > 7) throw std::runtime_error("gather floor: variant 0..7");
+    if (pm::g_gather.owner != static_cast<const void*>(static_cast<pm::Ctx*>(ctx))) pm::gather_floor_build(*ctx);
+    auto& G = pm::g_gather;
+    // the code array as superstep 0 leaves it (the codes of this launch)
+    pm::reset_state(*ctx);
+    pm::ensure_counts(*ctx, 1);
+    pm::lcc_first_prepare(*ctx);
+    pm::lcc_first_set_dense(*ctx);
+    pm::launch_lcc_first_kernel(*ctx, 0, ctx->k1_grid, ctx->d_counts);
+    const uint64_t ncode = variant == 6 ? (uint64_t(1) << 25) : ctx->lr.ncode;
+    const uint32_t* idx = variant == 5 ? G.d_sorted : (variant == 2 || variant == 3) ? G.d_bkt : G.d_idx;
+    const uint32_t* tab = variant == 6 ? G.d_big : ctx->d_tcode;
+    const unsigned grid = 2048;  // 8 waves per SIMD, a multiple of 8 (the XCD round-robin)
+    auto launch = [&] {
+      pm::GfArgs g{idx, G.n, tab, ncode, variant == 7 ? G.d_boff + 9 : G.d_boff, G.d_sink, G.d_bout, G.d_bcnt};
+      switch (variant) {
+        case 0: pm::launch_gather_floor<0>(g, grid, ctx->stream); break;
+        case 1: pm::launch_gather_floor<1>(g, grid, ctx->stream); break;
+        case 2: pm::launch_gather_floor<2>(g, grid, ctx->stream); break;
+        case 3: pm::launch_gather_floor<3>(g, grid, ctx->stream); break;
+        case 4: pm::launch_gather_floor<4>(g, grid, ctx->stream); break;
+        case 5: pm::launch_gather_floor<5>(g, grid, ctx->stream); break;
+        case 6: pm::launch_gather_floor<6>(g, grid, ctx->stream); break;
+        default: pm::launch_gather_floor<7>(g, grid, ctx->stream); break;
+      }
+    };
+    hipEvent_t a, b;
+    PM_HIP_CHECK(hipEventCreate(&a));
+    PM_HIP_CHECK(hipEventCreate(&b));
+    PM_HIP_CHECK(hipMemsetAsync(G.d_bcnt, 0, 8 * sizeof(unsigned int), ctx->stream));
+    launch();  // warm
+    float total = 0.f;
+    for (int i = 0; i < std::max(reps, 1); ++i) {
+      // the sink reset outside the events
+      PM_HIP_CHECK(hipMemsetAsync(G.d_sink, 0, sizeof(unsigned long long), ctx->stream));
+      if (variant == 7) PM_HIP_CHECK(hipMemsetAsync(G.d_bcnt, 0, 8 * sizeof(unsigned int), ctx->stream));
+      PM_HIP_CHECK(hipEventRecord(a, ctx->stream));
+      launch();
+      PM_HIP_CHECK(hipEventRecord(b, ctx->stream));
+      PM_HIP_CHECK(hipEventSynchronize(b));
+      float ms = 0.f;
+      PM_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+      total += ms;
+    }
+    unsigned long long sum = 0;
+    PM_HIP_CHECK(hipMemcpy(&sum, G.d_sink, sizeof(sum), hipMemcpyDeviceToHost));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (ms_out) *ms_out = total / std::max(1, reps);
+    if (info) {
+      info[0] = G.n;
+      info[1] = sum;
+      info[2] = pm::tcode_words(ctx->lr) * sizeof(uint32_t);
+    }
+    ctx->k1_dense = false;
+    ctx->tpub_clean = false;
+    pm::reset_state(*ctx);
+  });
+}

@@ -251,6 +251,7 @@ struct LineStats {
   unsigned long long census;  // sources the line would select on the state at the launch's start (k_lines)
   unsigned long long census_tok;  // their first-position tokens (sum of |M[s]|): the line's work estimate
   unsigned long long ptime[20];  // s_memrealtime at the end of each position's phase (diagnostics, PM_PHASE_TIMES)
+  unsigned long long pmid[20][3];  // TDS position, thread 0: its first walks' state loaded, its expansion done, its wave's entries
 };
 
 // One NLC line as seen by the fused line kernel (pm_lines.hip).

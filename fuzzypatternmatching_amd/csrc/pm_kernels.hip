@@ -831,7 +831,9 @@ __device__ __forceinline__ BlockAcc k1_heavy_tile(KTab kt, uint32_t hi,
 // and the label test (checksum), bit4 stops light tiles after phase A, bit5
 // after phase B1.  WIDE: some range has more than four
 // relevant label runs (tbits_rel scans them all).
-template <int MODE, bool WIDE = false, int WMIN = 8>
+// NT > 1: NT tiles per wait -- the slots of the next NT tiles in flight while the current NT are processed (NT
+// times the bytes in flight per wave, 1/NT of the waits; more registers, fewer waves).
+template <int MODE, bool WIDE = false, int WMIN = 8, int NT = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8))) void k_lcc_first(
     const KRange* __restrict__ ktab, const uint64_t* __restrict__ ttab, uint32_t ntiles, const HSeg* __restrict__ hseg,
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ colp, LabelRuns lr, PatArgs pa, OwnerArgs oa,
@@ -862,34 +864,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
   const int nruns = lr.n;
   const TTab tt = (TTab)ttab;
   const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWpb + wid);
-  // tiles t = (j W + gw) kTileBlock + i; descriptors read one tile ahead of the loads they address, the
-  // slots of the next tile in flight while the current one is processed
-  uint32_t t = gw * kTileBlock;
-  uint32_t tn = k1_next(t, W);
-  uint64_t wcur = t < ntiles ? tt[t] : 0ull, wnx = tn < ntiles ? tt[tn] : 0ull;
-  uint32_t vc[kSub], vn[kSub];
-  const uint32_t voff = 16u * static_cast<uint32_t>(lane_id());  // byte offset of the lane's 16 B in a load
-  uint32_t sc = k1_load(vc, wcur, colp, voff);
-  // dense M: this wave's slice of the region
-  uint64_t dcur = uniform64(uint64_t(gw) * o.dslice);
-  const uint64_t dend = uniform64(dcur + o.dslice);
-  // dense mode: this wave's record slice
-  uint64_t rcur = o.rarea ? uniform64(o.rbase[gw]) : 0;
-  while (t < ntiles) {
-    t = __builtin_amdgcn_readfirstlane(t);
-    tn = __builtin_amdgcn_readfirstlane(tn);
-    wcur = uniform64(wcur);
-    wnx = uniform64(wnx);
-    // this tile's slots (requested a whole tile ago) and the previous tile's stores are complete here,
-    // ahead of the next tile's loads: the vector memory counter retires in issue order, so a wait at
-    // the first use would also wait for the stores this tile issues
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    dcur = uniform64(dcur);
-    rcur = uniform64(rcur);
-    const uint32_t sn = k1_load(vn, wnx, colp, voff);
-    const uint32_t tnn = k1_next(tn, W);
-    const uint64_t wnn = tnn < ntiles ? tt[tnn] : 0ull;
-    sc = __builtin_amdgcn_readfirstlane(sc);
+  // one light tile (w: its descriptor, v: its slots, s: their alignment shift); a heavy tile or a tile past the
+  // end (w = 0) does nothing here
+  auto light2 = [&](uint32_t t, uint64_t wcur, const uint32_t (&vc)[kSub], uint32_t sc, uint64_t& dcur,
+                    uint64_t dend, uint64_t& rcur) {
     const uint32_t rem = ttab_rem(wcur);
     if (rem) {  // a light tile (heavy tiles: the loop below)
       const KTab R = kt + ttab_range(wcur);
@@ -909,16 +887,126 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WMIN, 8)
                                   st, o, dcur, dend, rcur, ustart + R->cdelta);
       }
     }
-    t = tn;
-    tn = tnn;
-    wcur = wnx;
-    wnx = wnn;
-    sc = sn;
+  };
+  if constexpr (NT > 1) {
+    // NT tiles per wait: the slots of the next NT tiles in flight while the current NT are processed
+    uint32_t tc[NT], tx[NT], sc[NT], sx[NT];
+    uint64_t wc[NT], wx[NT];
+    uint32_t vc[NT][kSub], vx[NT][kSub];
+    const uint32_t voff = 16u * static_cast<uint32_t>(lane_id());
+    tc[0] = gw * kTileBlock;
 #pragma unroll
-    for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
+    for (int i = 1; i < NT; ++i) tc[i] = k1_next(tc[i - 1], W);
+    tx[0] = k1_next(tc[NT - 1], W);
+#pragma unroll
+    for (int i = 1; i < NT; ++i) tx[i] = k1_next(tx[i - 1], W);
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      wc[i] = tc[i] < ntiles ? tt[tc[i]] : 0ull;
+      wx[i] = tx[i] < ntiles ? tt[tx[i]] : 0ull;
+      sc[i] = k1_load(vc[i], wc[i], colp, voff);
+    }
+    uint64_t dcur = uniform64(uint64_t(gw) * o.dslice);
+    const uint64_t dend = uniform64(dcur + o.dslice);
+    uint64_t rcur = o.rarea ? uniform64(o.rbase[gw]) : 0;
+    while (tc[0] < ntiles) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        tc[i] = __builtin_amdgcn_readfirstlane(tc[i]);
+        tx[i] = __builtin_amdgcn_readfirstlane(tx[i]);
+        wc[i] = uniform64(wc[i]);
+        wx[i] = uniform64(wx[i]);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the current tiles' slots (and the last group's stores)
+      dcur = uniform64(dcur);
+      rcur = uniform64(rcur);
+      uint32_t ty[NT];
+      uint64_t wy[NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) sx[i] = k1_load(vx[i], wx[i], colp, voff);
+      ty[0] = k1_next(tx[NT - 1], W);
+#pragma unroll
+      for (int i = 1; i < NT; ++i) ty[i] = k1_next(ty[i - 1], W);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) wy[i] = ty[i] < ntiles ? tt[ty[i]] : 0ull;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        sc[i] = __builtin_amdgcn_readfirstlane(sc[i]);
+        light2(tc[i], wc[i], vc[i], sc[i], dcur, dend, rcur);
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        tc[i] = tx[i];
+        tx[i] = ty[i];
+        wc[i] = wx[i];
+        wx[i] = wy[i];
+        sc[i] = sx[i];
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) vc[i][q] = vx[i][q];
+      }
+    }
+    rcur = uniform64(rcur);
+    if (o.rarea && lane_id() == 0) o.rcnt[gw] = static_cast<uint32_t>(rcur - o.rbase[gw]);
+  } else {
+    // tiles t = (j W + gw) kTileBlock + i; descriptors read one tile ahead of the loads they address, the
+    // slots of the next tile in flight while the current one is processed
+    uint32_t t = gw * kTileBlock;
+    uint32_t tn = k1_next(t, W);
+    uint64_t wcur = t < ntiles ? tt[t] : 0ull, wnx = tn < ntiles ? tt[tn] : 0ull;
+    uint32_t vc[kSub], vn[kSub];
+    const uint32_t voff = 16u * static_cast<uint32_t>(lane_id());  // byte offset of the lane's 16 B in a load
+    uint32_t sc = k1_load(vc, wcur, colp, voff);
+    // dense M: this wave's slice of the region
+    uint64_t dcur = uniform64(uint64_t(gw) * o.dslice);
+    const uint64_t dend = uniform64(dcur + o.dslice);
+    // dense mode: this wave's record slice
+    uint64_t rcur = o.rarea ? uniform64(o.rbase[gw]) : 0;
+    while (t < ntiles) {
+      t = __builtin_amdgcn_readfirstlane(t);
+      tn = __builtin_amdgcn_readfirstlane(tn);
+      wcur = uniform64(wcur);
+      wnx = uniform64(wnx);
+      // this tile's slots (requested a whole tile ago) and the previous tile's stores are complete here,
+      // ahead of the next tile's loads: the vector memory counter retires in issue order, so a wait at
+      // the first use would also wait for the stores this tile issues
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      dcur = uniform64(dcur);
+      rcur = uniform64(rcur);
+      const uint32_t sn = k1_load(vn, wnx, colp, voff);
+      const uint32_t tnn = k1_next(tn, W);
+      const uint64_t wnn = tnn < ntiles ? tt[tnn] : 0ull;
+      sc = __builtin_amdgcn_readfirstlane(sc);
+      // (the body of light2, written out: the lambda costs this loop ~6 % through its register allocation)
+      const uint32_t rem = ttab_rem(wcur);
+      if (rem) {  // a light tile (heavy tiles: the loop below)
+        const KTab R = kt + ttab_range(wcur);
+        const uint16_t tu = R->tu;
+        const uint16_t nm = R->nm;
+        const RelRuns rel_runs = load_rel(R);
+        if (MODE & 8) {
+#pragma unroll
+          for (int q = 0; q < kSub; ++q) acc.vs += vc[q] ^ tbits_rel<WIDE>(vc[q], rel_runs, s_runs, nruns);
+        } else if (!(MODE & 2)) {
+          const KeepArgs keep = load_keep(R);
+          const uint32_t rpt = R->rpt;
+          const uint32_t ustart = R->start + (t - R->tile0) * rpt;
+          const uint32_t rows = min(rpt, R->end - ustart);
+          k1_light_tile<MODE, WIDE>(vc, sc, ttab_slot(wcur), rem, ustart, rows, R->g, rpt, R->rdiv, R, tu, nm,
+                                    rel_runs, s_runs, nruns, keep, s_adj, oa, acc, s_hist, tmask + uint64_t(t) * kSub,
+                                    t, st, o, dcur, dend, rcur, ustart + R->cdelta);
+        }
+      }
+      t = tn;
+      tn = tnn;
+      wcur = wnx;
+      wnx = wnn;
+      sc = sn;
+#pragma unroll
+      for (int q = 0; q < kSub; ++q) vc[q] = vn[q];
+    }
+    rcur = uniform64(rcur);
+    if (o.rarea && lane_id() == 0) o.rcnt[gw] = static_cast<uint32_t>(rcur - o.rbase[gw]);
   }
-  rcur = uniform64(rcur);
-  if (o.rarea && lane_id() == 0) o.rcnt[gw] = static_cast<uint32_t>(rcur - o.rbase[gw]);
   // heavy rows, one segment per wave at a time (a separate loop: no slot
   // buffers live, so the light loop's register budget is its own)
   if (!(MODE & 4))
@@ -977,13 +1065,14 @@ __global__ void k_slist_write(const uint32_t* __restrict__ tcnt, const uint32_t*
 // through the live mask of the previous superstep.
 static constexpr uint32_t kLprMax = 32;
 
+// (store = false: timing variant PM_DIAG_STEP & 4)
 __device__ __forceinline__ void k2_entry(uint32_t* __restrict__ mcol, uint64_t e, uint32_t m, uint16_t tv,
-                                         uint16_t nm, uint32_t& tn, uint32_t& cnt, bool& asym) {
+                                         uint16_t nm, uint32_t& tn, uint32_t& cnt, bool& asym, bool store = true) {
   const bool ok = (tv & nm) != 0;
   const bool fl = (m & kFlag) != 0;
   const bool flag = ok || fl;
   const uint32_t m2 = (m & kPosMask) | (flag ? kAlive : 0u);  // flags cleared by verify
-  if (m2 != m) mcol[e] = m2;
+  if (store && m2 != m) mcol[e] = m2;
   if (fl && !ok && tv) asym = true;
   if (ok) tn |= tv;
   cnt += flag ? 1u : 0u;
@@ -1012,7 +1101,7 @@ struct RecSrc {
   uint32_t W;
 };
 #ifndef PM_STEP_UNROLL
-#define PM_STEP_UNROLL 4  // entries in flight per lane in k_lcc_step's flattened rows
+#define PM_STEP_UNROLL 3  // entries in flight per lane in k_lcc_step's flattened rows (4 spills registers at 6 waves)
 #endif
 static constexpr int kStepUnroll = PM_STEP_UNROLL;
 #ifndef PM_STEP_WAVES
@@ -1178,7 +1267,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
         for (int q = 0; q < kStepUnroll; ++q)
           if (m[q] & kAlive) {
             uint32_t tq = 0, cq = 0;
-            k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym);
+            k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym, !(diag & 4));
             if (tq) atomicOr(&s_tn[w][rr[q]], tq);
             if (cq) atomicAdd(&s_cnt[w][rr[q]], cq);
           }
@@ -1210,7 +1299,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
         for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tpub_of(m[q] & kPosMask) : uint16_t(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (m[q] & kAlive) k2_entry(mcol, br + j0 + q * kWave + lane, m[q], tv[q], nmr, tnr, cntr, asym);
+          if (m[q] & kAlive) k2_entry(mcol, br + j0 + q * kWave + lane, m[q], tv[q], nmr, tnr, cntr, asym, !(diag & 4));
       }
       tnr = wave_or32(tnr);
       cntr = static_cast<uint32_t>(wave_sum(cntr));
@@ -1262,6 +1351,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
     // the dense survivors' rows, concatenated over the wave: every lane moves every 64th entry, four in flight
     // (a row per lane would wait out one load per entry)
     {
+      if (diag & 2) mv = 0;  // (timing variant: no row moves)
       const uint32_t incl2 = static_cast<uint32_t>(wave_incl_scan(mv));
       const uint32_t total2 = static_cast<uint32_t>(__shfl(incl2, kWave - 1, kWave));
       if (total2) {
@@ -2180,6 +2270,14 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
     case 4096: hipLaunchKernelGGL(k_lcc_first<4096>, PM_K1_ARGS); break;
     case 7168: hipLaunchKernelGGL(k_lcc_first<7168>, PM_K1_ARGS); break;
     case 5: hipLaunchKernelGGL((k_lcc_first<0, false, 5>), PM_K1_ARGS); break;  // 5 waves/SIMD, no spills
+    // (variant numbers keep bit 1 clear: the timing harness reads it as "no dense M")
+    case 13: hipLaunchKernelGGL((k_lcc_first<0, false, 6>), PM_K1_ARGS); break;      // 6 waves/SIMD
+    case 17: hipLaunchKernelGGL((k_lcc_first<0, false, 8, 2>), PM_K1_ARGS); break;   // 2 tiles per wait
+    case 21: hipLaunchKernelGGL((k_lcc_first<0, false, 6, 2>), PM_K1_ARGS); break;
+    case 25: hipLaunchKernelGGL((k_lcc_first<0, false, 7, 2>), PM_K1_ARGS); break;
+    case 29: hipLaunchKernelGGL((k_lcc_first<0, false, 5, 3>), PM_K1_ARGS); break;   // 3 tiles per wait
+    case 33: hipLaunchKernelGGL((k_lcc_first<0, false, 4, 3>), PM_K1_ARGS); break;
+    case 37: hipLaunchKernelGGL((k_lcc_first<0, false, 4, 4>), PM_K1_ARGS); break;   // 4 tiles per wait
 #endif
     default: throw std::runtime_error("unknown superstep-0 kernel variant (ablation variants: lib/libpm_diag.so)");
   }
@@ -2195,7 +2293,9 @@ unsigned lcc_first_grid(const Ctx& c) {
                                                            0));
   hipDeviceProp_t prop;
   PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
-  const uint64_t cap = std::min<uint64_t>(kPartGridMax, uint64_t(std::max(per_cu, 1)) * prop.multiProcessorCount);
+  uint64_t cap = std::min<uint64_t>(kPartGridMax, uint64_t(std::max(per_cu, 1)) * prop.multiProcessorCount);
+  // (diagnostics: PM_K1_GRID sets the persistent grid -- the record slices follow it)
+  if (const char* e = std::getenv("PM_K1_GRID")) cap = std::clamp<uint64_t>(std::strtoull(e, nullptr, 10), 1, kPartGridMax);
   return grid_for(c.ntiles, kWpb, static_cast<unsigned>(cap));
 }
 

@@ -131,6 +131,12 @@ struct LineKernelArgs {
   uint64_t n, mcap;
 };
 
+// The current line's constants, copied into LDS at the line's start by k_lines (read at every entry of the
+// walks: from global memory they were vector loads -- the kernel writes global memory, so they cannot go
+// through the scalar cache -- each a round trip in the walks' dependent chains).
+__shared__ LineArgs s_la;
+static_assert(sizeof(LineArgs) % sizeof(uint32_t) == 0, "LineArgs is copied in words");
+
 // (diagnostics) false when the row (b, L) of vertex u lies outside the M buffer: recorded, not read
 __device__ __forceinline__ bool row_ok(const LineKernelArgs& a, uint32_t u, uint64_t b, uint64_t L) {
   if (!a.dbg) return true;
@@ -207,7 +213,7 @@ __device__ __forceinline__ bool row_has_alive(const LineKernelArgs& a, uint64_t 
 
 // Terminal position C+1 of a path / cycle line (nem_1.hpp:661-791).
 __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u, uint32_t s, uint32_t p) {
-  const LineArgs& la = *a.la;
+  const LineArgs& la = s_la;
   if (!pos_ok(a.tpub[u], la.C + 1, la)) return;
   if (!la.VC) {
     if (u == s) return;
@@ -235,6 +241,8 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
 // long row costs one pass over the wave instead of a serial walk by one lane).
 static constexpr int kLineWaves = 16;  // kLineBlock / kWave
 static constexpr int kStage = 10;      // TDS walks of up to kStage positions are staged in LDS
+static constexpr int kChildBuf = 256;  // TDS children a wave holds in LDS before writing them out
+static constexpr int kTdsUnroll = 2;   // entry groups per round of the TDS expansion (one round in flight ahead)
 struct WaveRows {
   uint64_t beg[kLineWaves][kWave];
   uint32_t end[kLineWaves][kWave];  // inclusive scan of the row lengths
@@ -246,6 +254,9 @@ struct WaveRows {
   };
   unsigned long long wn[20];  // walks per position of a single-block TDS line
   unsigned lpany[20];         // a row of this position went to the piece list (single-block lines: no global read)
+  // TDS expansion: the children a wave found, written out after its rows are walked (tds_expand_wave)
+  uint32_t cnb[kLineWaves][kChildBuf];  // the child's new vertex
+  uint8_t cpar[kLineWaves][kChildBuf];  // its parent walk (the wave's lane)
 };
 
 // Lane owning concatenated entry t (end[] inclusive scan of the wave's rows).
@@ -287,7 +298,8 @@ __device__ __forceinline__ bool line_pieces(const LineKernelArgs& a, int k, uint
 __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows& wr, uint32_t u, uint32_t s,
                                                uint32_t excl, int k, bool active, uint32_t item) {
   uint32_t emitted = 0;
-  const LineArgs& la = *a.la;
+  const LineArgs& la = s_la;
+  k = __builtin_amdgcn_readfirstlane(k);
   const int wv = threadIdx.x / kWave, lane = lane_id();
   uint64_t b = 0;
   uint32_t L = 0;
@@ -373,7 +385,7 @@ __device__ __forceinline__ uint32_t tp_forward(const LineKernelArgs& a, WaveRows
 // slot after): the entries [q kLineLong, (q + 1) kLineLong) of the item's row, one piece per wave and round,
 // with tp_forward's per-entry rule.  Returns the lane's share of the emitted tokens.
 __device__ __forceinline__ uint32_t tp_pieces(const LineKernelArgs& a, const GridIdx& g, int k) {
-  const LineArgs& la = *a.la;
+  const LineArgs& la = s_la;
   const int lane = lane_id();
   uint32_t emitted = 0;
   const uint64_t np = min<uint64_t>(ld_dev(&a.st->lp[k]), a.lp_cap);
@@ -476,8 +488,8 @@ __device__ __forceinline__ bool select_source(const LineKernelArgs& a, uint64_t 
   if (i < nact) {
     s = ld_dev(&a.act[i]);
     const uint16_t T = a.tpub[s];
-    ok = T && pos_ok(T, 0, *a.la);
-    if (ok && !tds && !a.la->VC && !((T >> a.la->ilast) & 1u)) ok = false;
+    ok = T && pos_ok(T, 0, s_la);
+    if (ok && !tds && !s_la.VC && !((T >> s_la.ilast) & 1u)) ok = false;
     if (ok && a.split && owner_of(s, a.so) != a.shard) ok = false;  // a split line: this shard's sources
   }
   const uint64_t pos = wave_reserve(&a.st->nsrc, ok ? 1u : 0u);
@@ -599,7 +611,8 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
                                                 uint64_t i0, int k, uint64_t b, uint32_t L, uint32_t* out,
                                                 uint64_t out_room, int stride, bool stage,
                                                 unsigned long long* ctr) {
-  const LineArgs& la = *a.la;
+  const LineArgs& la = s_la;
+  k = __builtin_amdgcn_readfirstlane(k);
   const int wv = threadIdx.x / kWave, lane = lane_id();
   const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
   const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
@@ -607,12 +620,14 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
   wr.beg[wv][lane] = b;
   wr.end[wv][lane] = incl;
   __builtin_amdgcn_wave_barrier();
-  // kUnroll groups of 64 entries per round (tp_forward); the round's children share one reservation
-  for (uint32_t t0 = 0; t0 < total; t0 += kUnroll * kWave) {
-    uint32_t mm[kUnroll];
-    int rr[kUnroll];
+  // The rows are walked in rounds of kTdsUnroll groups of 64 entries, the next round's entries requested before
+  // the current round is checked; the children go to the wave's LDS buffer and are written out after the
+  // last round (or when the buffer is full).  The only vector memory operations of the rounds are the entry
+  // loads, so a round waits for its own entries only (the memory counter retires loads and stores in issue
+  // order: a child store between two rounds would make the next round's loads wait for it too).
+  auto load_round = [&](uint32_t t0, uint32_t (&mm)[kTdsUnroll], int (&rr)[kTdsUnroll]) {
 #pragma unroll
-    for (int j = 0; j < kUnroll; ++j) {
+    for (int j = 0; j < kTdsUnroll; ++j) {
       const uint32_t t = t0 + j * kWave + lane;
       mm[j] = 0;
       rr[j] = 0;
@@ -623,30 +638,61 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
         mm[j] = a.mcol[wr.beg[wv][r] + (t - first)];
       }
     }
+  };
+  auto walk_of = [&](int r) -> const uint32_t* {
+    return stage ? wr.walk[wv] + r * stride : win + (i0 + r) * stride;
+  };
+  uint32_t nbuf = 0;  // children in the buffer (wave-uniform)
+  auto flush = [&]() {
+    for (uint32_t c0 = 0; c0 < nbuf; c0 += kWave) {
+      const uint32_t c = c0 + lane;
+      const uint64_t pos = wave_reserve(ctr, c < nbuf ? 1u : 0u);
+      if (c < nbuf) {
+        const uint32_t* w = walk_of(wr.cpar[wv][c]);
+        if ((pos + 1) * stride <= out_room) {
+          uint32_t* d = out + pos * stride;
+          for (int p = 0; p <= k; ++p) d[p] = w[p];
+          d[k + 1] = wr.cnb[wv][c];
+        } else {
+          atomicOr(&a.st->overflow, 1u);
+        }
+      }
+    }
+    nbuf = 0;
+    __builtin_amdgcn_wave_barrier();
+  };
+  uint32_t mn[kTdsUnroll];
+  int rn[kTdsUnroll];
+  load_round(0, mn, rn);
+  for (uint32_t t0 = 0; t0 < total; t0 += kTdsUnroll * kWave) {
+    uint32_t mm[kTdsUnroll];
+    int rr[kTdsUnroll];
+#pragma unroll
+    for (int j = 0; j < kTdsUnroll; ++j) {
+      mm[j] = mn[j];
+      rr[j] = rn[j];
+    }
+    if (t0 + kTdsUnroll * kWave < total) load_round(t0 + kTdsUnroll * kWave, mn, rn);
     uint32_t cm = 0;  // children of the round (bit j)
 #pragma unroll
-    for (int j = 0; j < kUnroll; ++j) {
-      const uint32_t* w = stage ? wr.walk[wv] + rr[j] * stride : win + (i0 + rr[j]) * stride;
-      if ((mm[j] & kAlive) && tds_child_ok(w, k, mm[j] & kPosMask, la)) cm |= 1u << j;
-    }
+    for (int j = 0; j < kTdsUnroll; ++j)
+      if ((mm[j] & kAlive) && tds_child_ok(walk_of(rr[j]), k, mm[j] & kPosMask, la)) cm |= 1u << j;
     const uint32_t nc = __popc(cm);
-    const uint64_t pos = wave_reserve(ctr, nc);
-    uint32_t c = 0;
+    const uint32_t cincl = static_cast<uint32_t>(wave_incl_scan(nc));
+    const uint32_t rtotal = static_cast<uint32_t>(__shfl(cincl, kWave - 1, kWave));
+    if (nbuf + rtotal > static_cast<uint32_t>(kChildBuf)) flush();
+    uint32_t c = nbuf + cincl - nc;
 #pragma unroll
-    for (int j = 0; j < kUnroll; ++j) {
+    for (int j = 0; j < kTdsUnroll; ++j) {
       if (!((cm >> j) & 1u)) continue;
-      const uint32_t* w = stage ? wr.walk[wv] + rr[j] * stride : win + (i0 + rr[j]) * stride;
-      if ((pos + c + 1) * stride <= out_room) {
-        uint32_t* d = out + (pos + c) * stride;
-        for (int p = 0; p <= k; ++p) d[p] = w[p];
-        d[k + 1] = mm[j] & kPosMask;
-      } else {
-        atomicOr(&a.st->overflow, 1u);
-      }
+      wr.cnb[wv][c] = mm[j] & kPosMask;
+      wr.cpar[wv][c] = static_cast<uint8_t>(rr[j]);
       ++c;
     }
+    nbuf += rtotal;
+    __builtin_amdgcn_wave_barrier();
   }
-  __builtin_amdgcn_wave_barrier();
+  flush();
 }
 
 // The long-row pieces of position k of a TDS line (items: the source at k = 0, the walk's index in win after):
@@ -655,7 +701,7 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
 // was listed.
 __device__ __forceinline__ void tds_pieces(const LineKernelArgs& a, const GridIdx& g, int k, const uint32_t* win,
                                            uint32_t* out, uint64_t out_room, int stride, unsigned long long* ctr) {
-  const LineArgs& la = *a.la;
+  const LineArgs& la = s_la;
   const int lane = lane_id();
   const uint64_t np = min<uint64_t>(ld_dev(&a.st->lp[k]), a.lp_cap);
   for (uint64_t pi = g.gw; pi < np; pi += g.nw) {
@@ -729,7 +775,8 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
     if (threadIdx.x < 20) wr.lpany[threadIdx.x] = 0u;
     __syncthreads();
   }
-  for (int k = k0; k <= a.la->C; ++k) {
+  for (int k = k0; k <= s_la.C; ++k) {
+    k = __builtin_amdgcn_readfirstlane(k);  // (uniform: the line's constants indexed by k load through the scalar cache)
     if (ld_dev(&st->overflow)) break;  // same value in every wave after the barrier
     const uint64_t hi = ld_dev(&st->ftotal);
     if (single && hi - lo > a.small_line) {  // the frontier outgrew the block: the grid takes position k
@@ -824,7 +871,7 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
                                          unsigned long long* s_hist, WaveRows& wr, uint64_t kept_base,
                                          int k0 = 1, uint64_t in_base0 = 0) {
   LineStats* st = a.st;
-  const LineArgs& la = *a.la;
+  const LineArgs& la = s_la;
   const int stride = la.C + 2;
   uint64_t trav = 0, tokens = 0, in_base = in_base0;
   // single block: the walk counters live in LDS (no global atomic per wave and round)
@@ -838,6 +885,7 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
   }
   const int wv = threadIdx.x / kWave, lane = lane_id();
   for (int k = k0; k <= la.C; ++k) {
+    k = __builtin_amdgcn_readfirstlane(k);  // (uniform: the line's constants indexed by k load through the scalar cache)
     if (ld_dev(&st->overflow)) break;
     const uint64_t nin = single ? wr.wn[k] : ld_dev(&st->wn[k]);
     if (single && nin > a.small_line) {  // the walks outgrew the block: the grid takes position k
@@ -878,6 +926,10 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
         const uint64_t ob = a.offp[u];
         uint32_t ml = a.mlen[u], ma = a.malive[u];
         if (!row_ok(a, u, ob, ml)) ml = 0;
+        if (a.stamps && g.tid == 0 && i0 == g.gw * kWave) {  // (diagnostics: the first walks' state is in)
+          __builtin_amdgcn_s_waitcnt(0);
+          st->pmid[k][0] = __builtin_amdgcn_s_memrealtime() + (T & 0u) + (ml & 0u);
+        }
         if (pos_ok(T, k, la) && enum_ok(w, k, u, la)) {
           b = ob;
           L = ml;
@@ -906,9 +958,14 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
         continue;
       }
       __builtin_amdgcn_wave_barrier();
+      if (a.stamps && g.gw == 0) {  // (diagnostics: entries of thread 0's wave)
+        const uint64_t tw = wave_sum(uint64_t(L));
+        if (lane == 0) st->pmid[k][2] += tw;
+      }
       tds_expand_wave(a, wr, win, i0, k, b, L, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride,
                       stage, ctr);
     }
+    if (a.stamps && g.tid == 0) st->pmid[k][1] = __builtin_amdgcn_s_memrealtime();
     phase_sync(a, single);
     if (single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull) {  // the position's long rows, over every wave
       tds_pieces(a, g, k, win, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride, ctr);
@@ -917,6 +974,8 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
     in_base = out_base;
     if (a.stamps && g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
+  // (diagnostics: a single block's walk counts, kept in LDS, for the phase-time print)
+  if (single && a.stamps && threadIdx.x >= 2 && threadIdx.x < 20) st->wn[threadIdx.x] = wr.wn[threadIdx.x];
   // every final walk may be kept: its room must exist before any terminal effect
   const uint64_t nw = single ? wr.wn[la.C + 1] : ld_dev(&st->wn[la.C + 1]);
   // kept slots used by the launch's earlier lines (read at line start: the
@@ -970,7 +1029,7 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
 __device__ __forceinline__ void tds_line(const LineKernelArgs& a, unsigned long long* s_hist, WaveRows& wr) {
   const GridIdx g = grid_idx();
   LineStats* st = a.st;
-  const int stride = a.la->C + 2;
+  const int stride = s_la.C + 2;
   uint64_t trav = 0;
   // P1 + position 1 walks [s, w]; region 1 starts at slot 0
   const uint64_t kept_base = ld_dev(a.kept_ctr);  // no kept walk of this line exists yet
@@ -1093,6 +1152,10 @@ __global__ __launch_bounds__(kLineBlock) void k_lines(LineKernelArgs a) {
     const bool split = a.split_min && a.so.nranks > 1 && ld_dev(&a.st[pl].census_tok) >= a.split_min;
     if (split && !fresh) break;
     fresh = false;
+    __syncthreads();  // (every wave is done with the previous line's constants)
+    if (threadIdx.x < sizeof(LineArgs) / sizeof(uint32_t))
+      reinterpret_cast<uint32_t*>(&s_la)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&d.la)[threadIdx.x];
+    __syncthreads();
     LineKernelArgs b = a;
     b.la = &d.la;
     b.i0 = d.i0;
@@ -1399,6 +1462,10 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
       for (int k = 1; k < 20 && st.ptime[k]; ++k) {
         char b[96];
         std::snprintf(b, sizeof(b), " %d:(%llu, %.1f, %llu)", k, st.wn[k], (st.ptime[k] - prev) * 0.01, st.lp[k]);
+        if (st.pmid[k][1] > prev)  // TDS: [state of the first walks in, expansion done] after the position start
+          std::snprintf(b + std::strlen(b), sizeof(b) - std::strlen(b), "[%.1f %.1f %llu]",
+                        st.pmid[k][0] > prev ? (st.pmid[k][0] - prev) * 0.01 : 0.0, (st.pmid[k][1] - prev) * 0.01,
+                        st.pmid[k][2]);
         pos += b;
         prev = st.ptime[k];
       }

@@ -45,6 +45,12 @@
  *                                 never leaving HBM (config C5)
  *   pm_vertex_data_files          vertex_data_db(graph, labels, prefix, 10000) (-v) parsed on the GPU:
  *                                 include/havoqgt/vertex_data_db.hpp:137-257
+ *   pm_create_shard_host_comm     pm_create_shard with the exchanges through caller-supplied host
+ *                                 collectives (pm_host_comm): the reference's own MPI transport
+ *                                 (new_mailbox.hpp:358-405, impl/vertex_data.hpp:114-126) or a gloo group
+ *   pm_run_rmat_local_shards2     the N-rank delegate partition of generate_rmat's graph
+ *                                 (delegate_partitioned_graph.ipp:1402-1648, 346-355) run as N shards on
+ *                                 one device, with every shard's statistics (balance / N-GPU projection)
  *
  * Conventions: plain C types; int status (0 = OK, negative = error with
  * pm_last_error()); device memory is owned by the context; host buffers are
@@ -294,6 +300,12 @@ int pm_debug_rccl_selftest(int device, uint64_t bytes, int op);
 /* Diagnostics: HBM copy bandwidth of a 16-B nontemporal copy kernel over two `bytes` buffers (read + write
    bytes per second / 1e9), the measured ceiling beside the datasheet peak. */
 int pm_debug_copy_gbs(int device, uint64_t bytes, int reps, double* gbs);
+/* Diagnostics: the floor of the first later superstep's neighbour-T_pub gathers: superstep 0
+   runs, its light survivors' alive M entries are collected as code indices in record order, and gather-only
+   kernels are timed over them (variant 0 record order, 1 index stream only, 2 XCD-sliced buckets, 3 the buckets
+   spread over every XCD, 4 uniformly random, 5 sorted, 6 distinct-line misses of a 4 GiB buffer (FETCH_SIZE calibration),
+   7 the bucketing pass).  info[0] entries, [1] checksum of the gathered codes, [2] code array bytes. */
+int pm_debug_gather_floor(pm_ctx* ctx, int variant, int reps, float* ms_out, uint64_t* info);
 /* Diagnostics: superstep-0 tiling statistics (real entries, loaded slots, rows, tiles, ranges, heavy rows). */
 int pm_debug_layout_stats(pm_ctx* ctx, uint64_t* out, uint64_t n);
 

@@ -1,9 +1,12 @@
 """Superstep-0 kernel timing: diagnostic variants / grid sizes (one process, interleaved rounds).
 
 usage: ubench.py SCALE [P_GEN] [variant,variant,...]
-  variant < 65536: diagnostic MODE (pm_kernels.hip k_lcc_first: 0 product, 1 no M stores,
+  variant & 0xFFFF: diagnostic MODE (pm_kernels.hip k_lcc_first: 0 product, 1 no M stores,
   8 loads + label test only, 2 skip light tiles, 4 skip heavy tiles, 16 phase A only,
-  32 phases A + B1, 512 no T_pub code atomics); >= 65536: product kernel on a grid of variant - 65536 blocks.  The graph is generated on the GPU.
+  32 phases A + B1, 512 no T_pub code atomics; 5 / 13: 5 / 6 waves per SIMD; 17 / 21 / 25: two tiles per wait at
+  8 / 6 / 7 waves per SIMD; 29 / 33: three tiles per wait at 5 / 4; 37: four at 4), plus grid << 16 (grid blocks;
+  0: the product grid -- only the product grid is valid in records mode, whose per-wave record slices follow it).
+  The graph is generated on the GPU.
 """
 import ctypes
 import os
@@ -18,7 +21,7 @@ from fuzzypatternmatching_amd import _abi  # noqa: E402
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 22
 p_gen = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-variants = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 8, 2, 4]
+variants = [int(x, 0) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 8, 2, 4]
 m, _ = pm.rmat_matcher(scale, p_gen, os.path.join(ROOT, "patterns", "rmat_log2_tree_pattern"))
 lib = _abi.load()
 st = (ctypes.c_uint64 * 6)()
