@@ -521,6 +521,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         // supersteps, the NLC lines and the next reset walk the live entries only.  (Appending the live
         // entries inside the superstep, one counter reservation per 64-entry chunk, measured 1.2 ms slower
         // at S=28: 153 k atomics on one address serialise.)
+        c.cur_ss = init_step ? ss : 0;
         launch_lcc_step(c, slot, init_step && ss == 1);
         debug_point(c, "pull superstep"); debug_watch(c, "pull superstep");
         if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
@@ -589,6 +590,15 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         out.loc_surv += local[r];
         out.loc_edges += local[P + r];
       }
+    }
+    if (init_step) {  // the survivors' mean |M| per superstep (the next search's entries in flight)
+      uint64_t v = 0, e = 0;
+      for (uint32_t r = 0; r < c.nranks; ++r) {
+        v += h[r];
+        e += h[P + r];
+      }
+      if (c.m_per_row.size() < D) c.m_per_row.resize(D, 0.0);
+      c.m_per_row[ss] = v ? double(e) / double(v) : 0.0;
     }
     if (h[2 * P + 2]) out.not_finished = true;
     if (h[2 * P + 3]) asym = true;

@@ -441,6 +441,10 @@ struct Ctx {
   bool k1_records = false;        // the last superstep-0 launch wrote records (and no tile masks)
   bool k1_dense = false;         // the last superstep-0 launch wrote dense M
   uint32_t diag_step = 0;        // diagnostics only (PM_DIAG_STEP): k_lcc_step timing variants
+  // the last first LCC call's mean |M| of each superstep's survivors (k_lcc_step's entries in flight for the
+  // next superstep's rows), and the superstep being launched
+  std::vector<double> m_per_row;
+  uint64_t cur_ss = 0;
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile
   uint32_t* d_tstart = nullptr;   // position of a tile's row 0 (heavy tile: its row)
   void* d_scan_tmp = nullptr;     // rocPRIM scan workspace for the slist build

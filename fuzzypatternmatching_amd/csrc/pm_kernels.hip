@@ -1100,13 +1100,14 @@ struct RecSrc {
   const uint4* cdesc;  // per chunk {rarea index of its first record (lo, hi), its records in that slice, next slice}
   uint32_t W;
 };
-#ifndef PM_STEP_UNROLL
-#define PM_STEP_UNROLL 3  // entries in flight per lane in k_lcc_step's flattened rows (4 spills registers at 6 waves)
-#endif
-static constexpr int kStepUnroll = PM_STEP_UNROLL;
+// U: entries in flight per lane in the flattened rows.  3 when the superstep's rows are short (S=28's first
+// later superstep: 3.2 entries per row, a chunk of 64 rows fits one round of 192; 4 spills 16 VGPRs at 6 waves
+// per SIMD, and the spill reloads are memory operations in the same in-order counter: 564 -> 519 us), 4
+// otherwise (C5: longer rows, 4 in flight was 10-40 % faster on every pull superstep).
 #ifndef PM_STEP_WAVES
 #define PM_STEP_WAVES 6  // waves per SIMD the register budget of k_lcc_step is sized for
 #endif
+template <int U>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_WAVES, 8))) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
@@ -1238,13 +1239,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
       s_tn[w][lane] = 0;
       s_cnt[w][lane] = 0;
       __builtin_amdgcn_wave_barrier();
-      for (uint32_t t0 = 0; t0 < total; t0 += kStepUnroll * kWave) {
-        uint32_t m[kStepUnroll];
-        uint16_t tv[kStepUnroll];
-        int rr[kStepUnroll];
-        uint64_t e[kStepUnroll];
+      for (uint32_t t0 = 0; t0 < total; t0 += U * kWave) {
+        uint32_t m[U];
+        uint16_t tv[U];
+        int rr[U];
+        uint64_t e[U];
 #pragma unroll
-        for (int q = 0; q < kStepUnroll; ++q) {
+        for (int q = 0; q < U; ++q) {
           const uint32_t t = t0 + q * kWave + lane;
           m[q] = 0u;
           rr[q] = 0;
@@ -1261,10 +1262,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
           }
         }
 #pragma unroll
-        for (int q = 0; q < kStepUnroll; ++q)
+        for (int q = 0; q < U; ++q)
           tv[q] = (m[q] & kAlive) ? ((diag & 1) ? uint16_t(m[q] & 0x7Fu) : tpub_of(m[q] & kPosMask)) : uint16_t(0);
 #pragma unroll
-        for (int q = 0; q < kStepUnroll; ++q)
+        for (int q = 0; q < U; ++q)
           if (m[q] & kAlive) {
             uint32_t tq = 0, cq = 0;
             k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym, !(diag & 4));
@@ -2536,7 +2537,12 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   RecSrc rs{};
   if (first_after_ss0 && c.k1_records && c.records_in_place)
     rs = RecSrc{c.d_rarea, c.d_rbase, c.d_rofs, c.d_cdesc, c.rwaves};
-  hipLaunchKernelGGL(k_lcc_step, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
+  // short rows: the previous search's mean |M| of this superstep's rows (the survivors of the one before;
+  // the first search guesses long)
+  const double mpr = c.cur_ss > 0 && c.cur_ss - 1 < c.m_per_row.size() ? c.m_per_row[c.cur_ss - 1] : 0.0;
+  const bool short_rows = mpr > 0 && mpr <= 4.0;
+  auto kern = short_rows ? k_lcc_step<3> : k_lcc_step<4>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                      c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,

@@ -241,8 +241,6 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
 // long row costs one pass over the wave instead of a serial walk by one lane).
 static constexpr int kLineWaves = 16;  // kLineBlock / kWave
 static constexpr int kStage = 10;      // TDS walks of up to kStage positions are staged in LDS
-static constexpr int kChildBuf = 256;  // TDS children a wave holds in LDS before writing them out
-static constexpr int kTdsUnroll = 2;   // entry groups per round of the TDS expansion (one round in flight ahead)
 struct WaveRows {
   uint64_t beg[kLineWaves][kWave];
   uint32_t end[kLineWaves][kWave];  // inclusive scan of the row lengths
@@ -254,9 +252,6 @@ struct WaveRows {
   };
   unsigned long long wn[20];  // walks per position of a single-block TDS line
   unsigned lpany[20];         // a row of this position went to the piece list (single-block lines: no global read)
-  // TDS expansion: the children a wave found, written out after its rows are walked (tds_expand_wave)
-  uint32_t cnb[kLineWaves][kChildBuf];  // the child's new vertex
-  uint8_t cpar[kLineWaves][kChildBuf];  // its parent walk (the wave's lane)
 };
 
 // Lane owning concatenated entry t (end[] inclusive scan of the wave's rows).
@@ -611,8 +606,7 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
                                                 uint64_t i0, int k, uint64_t b, uint32_t L, uint32_t* out,
                                                 uint64_t out_room, int stride, bool stage,
                                                 unsigned long long* ctr) {
-  const LineArgs& la = s_la;
-  k = __builtin_amdgcn_readfirstlane(k);
+  const LineArgs& la = *a.la;
   const int wv = threadIdx.x / kWave, lane = lane_id();
   const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(L));
   const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
@@ -620,14 +614,12 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
   wr.beg[wv][lane] = b;
   wr.end[wv][lane] = incl;
   __builtin_amdgcn_wave_barrier();
-  // The rows are walked in rounds of kTdsUnroll groups of 64 entries, the next round's entries requested before
-  // the current round is checked; the children go to the wave's LDS buffer and are written out after the
-  // last round (or when the buffer is full).  The only vector memory operations of the rounds are the entry
-  // loads, so a round waits for its own entries only (the memory counter retires loads and stores in issue
-  // order: a child store between two rounds would make the next round's loads wait for it too).
-  auto load_round = [&](uint32_t t0, uint32_t (&mm)[kTdsUnroll], int (&rr)[kTdsUnroll]) {
+  // kUnroll groups of 64 entries per round (tp_forward); the round's children share one reservation
+  for (uint32_t t0 = 0; t0 < total; t0 += kUnroll * kWave) {
+    uint32_t mm[kUnroll];
+    int rr[kUnroll];
 #pragma unroll
-    for (int j = 0; j < kTdsUnroll; ++j) {
+    for (int j = 0; j < kUnroll; ++j) {
       const uint32_t t = t0 + j * kWave + lane;
       mm[j] = 0;
       rr[j] = 0;
@@ -638,61 +630,30 @@ __device__ __forceinline__ void tds_expand_wave(const LineKernelArgs& a, WaveRow
         mm[j] = a.mcol[wr.beg[wv][r] + (t - first)];
       }
     }
-  };
-  auto walk_of = [&](int r) -> const uint32_t* {
-    return stage ? wr.walk[wv] + r * stride : win + (i0 + r) * stride;
-  };
-  uint32_t nbuf = 0;  // children in the buffer (wave-uniform)
-  auto flush = [&]() {
-    for (uint32_t c0 = 0; c0 < nbuf; c0 += kWave) {
-      const uint32_t c = c0 + lane;
-      const uint64_t pos = wave_reserve(ctr, c < nbuf ? 1u : 0u);
-      if (c < nbuf) {
-        const uint32_t* w = walk_of(wr.cpar[wv][c]);
-        if ((pos + 1) * stride <= out_room) {
-          uint32_t* d = out + pos * stride;
-          for (int p = 0; p <= k; ++p) d[p] = w[p];
-          d[k + 1] = wr.cnb[wv][c];
-        } else {
-          atomicOr(&a.st->overflow, 1u);
-        }
-      }
-    }
-    nbuf = 0;
-    __builtin_amdgcn_wave_barrier();
-  };
-  uint32_t mn[kTdsUnroll];
-  int rn[kTdsUnroll];
-  load_round(0, mn, rn);
-  for (uint32_t t0 = 0; t0 < total; t0 += kTdsUnroll * kWave) {
-    uint32_t mm[kTdsUnroll];
-    int rr[kTdsUnroll];
-#pragma unroll
-    for (int j = 0; j < kTdsUnroll; ++j) {
-      mm[j] = mn[j];
-      rr[j] = rn[j];
-    }
-    if (t0 + kTdsUnroll * kWave < total) load_round(t0 + kTdsUnroll * kWave, mn, rn);
     uint32_t cm = 0;  // children of the round (bit j)
 #pragma unroll
-    for (int j = 0; j < kTdsUnroll; ++j)
-      if ((mm[j] & kAlive) && tds_child_ok(walk_of(rr[j]), k, mm[j] & kPosMask, la)) cm |= 1u << j;
+    for (int j = 0; j < kUnroll; ++j) {
+      const uint32_t* w = stage ? wr.walk[wv] + rr[j] * stride : win + (i0 + rr[j]) * stride;
+      if ((mm[j] & kAlive) && tds_child_ok(w, k, mm[j] & kPosMask, la)) cm |= 1u << j;
+    }
     const uint32_t nc = __popc(cm);
-    const uint32_t cincl = static_cast<uint32_t>(wave_incl_scan(nc));
-    const uint32_t rtotal = static_cast<uint32_t>(__shfl(cincl, kWave - 1, kWave));
-    if (nbuf + rtotal > static_cast<uint32_t>(kChildBuf)) flush();
-    uint32_t c = nbuf + cincl - nc;
+    const uint64_t pos = wave_reserve(ctr, nc);
+    uint32_t c = 0;
 #pragma unroll
-    for (int j = 0; j < kTdsUnroll; ++j) {
+    for (int j = 0; j < kUnroll; ++j) {
       if (!((cm >> j) & 1u)) continue;
-      wr.cnb[wv][c] = mm[j] & kPosMask;
-      wr.cpar[wv][c] = static_cast<uint8_t>(rr[j]);
+      const uint32_t* w = stage ? wr.walk[wv] + rr[j] * stride : win + (i0 + rr[j]) * stride;
+      if ((pos + c + 1) * stride <= out_room) {
+        uint32_t* d = out + (pos + c) * stride;
+        for (int p = 0; p <= k; ++p) d[p] = w[p];
+        d[k + 1] = mm[j] & kPosMask;
+      } else {
+        atomicOr(&a.st->overflow, 1u);
+      }
       ++c;
     }
-    nbuf += rtotal;
-    __builtin_amdgcn_wave_barrier();
   }
-  flush();
+  __builtin_amdgcn_wave_barrier();
 }
 
 // The long-row pieces of position k of a TDS line (items: the source at k = 0, the walk's index in win after):
@@ -1460,7 +1421,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
       std::string pos = "[pm]   positions (walks in, us, long-row pieces):";
       unsigned long long prev = st.tstamp[1];
       for (int k = 1; k < 20 && st.ptime[k]; ++k) {
-        char b[96];
+        char b[192];
         std::snprintf(b, sizeof(b), " %d:(%llu, %.1f, %llu)", k, st.wn[k], (st.ptime[k] - prev) * 0.01, st.lp[k]);
         if (st.pmid[k][1] > prev)  // TDS: [state of the first walks in, expansion done] after the position start
           std::snprintf(b + std::strlen(b), sizeof(b) - std::strlen(b), "[%.1f %.1f %llu]",

@@ -10,8 +10,10 @@ C5: ingested text edge list (-u 1) + explicit -v label files (hash32(v) % 64)
     S=22, and at size (S=27, alphabet 256, GPU ingest, chunked TDS, oracle).
 C4': S=28, P_gen=8, tree on ONE GPU against tests/golden/rmat_s28_p8_tree.json
     (the oracle needs ~100 GB of host memory there, so its result was made once:
-    tests/golden/make_rmat_fixture.py), and C4's sharded path at full size (two
-    in-process shards, delegates at -d 1048576) against the same fixture.
+    tests/golden/make_rmat_fixture.py), and C4's sharded path at full size (2, 4 and
+    8 in-process shards, delegates at -d 1048576) against the same fixture.
+C5 at S=27 on the GPU-generated graph (hash-256 labels, 4-cycle), one and four
+    shards (every line split by owner), against tests/golden/rmat_s27_p8_cycle4_hash256.json.
 """
 import os
 import subprocess
@@ -249,6 +251,35 @@ def test_c4_s28_sharded_delegates_one_gpu(nshards, tmp_path):
     assert all(x > 0 for x in table["shard_hub_entries"])  # every shard holds delegate shares
     assert sum(x > 0 for x in table["shard_hubs_controlled"]) >= min(2, nshards)  # controllers spread
     assert sum(table["shard_hubs_controlled"]) == sg["hubs"]
+    diffs = pmtest.digest_diffs(fx["digest"], pmtest.result_digest(str(out), 1))
+    for k_g, k_o in (("iterations", "iterations"), ("terminated", "terminated"), ("final_vertices", "final_vertices"),
+                     ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"),
+                     ("tds_edges", "tds_edges"), ("walks", "paths")):
+        if sg[k_g] != fx["stats"][k_o]:
+            diffs.append(f"{k_g}: gpu {sg[k_g]} != oracle {fx['stats'][k_o]}")
+    assert diffs == [], diffs[:5]
+
+
+@pytest.mark.parametrize("nshards", [1, 4])
+def test_c5_s27_generated_split_lines_fixture(nshards, tmp_path):
+    """Config C5's search (S=27, P_gen=8, labels hash32(v ^ 5) % 256, 4-cycle: 4 cycle-check lines + the TDS
+    line) on the GPU-generated graph, one shard and four in-process shards, against the oracle's S=27 digest
+    (tests/golden/rmat_s27_p8_cycle4_hash256.json, made on the GPU box's host by make_rmat_fixture.py; the
+    bench's nlcc_config checks the one-context path against it).  With four shards every NLC line runs split by
+    source owner (the split is decided on the lines' first-position token census) and its
+    effects are exchanged; the result must not change."""
+    import json
+    fixture = os.path.join(pmtest.ROOT, "tests", "golden", "rmat_s27_p8_cycle4_hash256.json")
+    fx = json.load(open(fixture))
+    _graphs.clear()
+    out = tmp_path / "shards"
+    labels = pmtest.hash_labels(1 << 27, 256, salt=5)
+    each = pm.run_rmat_local_shards_each(27, 8, CYCLE, nshards, str(out), max_iterations=64, nranks=1,
+                                         hub_threshold=pm.DEFAULT_HUB_THRESHOLD, labels=labels)
+    sg = each[0]
+    print(f"C5 S=27 x{nshards}: split lines {[s['split_lines'] for s in each]}, {sg}")
+    if nshards > 1:
+        assert all(s["split_lines"] > 0 for s in each)  # the lines ran split by owner
     diffs = pmtest.digest_diffs(fx["digest"], pmtest.result_digest(str(out), 1))
     for k_g, k_o in (("iterations", "iterations"), ("terminated", "terminated"), ("final_vertices", "final_vertices"),
                      ("final_edges", "final_edges"), ("lcc_edges", "lcc_edges"), ("nlcc_edges", "nlcc_edges"),

@@ -53,6 +53,28 @@ def test_rmat_matches_oracle(pat, scale, p_gen, alphabet, nranks, tmp_path):
     assert sg["walks"] == so["paths"]
 
 
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet", [("tree", 16, 4, None), ("cycle", 14, 4, None),
+                                                     ("cycle", 12, 4, 8)])
+def test_repeated_searches_on_one_context(pat, scale, p_gen, alphabet, tmp_path):
+    # three searches on one context (as the bench runs them): each must reproduce the oracle.  From the second
+    # search on, the first later superstep's kernel is chosen from the previous search's superstep-0 survivors
+    # (short rows: 3 entries in flight per lane, else 4), so both instantiations meet the oracle here.
+    g = pm.rmat_graph(scale, p_gen)
+    labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
+    a = tmp_path / "oracle"
+    so = oracle.run(g.off, g.col, PATTERNS[pat], str(a), labels=labels, nranks=1)
+    m = pm.PatternMatcher(pm.Graph(g.off, g.col, True, 1), PATTERNS[pat], labels=labels)
+    try:
+        for i in range(3):
+            b = tmp_path / f"gpu{i}"
+            sg = m.run_beta(str(b))
+            assert pmtest.compare_result_dirs(str(a), str(b), 1) == [], i
+            assert (sg["lcc_edges"], sg["nlcc_edges"], sg["tds_edges"], sg["walks"]) == \
+                (so["lcc_edges"], so["nlcc_edges"], so["tds_edges"], so["paths"]), i
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks", [RMAT_CASES[2], RMAT_CASES[5], RMAT_CASES[7]])
 def test_exact_count_token_passing_matches_oracle(pat, scale, p_gen, alphabet, nranks, tmp_path, monkeypatch):
     # PM_FUSED_LINES=0: every NLC line through the per-position launch path
