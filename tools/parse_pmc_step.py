@@ -44,6 +44,9 @@ def main():
         d = {"index": j - max(0, n - per), "counters": c, "us_under_pmc": round(min(ns) / 1e3, 1)}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             d["hbm_bytes"] = int((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+            # (the 2x is the streaming-read correction; a narrow random gather miss is tallied as one 64-B
+            # request (tools/gather_floor.py calibration), so the gathers' share is over-stated by it)
+            d["fetch_requests_64B"] = int(c["FETCH_SIZE"] * 1024 / 64)
         res["dispatches"].append(d)
     json.dump(res, open(out, "w"), indent=1)
     for d in res["dispatches"]:
