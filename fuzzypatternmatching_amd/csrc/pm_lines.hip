@@ -722,8 +722,11 @@ __device__ __forceinline__ void phase_sync(const LineKernelArgs& a, bool single)
 // wait at a grid barrier; once a position's frontier outgrows it, block 0 stops
 // and the whole grid continues from that position (escalation: R-MAT hubs make
 // a small line's later positions explode).  LineKernelArgs::small_line,
-// PM_SMALL_LINE overrides.
-static constexpr uint64_t kSmallLine = 16384;
+// PM_SMALL_LINE overrides.  Round 5: with a position's items spread over every wave (16 to 64 per wave), the
+// grid finishes a position of a few hundred walks sooner than block 0 does despite its barriers (the S=28 TDS
+// line: 7 positions of 446-1693 walks, 85 us on the grid vs 125 us on block 0), so block 0 keeps only the
+// tiny lines.
+static constexpr uint64_t kSmallLine = 256;
 
 // ---- path / cycle lines (nem_1) ----------------------------------------
 // Positions 2..C+1 and post-processing; every participating wave calls it.
@@ -749,9 +752,11 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
       }
       return true;
     }
-    for (uint64_t i0 = lo + g.gw * kWave; i0 < hi; i0 += g.nw * kWave) {
+    // frontier items per wave and pass: spread over every wave (16 to 64 each), as in tds_rest
+    const uint64_t per = min<uint64_t>(kWave, max<uint64_t>(16, (hi - lo + g.nw - 1) / g.nw));
+    for (uint64_t i0 = lo + g.gw * per; i0 < hi; i0 += g.nw * per) {
       const uint64_t i = i0 + lane_id();
-      const bool act = i < hi;
+      const bool act = static_cast<uint64_t>(lane_id()) < per && i < hi;
       uint32_t s = 0, u = 0, excl = kNone, h = 0;
       if (act) {
         h = ld_dev(&a.front[i]);
@@ -864,12 +869,15 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
     const uint32_t* win = a.wbuf + in_base;
     unsigned long long* ctr = single ? &wr.wn[k + 1] : &st->wn[k + 1];
     const bool closing = k == la.C && la.VC;
-    for (uint64_t i0 = g.gw * kWave; i0 < nin; i0 += g.nw * kWave) {
+    // walks per wave and pass: a position of a few hundred walks is spread over every wave (16 to 64 each), so
+    // no wave walks the rows of 64 walks while others idle
+    const uint64_t per = min<uint64_t>(kWave, max<uint64_t>(16, (nin + g.nw - 1) / g.nw));
+    for (uint64_t i0 = g.gw * per; i0 < nin; i0 += g.nw * per) {
       const uint64_t i = i0 + lane;
       uint64_t b = 0;
       uint32_t L = 0;
       const uint32_t* cw = nullptr;
-      if (i < nin) {
+      if (static_cast<uint64_t>(lane) < per && i < nin) {
         const uint32_t* w = win + i * stride;
         uint32_t u;
         if (stage) {  // the walk's positions (independent loads) into the wave's stage
@@ -887,7 +895,7 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
         const uint64_t ob = a.offp[u];
         uint32_t ml = a.mlen[u], ma = a.malive[u];
         if (!row_ok(a, u, ob, ml)) ml = 0;
-        if (a.stamps && g.tid == 0 && i0 == g.gw * kWave) {  // (diagnostics: the first walks' state is in)
+        if (a.stamps && g.tid == 0 && i0 == g.gw * per) {  // (diagnostics: the first walks' state is in)
           __builtin_amdgcn_s_waitcnt(0);
           st->pmid[k][0] = __builtin_amdgcn_s_memrealtime() + (T & 0u) + (ml & 0u);
         }
