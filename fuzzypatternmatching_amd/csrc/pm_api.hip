@@ -474,6 +474,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   // the search's reset fills go with superstep 0's own (one launch, before the call's timing event)
   if (init_step) queue_lcc_first_fills(c);
   flush_zero(c);
+  c.probe("zero flushed");
   PM_HIP_CHECK(hipEventRecord(ev[0], c.stream));
   bool k_timed = false, handed_off = false;
   // diagnostics: PM_DEBUG_LCC_STOP=k -- the first call runs supersteps 0..k-1 only
@@ -495,6 +496,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
       launch_lcc_first(c, slot, ev[D + 1], ev[D + 2]);
+      c.probe("superstep 0 launched");
       debug_point(c, "superstep 0"); debug_watch(c, "superstep 0");
       k_timed = true;
       // |slist| is read back with the counters at the end of the call; until
@@ -557,7 +559,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
   if (c.prelaunch_lines) prelaunch_lines_fused(c);  // the device goes on with the lines while the host parses
   debug_point(c, "counters + prelaunched lines");
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  stream_wait(c.stream);
   c.probe("lcc synced");
   std::vector<uint64_t> host(pin + 1 + D * W, pin + 1 + 2 * D * W);
   std::vector<uint64_t> local = sharded_slots ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
@@ -760,12 +762,22 @@ static void add_walk_lines(const Ctx& c, std::vector<std::vector<std::string>>& 
 }
 
 // run_pattern_matching_beta.cpp:539-1425
+// (diagnostics, PM_HOST_PROBES=1: the host's time between searches -- from the previous run_beta's return to
+// this one's entry, its setup before the first launch, and its end after the last sync -- on stderr)
+static std::chrono::steady_clock::time_point g_last_return{};
+static double g_last_tail_us = 0;  // the previous search: its last probe ("end") to its return
 static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations, pm_run_stats* st) {
+  const auto t_entry = std::chrono::steady_clock::now();
+  static const bool host_probes = std::getenv("PM_HOST_PROBES") != nullptr;
+  c.probes.clear();
+  c.probing = host_probes || std::getenv("PM_PHASE_TIMES") != nullptr;
+  c.probe("entry");
   const Pattern& P = c.pattern;
   const bool files = !out_dir.empty();
   static const bool build_lines_anyway = std::getenv("PM_BUILD_LINES") != nullptr;  // diagnostics (A/B)
   const bool lines_on = files || build_lines_anyway;
   reset_state(c, true);  // flushed with superstep 0's fills
+  c.probe("reset");
   DriverFiles f;
   f.vcount.assign(c.nranks, {});
   f.ecount.assign(c.nranks, {});
@@ -788,8 +800,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
   // PM_PHASE_TIMES=1: per-phase host wall time on stderr (diagnostics)
   const bool phase_times = std::getenv("PM_PHASE_TIMES") != nullptr;
   c.fine_timing = files || phase_times;
-  c.probing = phase_times;
-  c.probes.clear();
+  c.probing = phase_times || host_probes;
   double ph_lcc = 0, ph_tp = 0, ph_post = 0, ph_count = 0;
   auto tick = [] { return std::chrono::steady_clock::now(); };
   uint64_t itr = 0;
@@ -973,14 +984,21 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     ++itr;
   } while (nf);
   c.probe("iterations done");
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  stream_wait(c.stream);
   c.probe("end");
   const double secs = since(t_pattern);
   if (phase_times)
     std::fprintf(stderr, "[pm] run_beta %.3f ms: lcc %.3f, token passing %.3f, post %.3f, counts %.3f, device %.3f\n",
                  secs * 1e3, ph_lcc * 1e3, ph_tp * 1e3, ph_post * 1e3, ph_count * 1e3, c.device_seconds * 1e3);
-  if (phase_times && !c.probes.empty()) {
+  if ((phase_times || host_probes) && !c.probes.empty()) {
     std::string line = "[pm] host:";
+    if (g_last_return.time_since_epoch().count()) {
+      char buf[128];
+      std::snprintf(buf, sizeof(buf), " (previous end to return %.1f, return to entry %.1f, entry to start %.1f)",
+                    g_last_tail_us, std::chrono::duration<double>(t_entry - g_last_return).count() * 1e6,
+                    (c.probes[0].second - std::chrono::duration<double>(t_entry.time_since_epoch()).count()) * 1e6);
+      line += buf;
+    }
     double prev = c.probes[0].second;
     for (const auto& pr : c.probes) {
       char buf[96];
@@ -1059,6 +1077,12 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
     }
   }
   if (st) *st = s;
+  if (host_probes) {
+    g_last_return = std::chrono::steady_clock::now();
+    g_last_tail_us = c.probes.empty() ? 0.0
+                                      : (std::chrono::duration<double>(g_last_return.time_since_epoch()).count() -
+                                         c.probes.back().second) * 1e6;
+  }
 }
 
 }  // namespace pm

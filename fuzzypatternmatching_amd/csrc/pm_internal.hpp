@@ -567,6 +567,9 @@ void launch_clear_tpub(Ctx& c);
 void zero_later(Ctx& c, void* p, uint64_t bytes);
 void queue_lcc_first_fills(Ctx& c);
 void flush_zero(Ctx& c);
+// Waits for the stream by polling it (hipStreamQuery): the driver loop's read-back waits, so the host follows
+// the device at once instead of sleeping until the runtime wakes it (PM_SPIN=0: hipStreamSynchronize).
+void stream_wait(hipStream_t s);
 size_t slist_scan_tmp_bytes(uint64_t words);
 static constexpr unsigned kPartGridMax = 2048;
 

@@ -2788,6 +2788,19 @@ void zero_later(Ctx& c, void* p, uint64_t bytes) {
   c.zq[c.nzq++] = Ctx::ZeroRange{p, bytes};
 }
 
+void stream_wait(hipStream_t s) {
+  static const bool spin = !std::getenv("PM_SPIN") || std::string(std::getenv("PM_SPIN")) != "0";
+  if (!spin) {
+    PM_HIP_CHECK(hipStreamSynchronize(s));
+    return;
+  }
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) PM_HIP_CHECK(e);
+  }
+}
+
 void flush_zero(Ctx& c) {
   if (!c.nzq && !c.clear_pending) return;
   ZeroBatch b{};

@@ -1387,7 +1387,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
   c.lines_prelaunched = false;
   if (pl0 >= nl) return 0;
   uint64_t* pin = c.h_pin_lines;
-  PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+  stream_wait(c.stream);
   c.probe("lines synced");
   std::vector<LineStats> hs(nl - pl0);
   std::memcpy(hs.data(), reinterpret_cast<const char*>(pin) + 64 * sizeof(unsigned) + pl0 * sizeof(LineStats),
