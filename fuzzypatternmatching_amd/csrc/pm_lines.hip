@@ -739,10 +739,13 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
     if (threadIdx.x < 20) wr.lpany[threadIdx.x] = 0u;
     __syncthreads();
   }
+  // (the overflow flag and the frontier end read together after each position's barrier, as in tds_rest)
+  unsigned ovf_next = ld_dev(&st->overflow);
+  uint64_t hi_next = ld_dev(&st->ftotal);
   for (int k = k0; k <= s_la.C; ++k) {
     k = __builtin_amdgcn_readfirstlane(k);  // (uniform: the line's constants indexed by k load through the scalar cache)
-    if (ld_dev(&st->overflow)) break;  // same value in every wave after the barrier
-    const uint64_t hi = ld_dev(&st->ftotal);
+    if (ovf_next) break;  // same value in every wave after the barrier
+    const uint64_t hi = hi_next;
     if (single && hi - lo > a.small_line) {  // the frontier outgrew the block: the grid takes position k
       wave_add(&st->trav, trav);
       wave_add(&st->tokens, tokens);
@@ -771,9 +774,14 @@ __device__ __forceinline__ bool path_rest(const LineKernelArgs& a, const GridIdx
     }
     lo = hi;
     phase_sync(a, single);
-    if (single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull) {  // the position's long rows, over every wave
+    const bool pieces = single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull;
+    ovf_next = ld_dev(&st->overflow);
+    hi_next = ld_dev(&st->ftotal);
+    if (pieces) {  // the position's long rows, over every wave
       tokens += tp_pieces(a, g, k);
       phase_sync(a, single);
+      ovf_next = ld_dev(&st->overflow);
+      hi_next = ld_dev(&st->ftotal);
     }
     if (a.stamps && g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
   }
@@ -850,10 +858,14 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
     __syncthreads();
   }
   const int wv = threadIdx.x / kWave, lane = lane_id();
+  // the overflow flag and the next position's walk count, read together after each position's barrier (and
+  // the long-row piece count with them): three independent loads instead of a chain across the boundary
+  unsigned ovf_next = ld_dev(&st->overflow);
+  uint64_t nin_next = single ? 0 : ld_dev(&st->wn[k0]);
   for (int k = k0; k <= la.C; ++k) {
     k = __builtin_amdgcn_readfirstlane(k);  // (uniform: the line's constants indexed by k load through the scalar cache)
-    if (ld_dev(&st->overflow)) break;
-    const uint64_t nin = single ? wr.wn[k] : ld_dev(&st->wn[k]);
+    if (ovf_next) break;
+    const uint64_t nin = single ? wr.wn[k] : nin_next;
     if (single && nin > a.small_line) {  // the walks outgrew the block: the grid takes position k
       if (threadIdx.x >= 2 && threadIdx.x <= static_cast<unsigned>(k)) st->wn[threadIdx.x] = wr.wn[threadIdx.x];
       wave_add(&st->trav, trav);
@@ -936,9 +948,14 @@ __device__ __forceinline__ bool tds_rest(const LineKernelArgs& a, const GridIdx&
     }
     if (a.stamps && g.tid == 0) st->pmid[k][1] = __builtin_amdgcn_s_memrealtime();
     phase_sync(a, single);
-    if (single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull) {  // the position's long rows, over every wave
+    const bool pieces = single ? wr.lpany[k] != 0u : ld_dev(&st->lp[k]) != 0ull;
+    ovf_next = ld_dev(&st->overflow);
+    nin_next = single ? 0 : ld_dev(&st->wn[k + 1]);
+    if (pieces) {  // the position's long rows, over every wave
       tds_pieces(a, g, k, win, a.wbuf + out_base, a.wcap > out_base ? a.wcap - out_base : 0, stride, ctr);
       phase_sync(a, single);
+      ovf_next = ld_dev(&st->overflow);
+      nin_next = single ? 0 : ld_dev(&st->wn[k + 1]);
     }
     in_base = out_base;
     if (a.stamps && g.tid == 0) st->ptime[k] = __builtin_amdgcn_s_memrealtime();
