@@ -1206,8 +1206,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PM_STEP_
       uint32_t a0 = l;
       if (dm == kNone) {
         b = offp[u];
-        a0 = malive[u];
-        Ts = tst[u];
+        a0 = (diag & 16) ? l : malive[u];  // (timing variant: two of the row's scattered state loads dropped)
+        Ts = (diag & 16) ? Tu : tst[u];
       } else {
         Ts = Tu;
       }
