@@ -34,6 +34,9 @@
 #include <thread>
 
 struct pm_ctx : public pm::Ctx {};
+namespace pm {
+void gather_floor_forget(const void* owner);  // (diagnostics: the gather-floor cache of a destroyed context)
+}
 
 namespace pm {
 
@@ -1099,7 +1102,10 @@ pm_ctx* pm_create(const pm_graph_desc* graph, const char* pattern_dir, int devic
   }
 }
 
-void pm_destroy(pm_ctx* ctx) { pm::destroy_ctx(ctx); }
+void pm_destroy(pm_ctx* ctx) {
+  pm::gather_floor_forget(ctx ? static_cast<const void*>(static_cast<pm::Ctx*>(ctx)) : nullptr);
+  pm::destroy_ctx(ctx);
+}
 
 const char* pm_last_error(const pm_ctx* ctx) {
   if (ctx && !ctx->err.empty()) return ctx->err.c_str();
@@ -2323,6 +2329,9 @@ struct GatherFloor {
   }
 };
 static GatherFloor g_gather;
+void gather_floor_forget(const void* owner) {
+  if (owner && g_gather.owner == owner) g_gather.release();
+}
 
 static void gather_floor_build(Ctx& c) {
   g_gather.release();
