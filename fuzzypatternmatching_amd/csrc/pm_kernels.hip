@@ -1107,10 +1107,9 @@ struct RecSrc {
 #ifndef PM_STEP_WAVES
 #define PM_STEP_WAVES 6  // waves per SIMD the register budget of k_lcc_step is sized for
 #endif
-// KIND 1: the first later superstep with superstep-0 records and codes (srec, tcode non-null, every entry live);
-// KIND 2: a later superstep from the list (srec, tcode null); KIND 0: either, decided at run time.  The
-// specialised kinds fold the other paths away, so each holds only the registers its superstep needs.
-template <int U, int KIND = 0, int WAVES = PM_STEP_WAVES>
+// FIRST: the first later superstep with superstep-0 records and codes (srec, tcode non-null, every entry live):
+// the generic paths folded away, so the instantiation holds only the registers that superstep needs.
+template <int U, bool FIRST = false, int WAVES = PM_STEP_WAVES>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_lcc_step(
     const uint64_t* __restrict__ offp, const uint32_t* __restrict__ slist, const uint32_t* __restrict__ nSp,
     const unsigned long long* __restrict__ mask_in, unsigned long long* __restrict__ mask_out,
@@ -1141,7 +1140,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   // T_pub of neighbour position p: from the 2-bit codes when present (the
   // label's template bits from its run), the T_pub array otherwise
   auto tpub_of = [&](uint32_t p) -> uint16_t {
-    if (KIND == 2 || (KIND == 0 && !tcode)) return tcur[p];
+    if (!FIRST && !tcode) return tcur[p];
     // the label's template bits and the code index from its run (an M entry lies in a template label's run)
     uint32_t tu = 0, ci = 0;
     for (int l = 0; l < nruns; ++l)
@@ -1172,7 +1171,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       // the row's state is loaded with T_pub in one round trip (a removed
       // row, T_pub = 0, ignores it)
       uint32_t l, dm = kNone;
-      if (KIND == 1 || (KIND == 0 && srec)) {  // dense superstep-0 output: the records, in slist order (coalesced)
+      if (FIRST || srec) {  // dense superstep-0 output: the records, in slist order (coalesced)
         uint4 r;
         if (rs.rarea) {  // in place: the chunk's first slice, a later one for lanes past its end (rare)
           // (descriptors exist for the light records' chunks only: the heavy records after them are in srec)
@@ -1333,14 +1332,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         // dense superstep-0 records: both T_pub buffers of u are still clean (superstep 0 wrote u's
         // T_pub only into its record) and its state arrays were never written, so a removed row writes
         // nothing -- M[v] cleared (nonunique_ee.hpp:941-964) is its absence from every later list
-        if (!(KIND == 1 || (KIND == 0 && srec)) || !drow) {
+        if (!(FIRST || srec) || !drow) {
           tnxt[u] = 0;
           malive[u] = 0;
         }
         // first later superstep: neighbours read u's T_pub through the 2-bit codes unless u's label has
         // more than two template vertices, so the buffer read now can be cleared at once and u leaves
         // the live list (otherwise it stays live one more superstep, which clears the other buffer)
-        if (KIND == 1 || (KIND == 0 && tcode)) {
+        if (FIRST || tcode) {
           uint32_t tu = 0;
           for (int l = 0; l < nruns; ++l)
             if (u - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
@@ -1409,7 +1408,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       }
     }
   };
-  if (KIND == 1 || !mask_in) {
+  if (FIRST || !mask_in) {
     // first later superstep (every entry live): one chunk per wave at a time
     for (uint64_t chunk = uint64_t(blockIdx.x) * kWpb + w; chunk < nchunks; chunk += uint64_t(gridDim.x) * kWpb)
       chunk_body(chunk, ~0ull);
@@ -2545,10 +2544,9 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   const double mpr = c.cur_ss > 0 && c.cur_ss - 1 < c.m_per_row.size() ? c.m_per_row[c.cur_ss - 1] : 0.0;
   const bool short_rows = mpr > 0 && mpr <= 4.0;
   auto kern = short_rows ? k_lcc_step<3> : k_lcc_step<4>;
-  // records and codes / a later superstep: the specialised instantiations (the first: no spills at 6 waves
-  // per SIMD; budgets for 7 / 8 waves spilled 13 / 31 VGPRs and ran 516-525 / 616-620 us against 513)
-  if (first_after_ss0 && c.k1_records && c.d_srec) kern = short_rows ? k_lcc_step<3, 1> : k_lcc_step<4, 1>;
-  else if (!first_after_ss0) kern = short_rows ? k_lcc_step<3, 2> : k_lcc_step<4, 2>;
+  // records and codes: the specialised instantiation (no spills at 6 waves per SIMD; budgets for 7 / 8 waves
+  // spilled 13 / 31 VGPRs and ran 516-525 / 616-620 us against 513)
+  if (first_after_ss0 && c.k1_records && c.d_srec) kern = short_rows ? k_lcc_step<3, true> : k_lcc_step<4, true>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
