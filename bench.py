@@ -71,6 +71,48 @@ def host_cpu_share():
     return share, info
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_launch_cmd(n, argv, port):
+    """The N-rank launch of this script (one process per GPU), as the driver itself runs it for N > 1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def rank_launch_env():
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # (dmabuf IPC only: RCCL needs it)
+    return env
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher: start N ranks as a child torch.distributed.run (this process
+    never touches the GPU -- torch.cuda.device_count() does not initialise it -- and never execs), wait for them and
+    return their exit status; rank 0 prints the JSON line to the shared stdout."""
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < n:
+        log(f"bench.py --gpus {n}: only {have} GPU(s) visible to this process; a {n}-GPU line cannot be measured "
+            f"here (no line printed)")
+        return 2
+    cmd = rank_launch_cmd(n, argv, free_port())
+    log("launching: " + " ".join(cmd))
+    return subprocess.run(cmd, env=rank_launch_env()).returncode
+
+
+def spread(vals):
+    vals = [float(v) for v in vals]
+    mean = sum(vals) / len(vals) if vals else 0.0
+    return {"max": max(vals), "mean": round(mean, 6), "min": min(vals),
+            "max_over_mean": round(max(vals) / mean, 4) if mean else None}
+
+
 def main():
     import faulthandler
     faulthandler.enable()  # a fatal signal prints the Python stack
@@ -102,6 +144,12 @@ def main():
                          "tests/golden/rmat_s27_p8_cycle4_hash256.json")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"bench.py: launched with WORLD_SIZE={env_world} but --gpus {args.gpus}; the line would mislabel the run")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -110,6 +158,9 @@ def main():
     if sharded:
         import torch
         import torch.distributed as dist
+        if world > 1 and local_rank >= torch.cuda.device_count():
+            log(f"bench.py rank {rank}: local rank {local_rank} but only {torch.cuda.device_count()} GPU(s) visible")
+            return 2
         torch.cuda.set_device(local_rank)
         dist.init_process_group(backend="nccl")
 
@@ -209,6 +260,26 @@ def main():
                                "of vertices / edges / subgraphs) and its counters against the oracle's"}
             if diffs:
                 invalid.append("GPU search differs from the oracle's S=28 fixture: " + "; ".join(diffs[:4]))
+
+    # N GPUs: the communicator as the library sees it, and every shard's share of the search
+    shards = None
+    if sharded:
+        info = m.comm_info()
+        mine = {k: s0[k] for k in ("shard_entries", "shard_rows", "shard_hub_entries", "shard_hubs_controlled",
+                                   "shard_ss0_entries", "shard_ss0_survivors", "shard_sharded_ms", "comm_calls",
+                                   "comm_bytes", "comm_seconds", "lcc_first_kernel_ms")}
+        mine.update(info)
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        shards = {"transport": info["transport"], "comm_ranks": info["comm_ranks"], "nshards": info["nshards"],
+                  "per_shard": {k: spread([e[k] for e in every])
+                                for k in ("shard_entries", "shard_rows", "shard_ss0_entries", "shard_sharded_ms",
+                                          "lcc_first_kernel_ms", "comm_bytes", "comm_seconds")},
+                  "comm_calls_per_search": s0["comm_calls"], "replica_rows": s0["replica_rows"],
+                  "replica_entries": s0["replica_entries"]}
+        if any(e["comm_ranks"] != world or e["nshards"] != world for e in every):
+            invalid.append(f"communicator ranks {[e['comm_ranks'] for e in every]} / shards "
+                           f"{[e['nshards'] for e in every]} differ from the {world} launched ranks")
 
     lay = None
     if not sharded:
@@ -443,6 +514,7 @@ def main():
         "fixture": fixture,
         "c3_config": c3,
         "nlcc_config": nlcc,
+        "shards": shards,
         # one-time work outside the timed region (the reference's graph load + label init analogue)
         "setup_s": setup,
     }

@@ -17,8 +17,9 @@ from . import _abi
 
 __all__ = ["Graph", "rmat_graph", "rmat_matcher", "rmat_shard_matcher", "mt19937_jump_outputs", "rmat_edges",
            "pattern_summary", "write_graph", "read_graph", "PatternMatcher", "ShardedPatternMatcher", "partition_edges",
-           "comm_unique_id", "run_beta_local_shards", "run_rmat_local_shards", "run_rmat_local_shards_each",
-           "TorchHostComm", "PMError"]
+           "comm_unique_id", "run_beta_local_shards", "run_beta_local_shards_each", "run_rmat_local_shards",
+           "run_rmat_local_shards_each", "read_graph_shard", "graph_partitions", "device_count", "TorchHostComm",
+           "PMError"]
 
 DEFAULT_HUB_THRESHOLD = 1048576  # generate_rmat.cpp:106
 
@@ -215,6 +216,57 @@ def run_beta_local_shards(graph, pattern_dir, nshards, result_dir="", max_iterat
     return st.as_dict()
 
 
+def run_beta_local_shards_each(graph, pattern_dir, nshards, result_dir="", max_iterations=0, device=0, labels=None,
+                               label_prefix=None, repeats=1):
+    """run_beta_local_shards with -v label files (label_prefix, parsed on the device once) or labels, the search
+    repeated `repeats` times (result files from the first) and every shard's statistics (pm_run_beta_local_shards2:
+    the drop-in executable's mode for a P-partition graph on fewer GPUs than P)."""
+    desc = _abi.GraphDesc(graph.n, graph.off.ctypes.data, graph.col.ctypes.data, int(graph.symmetric), graph.nranks,
+                          graph.hub_threshold)
+    lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.uint64)
+    if result_dir:
+        os.makedirs(result_dir, exist_ok=True)
+    st = (_abi.RunStats * nshards)()
+    rc = _lib().pm_run_beta_local_shards2(ctypes.byref(desc), pattern_dir.encode(), device, nshards,
+                                          None if lab is None else lab.ctypes.data,
+                                          None if label_prefix is None else os.fspath(label_prefix).encode(),
+                                          result_dir.encode(), max_iterations, repeats, st)
+    if rc != 0:
+        raise _err()
+    return [s.as_dict() for s in st]
+
+
+def graph_partitions(base):
+    """P of the graph files <base>_<r>_of_<P>."""
+    p = _lib().pm_graph_partitions(os.fspath(base).encode())
+    if p < 0:
+        raise _err()
+    return p
+
+
+def read_graph_shard(base, nshards, shard):
+    """Shard `shard` of `nshards` read from the graph files (pm_read_graph_shard): (off[n+1] by id -- the owned
+    rows whole, a delegate's entries whose target this shard owns, other rows empty --, col, degree[n] global,
+    info dict with symmetric / nranks / hub_threshold)."""
+    lib = _lib()
+    off_p, col_p, deg_p, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    sym, nr, hub = ctypes.c_int(), ctypes.c_uint32(), ctypes.c_uint64()
+    if lib.pm_read_graph_shard(os.fspath(base).encode(), nshards, shard, ctypes.byref(off_p), ctypes.byref(col_p),
+                               ctypes.byref(deg_p), ctypes.byref(n), ctypes.byref(sym), ctypes.byref(nr),
+                               ctypes.byref(hub)) != 0:
+        raise _err()
+    nv = n.value
+    deg = np.ctypeslib.as_array(ctypes.cast(deg_p, ctypes.POINTER(ctypes.c_uint32)), shape=(max(nv, 1),))[:nv].copy()
+    lib.pm_free_host(deg_p)
+    off, col = _take_host_csr(off_p, col_p, nv)
+    return off, col, deg, {"symmetric": bool(sym.value), "nranks": nr.value, "hub_threshold": hub.value, "n": nv}
+
+
+def device_count():
+    """HIP devices visible to this process (0 without a GPU)."""
+    return int(_lib().pm_device_count())
+
+
 def run_rmat_local_shards(scale, p_gen, pattern_dir, nshards, result_dir="", max_iterations=0, device=0, nranks=1,
                           hub_threshold=DEFAULT_HUB_THRESHOLD):
     """The sharded search over the R-MAT graph with `nshards` shards driven by threads of this process
@@ -352,6 +404,16 @@ class PatternMatcher:
         loop converts after the clock stops)."""
         self._check(_lib().pm_run_beta(self._ctx, b"", max_iterations, ctypes.byref(st)))
         return st
+
+    def comm_info(self):
+        """This context's place in its search: {"nshards", "shard", "comm_ranks" (the communicator's own count,
+        RCCL: ncclCommCount), "transport"} (pm_comm_info)."""
+        ns, sh = ctypes.c_uint32(), ctypes.c_uint32()
+        cr, tr = ctypes.c_int32(), ctypes.c_int32()
+        self._check(_lib().pm_comm_info(self._ctx, ctypes.byref(ns), ctypes.byref(sh), ctypes.byref(cr),
+                                        ctypes.byref(tr)))
+        return {"nshards": ns.value, "shard": sh.value, "comm_ranks": cr.value,
+                "transport": _abi.TRANSPORTS.get(tr.value, str(tr.value))}
 
     def tpub_census(self, deferred_reset=False):
         """(nonzero T_pub entries of buffer 0, of buffer 1, positions nonzero in either buffer outside the

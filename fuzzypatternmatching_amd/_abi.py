@@ -179,7 +179,18 @@ SIGNATURES = [
                                                ctypes.POINTER(ctypes.c_int)]),
     ("pm_create_edge_list", c_vp, [c_vp, c_u32, ctypes.c_int, c_char_p, ctypes.c_int, c_u32, c_u64,
                                    ctypes.POINTER(ctypes.c_double)]),
+    ("pm_run_beta_local_shards2", ctypes.c_int, [ctypes.POINTER(GraphDesc), c_char_p, ctypes.c_int, c_u32, c_vp,
+                                                 c_char_p, c_char_p, c_u64, c_u32, ctypes.POINTER(RunStats)]),
+    ("pm_graph_partitions", ctypes.c_int, [c_char_p]),
+    ("pm_read_graph_shard", ctypes.c_int, [c_char_p, c_u32, c_u32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                                           ctypes.POINTER(c_vp), ctypes.POINTER(c_u64), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(c_u32), ctypes.POINTER(c_u64)]),
+    ("pm_device_count", ctypes.c_int, []),
+    ("pm_comm_info", ctypes.c_int, [c_vp, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(ctypes.c_int32),
+                                    ctypes.POINTER(ctypes.c_int32)]),
 ]
+
+TRANSPORTS = {0: "none", 1: "rccl", 2: "host", 3: "threads"}  # PM_TRANSPORT_* (include/pm_abi.h)
 
 _lib = None
 

@@ -361,6 +361,109 @@ inline Csr read_graph_files(const std::string& base, uint32_t* nranks_out = null
   return g;
 }
 
+// P of the graph files of `base` (the first <base>_0_of_<P> found), 0 when there are none.
+inline uint32_t graph_file_partitions(const std::string& base) {
+  for (uint64_t p = 1; p <= 4096; ++p)
+    if (file_exists(graph_file_name(base, 0, p))) return static_cast<uint32_t>(p);
+  return 0;
+}
+
+// One shard of a sharded search, read from the graph files.  The reference's rank r opens only
+// <base>_<r>_of_<P> (distributed_db.hpp:353-357, beta.cpp:209-223) because its files ARE the partition; the
+// search's partition here is owner = id % nshards with a delegate's row (global degree >= the hub threshold)
+// split by target owner (delegate_partitioned_graph.ipp:1402-1648), which the files (a delegate's whole row at
+// its controller) do not hold as such.  So every file's row index and degrees are read (16 B per row: the
+// global degrees every shard needs for labels and the delegate rule), and only the entries this shard holds
+// are copied out of the mappings: owned rows whole, delegate rows filtered by target.  nshards may differ
+// from the files' P.
+struct ShardCsr {
+  uint64_t n = 0;
+  std::vector<uint64_t> off;     // n + 1 by id: the rows held here, every other row empty
+  std::vector<uint32_t> col;     // their entries, sorted within each row (>= 1 element)
+  std::vector<uint32_t> degree;  // n global degrees
+  bool symmetric = false;
+  uint32_t nranks = 1;           // P of the files (result-file attribution)
+  uint64_t hub_threshold = 0;
+};
+
+inline ShardCsr read_graph_shard(const std::string& base, uint32_t nshards, uint32_t shard,
+                                 unsigned threads = hw_threads()) {
+  if (nshards == 0 || shard >= nshards) throw std::runtime_error("read_graph_shard: bad shard index");
+  const uint32_t P = graph_file_partitions(base);
+  if (P == 0) throw std::runtime_error("no graph files found for base " + base);
+  ShardCsr s;
+  s.nranks = P;
+  std::vector<std::unique_ptr<MappedGraphFile>> files;
+  for (uint32_t r = 0; r < P; ++r) {
+    files.emplace_back(new MappedGraphFile(graph_file_name(base, r, P)));
+    const GraphFileHeader& h = files.back()->header();
+    if (r == 0) {
+      s.n = h.n;
+      s.symmetric = h.symmetric != 0;
+      s.hub_threshold = h.hub_threshold;
+    } else if (h.n != s.n || h.nranks != P) {
+      throw std::runtime_error("graph file " + graph_file_name(base, r, P) + " belongs to another graph");
+    }
+  }
+  const uint64_t n = s.n;
+  // global degrees and, for every row this shard may hold, where its entries lie: file << 48 | entry index
+  s.degree.assign(n, 0);
+  std::vector<uint64_t> loc(n, ~uint64_t(0));
+  for (uint32_t r = 0; r < P; ++r) {
+    const GraphFileHeader& h = files[r]->header();
+    const uint64_t* rows = files[r]->rows();
+    const uint64_t* d = files[r]->degrees();
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < h.nrows; ++i) {
+      const uint64_t v = rows[i];
+      if (v >= n) throw std::runtime_error("graph file row id out of range");
+      if (d[i] > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
+      if (pos + d[i] > h.nnz) throw std::runtime_error("truncated graph file");
+      s.degree[v] = static_cast<uint32_t>(d[i]);
+      loc[v] = (uint64_t(r) << 48) | pos;
+      pos += d[i];
+    }
+  }
+  const bool split = nshards > 1;
+  auto is_hub = [&](uint64_t v) { return split && s.degree[v] >= s.hub_threshold; };
+  auto row = [&](uint64_t v) { return files[loc[v] >> 48]->cols() + (loc[v] & ((uint64_t(1) << 48) - 1)); };
+  // entries held per row: an owned row whole, a delegate row's entries whose target this shard owns
+  std::vector<uint64_t> held(n, 0);
+  parallel_for(n, threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t v = b; v < e; ++v) {
+      if (!s.degree[v]) continue;
+      if (is_hub(v)) {
+        const uint32_t* c = row(v);
+        uint64_t k = 0;
+        for (uint64_t j = 0; j < s.degree[v]; ++j) k += c[j] % nshards == shard;
+        held[v] = k;
+      } else if (v % nshards == shard) {
+        held[v] = s.degree[v];
+      }
+    }
+  });
+  s.off.assign(n + 1, 0);
+  for (uint64_t v = 0; v < n; ++v) s.off[v + 1] = s.off[v] + held[v];
+  held.clear();
+  held.shrink_to_fit();
+  s.col.resize(std::max<uint64_t>(s.off[n], 1));
+  if (!s.off[n]) s.col[0] = 0;
+  parallel_for(n, threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t v = b; v < e; ++v) {
+      if (s.off[v + 1] == s.off[v]) continue;
+      const uint32_t* c = row(v);
+      uint32_t* out = s.col.data() + s.off[v];
+      if (is_hub(v)) {
+        for (uint64_t j = 0; j < s.degree[v]; ++j)
+          if (c[j] % nshards == shard) *out++ = c[j];
+      } else {
+        std::memcpy(out, c, uint64_t(s.degree[v]) * sizeof(uint32_t));
+      }
+    }
+  });
+  return s;
+}
+
 // ---------------------------------------------------------------------------
 // Labels.
 // Default: label = ceil(log2(degree + 1)) (vertex_data_db_degree.hpp:109),

@@ -40,7 +40,9 @@ void gather_floor_forget(const void* owner);  // (diagnostics: the gather-floor 
 
 namespace pm {
 
-static std::string g_last_error;
+// per thread: the shards of one process (pm_run_beta_local_shards, the CLI's one-thread-per-GPU mode) fail
+// independently
+static thread_local std::string g_last_error;
 
 static void mkdir_p(const std::string& path) {
   std::string cur;
@@ -143,6 +145,8 @@ struct PinnedRange {
   PinnedRange& operator=(const PinnedRange&) = delete;
 };
 
+static void destroy_ctx(pm_ctx* c);
+
 static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int device) {
   std::unique_ptr<Comm> comm(in.comm);
   // a device-resident input the caller handed over (col_release) is freed as soon as it is copied
@@ -158,7 +162,8 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (in.nshards == 0 || in.shard >= in.nshards) throw std::runtime_error("pm_create: bad shard index");
   if (in.nshards > 1 && !comm) throw std::runtime_error("pm_create: sharded context without a communicator");
   require_gfx950(device);
-  auto c = std::make_unique<pm_ctx>();
+  // a construction that throws releases what it allocated (device buffers, stream, communicator)
+  std::unique_ptr<pm_ctx, void (*)(pm_ctx*)> c(new pm_ctx(), destroy_ctx);
   c->device = device;
   PM_HIP_CHECK(hipSetDevice(device));
   PM_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -177,105 +182,117 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   std::vector<uint32_t> tin_col;
   const uint64_t* soff = in.off;
   const uint32_t* scol = in.col;
-  if (!c->symmetric) {
-    if (in.nshards > 1) throw std::runtime_error("directed input graphs are supported on one shard only");
-    if (in.in_off && in.in_col) {
-      soff = in.in_off;
-      scol = in.in_col;
-    } else {
-      if (in.col_on_device) throw std::runtime_error("directed device-resident graphs need their in-rows");
-      transpose_csr(c->n, in.off, in.col, tin_off, tin_col);
-      soff = tin_off.data();
-      scol = tin_col.data();
-    }
-    c->rdeg_host.resize(c->n);
-    for (uint64_t v = 0; v < c->n; ++v) c->rdeg_host[v] = static_cast<uint32_t>(soff[v + 1] - soff[v]);
-  }
-  c->pattern = load_pattern_dir(pattern_dir);
-  const PatternGraph& pg = c->pattern.graph;
-  if (pg.diameter == 0) throw std::runtime_error("pattern_stat: diameter is 0 or missing");
-  for (int t = 0; t < kMaxTemplateVertices; ++t) c->pa.adj[t] = pg.adj[t];
-  c->pa.K = static_cast<int32_t>(pg.vertex_data.size());
-  for (int t = 0; t < c->pa.K; ++t) c->pa.plabel[t] = pg.vertex_data[t];
-  // a label of more than two template vertices: its 2-bit code cannot carry T_pub (tpub_code)
-  for (int t = 0; t < c->pa.K; ++t) {
-    int k = 0;
-    for (int u = 0; u < c->pa.K; ++u) k += c->pa.plabel[u] == c->pa.plabel[t];
-    if (k > 2) c->xcode_wide = true;
-  }
+  size_t arena = 0;
   bool any_sv = false;
-  for (size_t pl = 0; pl < c->pattern.lines.size(); ++pl) {
-    const auto& l = c->pattern.lines[pl];
-    if (!l.selected_vertices) continue;
-    any_sv = true;
-    if (pl >= 4 || l.valid_cycle)  // the reference applies it in nem_1 path checks only
-      throw std::runtime_error("pattern_nlc selected_vertices=1 is supported on path lines (index < 4, valid_cycle 0)");
+  std::string build_err;
+  try {
+    if (!c->symmetric) {
+      if (in.nshards > 1) throw std::runtime_error("directed input graphs are supported on one shard only");
+      if (in.in_off && in.in_col) {
+        soff = in.in_off;
+        scol = in.in_col;
+      } else {
+        if (in.col_on_device) throw std::runtime_error("directed device-resident graphs need their in-rows");
+        transpose_csr(c->n, in.off, in.col, tin_off, tin_col);
+        soff = tin_off.data();
+        scol = tin_col.data();
+      }
+      c->rdeg_host.resize(c->n);
+      for (uint64_t v = 0; v < c->n; ++v) c->rdeg_host[v] = static_cast<uint32_t>(soff[v + 1] - soff[v]);
+    }
+    c->pattern = load_pattern_dir(pattern_dir);
+    const PatternGraph& pg = c->pattern.graph;
+    if (pg.diameter == 0) throw std::runtime_error("pattern_stat: diameter is 0 or missing");
+    for (int t = 0; t < kMaxTemplateVertices; ++t) c->pa.adj[t] = pg.adj[t];
+    c->pa.K = static_cast<int32_t>(pg.vertex_data.size());
+    for (int t = 0; t < c->pa.K; ++t) c->pa.plabel[t] = pg.vertex_data[t];
+    // a label of more than two template vertices: its 2-bit code cannot carry T_pub (tpub_code)
+    for (int t = 0; t < c->pa.K; ++t) {
+      int k = 0;
+      for (int u = 0; u < c->pa.K; ++u) k += c->pa.plabel[u] == c->pa.plabel[t];
+      if (k > 2) c->xcode_wide = true;
+    }
+    any_sv = false;
+    for (size_t pl = 0; pl < c->pattern.lines.size(); ++pl) {
+      const auto& l = c->pattern.lines[pl];
+      if (!l.selected_vertices) continue;
+      any_sv = true;
+      if (pl >= 4 || l.valid_cycle)  // the reference applies it in nem_1 path checks only
+        throw std::runtime_error("pattern_nlc selected_vertices=1 is supported on path lines (index < 4, valid_cycle 0)");
+    }
+    // global degrees (labels, hubs, layout order) and the lengths of the rows held here
+    c->deg_host.resize(c->n);
+    if (in.gdeg) c->ldeg_host.reserve(c->n);
+    for (uint64_t v = 0; v < c->n; ++v) {
+      const uint64_t d = in.gdeg ? in.gdeg[v] : in.off[v + 1] - in.off[v];
+      if (d > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
+      const uint64_t ld = in.off[v + 1] - in.off[v];
+      // a shard holds the whole rows it owns, and of a delegate (degree >= -d) the entries whose target it owns
+      if (in.gdeg && ld && (d >= c->hub_threshold && c->nshards > 1 ? ld > d
+                                                                     : (ld != d || v % c->nshards != c->shard)))
+        throw std::runtime_error("shard rows must be the owned rows (v % nshards == shard) with their full degree, "
+                                 "and delegate rows (degree >= hub threshold) split by target owner");
+      c->deg_host[v] = static_cast<uint32_t>(d);
+      if (d >= c->hub_threshold) c->hubs_host.push_back(v);
+      if (in.gdeg) c->ldeg_host.push_back(static_cast<uint32_t>(ld));
+      c->held_rows += ld != 0;
+      if (ld && d >= c->hub_threshold && c->nshards > 1) c->held_hub_entries += ld;
+    }
+    c->split_hubs = c->nshards > 1 && !c->hubs_host.empty();
+    for (uint64_t j = c->shard; c->split_hubs && j < c->hubs_host.size(); j += c->nshards)
+      c->hub_area += c->deg_host[c->hubs_host[j]];
+    // device graph + state; padded slot count of the rows scanned here (label independent)
+    c->nq = 0;
+    for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(soff[v + 1] - soff[v]);
+    c->mcap = c->nq;
+    c->d_offp = dalloc<uint64_t>(c->n + 1);
+    c->d_offr = dalloc<uint64_t>(c->n + 1);
+    // slot buffers carry kTileEntries entries of tail padding (superstep-0 tile loads read whole tiles)
+    // dense superstep-0 M region behind the tail padding (both buffers: relayout swaps them)
+    if (c->symmetric && c->nq)
+      c->dcap = std::min<uint64_t>(0xFFFFFFF0ull, std::max<uint64_t>(uint64_t(1) << 16, c->nq / 8));
+    c->dbase = c->nq + kTileEntries;
+    c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
+    c->d_perm = dalloc<uint32_t>(c->n);
+    c->d_pos = dalloc<uint32_t>(c->n);
+    if (!c->hubs_host.empty()) {
+      c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
+      PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    }
+    c->d_tpub[0] = dalloc<uint16_t>(c->n);
+    c->d_tpub[1] = dalloc<uint16_t>(c->n);
+    c->d_tst = dalloc<uint16_t>(c->n);
+    c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
+    c->d_mlen = dalloc<uint32_t>(c->n);
+    c->d_malive = dalloc<uint32_t>(c->n);
+    c->d_slist = dalloc<uint32_t>(c->n);
+    c->d_smask[0] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
+    c->d_smask[1] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
+    c->d_sources = dalloc<uint32_t>(c->n);
+    c->d_nS = dalloc<uint32_t>(2);  // [1]: long-row stamp (launch_compact_rows)
+    PM_HIP_CHECK(hipMemset(c->d_nS, 0, 2 * sizeof(uint32_t)));
+    c->d_flags = dalloc<uint32_t>(4);
+    c->d_tsm = dalloc<uint8_t>(c->n);
+    c->d_tcode = dalloc<uint32_t>((c->n + 15) / 16 + 1);
+    if (c->nranks > 64) throw std::runtime_error("more than 64 ranks for result-file attribution");
+    c->d_part = dalloc<uint64_t>(uint64_t(kPartGridMax) * slot_words(*c));
+    size_t free_b = 0, total_b = 0;
+    PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
+    if (in.inprocess_shards > 1)  // in-process shard groups share one device
+      arena = std::min<size_t>(arena, std::max<size_t>(size_t(1) << 30, free_b / (2 * in.inprocess_shards)));
+    arena = std::max<size_t>(arena, size_t(64) << 20);
+  } catch (const std::exception& e) {
+    build_err = e.what();
+    arena = 0;
   }
-  // global degrees (labels, hubs, layout order) and the lengths of the rows held here
-  c->deg_host.resize(c->n);
-  if (in.gdeg) c->ldeg_host.reserve(c->n);
-  for (uint64_t v = 0; v < c->n; ++v) {
-    const uint64_t d = in.gdeg ? in.gdeg[v] : in.off[v + 1] - in.off[v];
-    if (d > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
-    const uint64_t ld = in.off[v + 1] - in.off[v];
-    // a shard holds the whole rows it owns, and of a delegate (degree >= -d) the entries whose target it owns
-    if (in.gdeg && ld && (d >= c->hub_threshold && c->nshards > 1 ? ld > d
-                                                                   : (ld != d || v % c->nshards != c->shard)))
-      throw std::runtime_error("shard rows must be the owned rows (v % nshards == shard) with their full degree, "
-                               "and delegate rows (degree >= hub threshold) split by target owner");
-    c->deg_host[v] = static_cast<uint32_t>(d);
-    if (d >= c->hub_threshold) c->hubs_host.push_back(v);
-    if (in.gdeg) c->ldeg_host.push_back(static_cast<uint32_t>(ld));
-    c->held_rows += ld != 0;
-    if (ld && d >= c->hub_threshold && c->nshards > 1) c->held_hub_entries += ld;
-  }
-  c->split_hubs = c->nshards > 1 && !c->hubs_host.empty();
-  for (uint64_t j = c->shard; c->split_hubs && j < c->hubs_host.size(); j += c->nshards)
-    c->hub_area += c->deg_host[c->hubs_host[j]];
-  // device graph + state; padded slot count of the rows scanned here (label independent)
-  c->nq = 0;
-  for (uint64_t v = 0; v < c->n; ++v) c->nq += padded_degree(soff[v + 1] - soff[v]);
-  c->mcap = c->nq;
-  c->d_offp = dalloc<uint64_t>(c->n + 1);
-  c->d_offr = dalloc<uint64_t>(c->n + 1);
-  // slot buffers carry kTileEntries entries of tail padding (superstep-0 tile loads read whole tiles)
-  // dense superstep-0 M region behind the tail padding (both buffers: relayout swaps them)
-  if (c->symmetric && c->nq)
-    c->dcap = std::min<uint64_t>(0xFFFFFFF0ull, std::max<uint64_t>(uint64_t(1) << 16, c->nq / 8));
-  c->dbase = c->nq + kTileEntries;
-  c->d_colp = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
-  c->d_perm = dalloc<uint32_t>(c->n);
-  c->d_pos = dalloc<uint32_t>(c->n);
-  if (!c->hubs_host.empty()) {
-    c->d_hubs = dalloc<uint64_t>(c->hubs_host.size());
-    PM_HIP_CHECK(hipMemcpy(c->d_hubs, c->hubs_host.data(), c->hubs_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-  }
-  c->d_tpub[0] = dalloc<uint16_t>(c->n);
-  c->d_tpub[1] = dalloc<uint16_t>(c->n);
-  c->d_tst = dalloc<uint16_t>(c->n);
-  c->d_mcol = dalloc<uint32_t>(c->nq + kTileEntries + c->dcap + c->hub_area);
-  c->d_mlen = dalloc<uint32_t>(c->n);
-  c->d_malive = dalloc<uint32_t>(c->n);
-  c->d_slist = dalloc<uint32_t>(c->n);
-  c->d_smask[0] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
-  c->d_smask[1] = dalloc<uint64_t>((c->n + 63) / 64 + 1);
-  c->d_sources = dalloc<uint32_t>(c->n);
-  c->d_nS = dalloc<uint32_t>(2);  // [1]: long-row stamp (launch_compact_rows)
-  PM_HIP_CHECK(hipMemset(c->d_nS, 0, 2 * sizeof(uint32_t)));
-  c->d_flags = dalloc<uint32_t>(4);
-  c->d_tsm = dalloc<uint8_t>(c->n);
-  c->d_tcode = dalloc<uint32_t>((c->n + 15) / 16 + 1);
-  if (c->nranks > 64) throw std::runtime_error("more than 64 ranks for result-file attribution");
-  c->d_part = dalloc<uint64_t>(uint64_t(kPartGridMax) * slot_words(*c));
-  size_t free_b = 0, total_b = 0;
-  PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-  size_t arena = std::min<size_t>(free_b / 2, size_t(32) << 30);
-  if (in.inprocess_shards > 1)  // in-process shard groups share one device
-    arena = std::min<size_t>(arena, std::max<size_t>(size_t(1) << 30, free_b / (2 * in.inprocess_shards)));
-  arena = std::max<size_t>(arena, size_t(64) << 20);
   // one size on every shard: the replicated lines' walk storage and TDS chunk caps come from it, and a line
   // that overflowed on some shards only would send those into collectives the others never make
+  // -- and construction is collective: a shard that failed above still takes part (arena 0), so the others
+  // are not left in a collective it never makes, and every shard then fails
   arena = static_cast<size_t>(shard_agree_min(*c, arena));
+  if (!build_err.empty()) throw std::runtime_error(build_err);
+  if (arena == 0) throw std::runtime_error("another shard failed while building its context");
   c->arena.base = dalloc<char>(arena);
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
@@ -287,6 +304,7 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (const char* e = std::getenv("PM_HASH_SLOTS")) c->hash_slots = std::strtoull(e, nullptr, 10);
   if (const char* e = std::getenv("PM_HANDOFF")) c->handoff_ss = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("PM_DEBUG_NOGROW_SHARD")) c->nogrow_shard = std::strtoll(e, nullptr, 10);
+  if (const char* e = std::getenv("PM_DEBUG_OVERFLOW_SHARD")) c->overflow_shard = std::strtoll(e, nullptr, 10);
   // diagnostics: PM_FORCE_PULL=1 keeps the pull form in every LCC call (an
   // asymmetric M then aborts the search: tests use it to find such inputs)
   if (const char* e = std::getenv("PM_FORCE_PULL")) c->force_pull = std::string(e) == "1" && c->symmetric;
@@ -1279,6 +1297,7 @@ int pm_debug_rccl_selftest(int device, uint64_t bytes, int op) {
 pm_ctx* pm_create_shard(const pm_shard_desc* d, const char* pattern_dir, int device, const uint8_t* unique_id) {
   try {
     if (!d || !unique_id) throw std::runtime_error("pm_create_shard: null argument");
+    pm::require_gfx950(device);
     PM_HIP_CHECK(hipSetDevice(device));
     pm::CtxInput in;
     in.n = d->n;
@@ -1306,6 +1325,7 @@ pm_ctx* pm_create_shard_host_comm(const pm_shard_desc* d, const char* pattern_di
     if (!d || !comm) throw std::runtime_error("pm_create_shard_host_comm: null argument");
     if (comm->nshards != d->nshards || comm->shard != d->shard)
       throw std::runtime_error("pm_create_shard_host_comm: communicator and shard disagree on nshards / shard");
+    pm::require_gfx950(device);
     PM_HIP_CHECK(hipSetDevice(device));
     pm::CtxInput in;
     in.n = d->n;
@@ -1350,36 +1370,42 @@ static void pm_segv_trace(int sig) {
   raise(sig);
 }
 
-int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, int device, uint32_t nshards,
-                             const uint64_t* labels, const char* result_dir, uint64_t max_iterations,
-                             pm_run_stats* out) {
+int pm_run_beta_local_shards2(const pm_graph_desc* g, const char* pattern_dir, int device, uint32_t nshards,
+                              const uint64_t* labels, const char* label_prefix, const char* result_dir,
+                              uint64_t max_iterations, uint32_t repeats, pm_run_stats* per_shard) {
   try {
     if (!g || !g->off || !g->col) throw std::runtime_error("pm_run_beta_local_shards: null graph");
     if (nshards == 0 || nshards > 64) throw std::runtime_error("pm_run_beta_local_shards: 1..64 shards");
+    pm::require_gfx950(device);
     const uint64_t n = g->n;
     std::vector<uint32_t> gdeg(n);
-    for (uint64_t v = 0; v < n; ++v) gdeg[v] = static_cast<uint32_t>(g->off[v + 1] - g->off[v]);
-    // owner rule: shard q holds the rows of ids v % nshards == q; a delegate's row (degree >= the hub
-    // threshold) is split by target owner: shard q holds its entries u with u % nshards == q
-    // (delegate_partitioned_graph.ipp:818-969, 1402-1648)
-    std::vector<std::vector<uint64_t>> offs(nshards, std::vector<uint64_t>(n + 1, 0));
-    std::vector<std::vector<uint32_t>> cols(nshards);
-    for (uint32_t q = 0; q < nshards; ++q) {
-      for (uint64_t v = 0; v < n; ++v) {
-        uint64_t k = 0;
-        if (nshards > 1 && gdeg[v] >= g->hub_threshold) {
-          for (uint64_t e = g->off[v]; e < g->off[v + 1]; ++e)
-            if (g->col[e] % nshards == q) {
-              cols[q].push_back(g->col[e]);
-              ++k;
-            }
-        } else if (v % nshards == q) {
-          cols[q].insert(cols[q].end(), g->col + g->off[v], g->col + g->off[v + 1]);
-          k = gdeg[v];
-        }
-        offs[q][v + 1] = offs[q][v] + k;
+    for (uint64_t v = 0; v < n; ++v) {
+      const uint64_t d = g->off[v + 1] - g->off[v];
+      if (d > 0xFFFFFFFFull) throw std::runtime_error("degree above 2^32");
+      gdeg[v] = static_cast<uint32_t>(d);
+    }
+    // -v files: parsed on the device once, the same labels for every shard
+    std::vector<uint64_t> file_labels;
+    if (label_prefix) {
+      PM_HIP_CHECK(hipSetDevice(device));
+      const std::vector<std::string> files = pm::vertex_label_files(label_prefix);
+      hipStream_t s = nullptr;
+      uint64_t* d_labels = nullptr;
+      try {
+        PM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        PM_HIP_CHECK(hipMalloc(&d_labels, std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
+        pm::labels_from_files_device(files, n, d_labels, s);
+        file_labels.resize(n);
+        if (n) PM_HIP_CHECK(hipMemcpyAsync(file_labels.data(), d_labels, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        PM_HIP_CHECK(hipStreamSynchronize(s));
+      } catch (...) {
+        if (d_labels) (void)hipFree(d_labels);
+        if (s) (void)hipStreamDestroy(s);
+        throw;
       }
-      if (cols[q].empty()) cols[q].push_back(0);
+      (void)hipFree(d_labels);
+      (void)hipStreamDestroy(s);
+      labels = file_labels.data();
     }
     if (std::getenv("PM_SEGV_TRACE")) signal(SIGSEGV, pm_segv_trace);
     pm::ThreadGroup grp(static_cast<int>(nshards));
@@ -1387,14 +1413,39 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
     std::vector<std::string> errs(nshards);
     const std::string dir = result_dir ? result_dir : "";
     auto work = [&](uint32_t q) {
-      std::unique_lock<std::mutex> dev(grp.device);
       pm_ctx* ctx = nullptr;
       try {
+        // this shard's rows, built on the host by every shard thread at once: shard q holds the rows of ids
+        // v % nshards == q; a delegate's row (degree >= the hub threshold) is split by target owner -- shard q
+        // holds its entries u with u % nshards == q (delegate_partitioned_graph.ipp:818-969, 1402-1648)
+        std::vector<uint64_t> off(n + 1, 0);
+        const bool split = nshards > 1;
+        for (uint64_t v = 0; v < n; ++v) {
+          uint64_t k = 0;
+          if (split && gdeg[v] >= g->hub_threshold) {
+            for (uint64_t e = g->off[v]; e < g->off[v + 1]; ++e) k += g->col[e] % nshards == q;
+          } else if (v % nshards == q) {
+            k = gdeg[v];
+          }
+          off[v + 1] = off[v] + k;
+        }
+        std::vector<uint32_t> col(std::max<uint64_t>(off[n], 1), 0);
+        for (uint64_t v = 0; v < n; ++v) {
+          if (off[v + 1] == off[v]) continue;
+          uint32_t* out = col.data() + off[v];
+          if (split && gdeg[v] >= g->hub_threshold) {
+            for (uint64_t e = g->off[v]; e < g->off[v + 1]; ++e)
+              if (g->col[e] % nshards == q) *out++ = g->col[e];
+          } else {
+            std::copy(g->col + g->off[v], g->col + g->off[v + 1], out);
+          }
+        }
+        std::unique_lock<std::mutex> dev(grp.device);
         PM_HIP_CHECK(hipSetDevice(device));
         pm::CtxInput in;
         in.n = n;
-        in.off = offs[q].data();
-        in.col = cols[q].data();
+        in.off = off.data();
+        in.col = col.data();
         in.gdeg = gdeg.data();
         in.symmetric = g->symmetric != 0;
         in.nranks = g->nranks;
@@ -1404,27 +1455,49 @@ int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, in
         in.comm = pm::make_thread_comm(&grp, static_cast<int>(q));
         in.inprocess_shards = nshards;
         ctx = pm::create_ctx(in, pattern_dir, device);
+        std::vector<uint64_t>().swap(off);  // (the context holds its copy)
+        std::vector<uint32_t>().swap(col);
         if (labels) {
           ctx->labels_host.assign(labels, labels + n);
           pm::relayout(*ctx);
         }
-        pm::run_beta(*ctx, dir, max_iterations, &st[q]);
+        for (uint32_t r = 0; r < std::max<uint32_t>(repeats, 1); ++r)
+          pm::run_beta(*ctx, r == 0 ? dir : std::string(), max_iterations, &st[q]);
+        pm::destroy_ctx(ctx);  // (the device lock still held)
+        ctx = nullptr;
       } catch (const std::exception& e) {
         errs[q] = e.what();
         grp.abort();
       }
-      if (ctx) pm::destroy_ctx(ctx);
+      if (ctx) {
+        std::lock_guard<std::mutex> dev(grp.device);
+        pm::destroy_ctx(ctx);
+      }
     };
     std::vector<std::thread> pool;
     for (uint32_t q = 0; q < nshards; ++q) pool.emplace_back(work, q);
     for (auto& t : pool) t.join();
     throw_shard_errors(errs);
-    if (out) *out = st[0];
+    if (per_shard) std::copy(st.begin(), st.end(), per_shard);
     return 0;
   } catch (const std::exception& e) {
     pm::g_last_error = e.what();
     return -1;
   }
+}
+
+int pm_run_beta_local_shards(const pm_graph_desc* g, const char* pattern_dir, int device, uint32_t nshards,
+                             const uint64_t* labels, const char* result_dir, uint64_t max_iterations,
+                             pm_run_stats* out) {
+  if (nshards == 0 || nshards > 64) {
+    pm::g_last_error = "pm_run_beta_local_shards: 1..64 shards";
+    return -1;
+  }
+  std::vector<pm_run_stats> st(nshards);
+  const int rc = pm_run_beta_local_shards2(g, pattern_dir, device, nshards, labels, nullptr, result_dir,
+                                           max_iterations, 1, st.data());
+  if (rc == 0 && out) *out = st[0];
+  return rc;
 }
 
 int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t stride, uint32_t** src, uint32_t** dst,
@@ -1893,6 +1966,72 @@ int pm_read_graph(const char* base, uint64_t** off, uint32_t** col, uint64_t* n,
     if (symmetric) *symmetric = g.symmetric ? 1 : 0;
     if (nranks) *nranks = p;
     if (hub_threshold) *hub_threshold = h;
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pm_graph_partitions(const char* base) {
+  try {
+    if (!base) throw std::runtime_error("pm_graph_partitions: null base");
+    const uint32_t p = pm::graph_file_partitions(base);
+    if (p == 0) throw std::runtime_error(std::string("no graph files found for base ") + base);
+    return static_cast<int>(p);
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pm_read_graph_shard(const char* base, uint32_t nshards, uint32_t shard, uint64_t** off, uint32_t** col,
+                        uint32_t** degree, uint64_t* n, int* symmetric, uint32_t* nranks, uint64_t* hub_threshold) {
+  try {
+    if (!base || !off || !col || !degree || !n) throw std::runtime_error("pm_read_graph_shard: null argument");
+    pm::ShardCsr s = pm::read_graph_shard(base, nshards, shard);
+    auto* o = static_cast<uint64_t*>(std::malloc(s.off.size() * sizeof(uint64_t)));
+    auto* c = static_cast<uint32_t*>(std::malloc(s.col.size() * sizeof(uint32_t)));
+    auto* d = static_cast<uint32_t*>(std::malloc(std::max<size_t>(1, s.degree.size()) * sizeof(uint32_t)));
+    if (!o || !c || !d) {
+      std::free(o);
+      std::free(c);
+      std::free(d);
+      throw std::runtime_error("pm_read_graph_shard: out of host memory");
+    }
+    std::memcpy(o, s.off.data(), s.off.size() * sizeof(uint64_t));
+    std::memcpy(c, s.col.data(), s.col.size() * sizeof(uint32_t));
+    std::memcpy(d, s.degree.data(), s.degree.size() * sizeof(uint32_t));
+    *off = o;
+    *col = c;
+    *degree = d;
+    *n = s.n;
+    if (symmetric) *symmetric = s.symmetric ? 1 : 0;
+    if (nranks) *nranks = s.nranks;
+    if (hub_threshold) *hub_threshold = s.hub_threshold;
+    return 0;
+  } catch (const std::exception& e) {
+    pm::g_last_error = e.what();
+    return -1;
+  }
+}
+
+int pm_device_count(void) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return count;
+}
+
+int pm_comm_info(const pm_ctx* ctx, uint32_t* nshards, uint32_t* shard, int32_t* comm_ranks, int32_t* transport) {
+  if (!ctx) return -1;
+  try {
+    if (nshards) *nshards = ctx->nshards;
+    if (shard) *shard = ctx->shard;
+    if (comm_ranks) *comm_ranks = ctx->comm ? ctx->comm->ranks() : 0;
+    if (transport) *transport = ctx->comm ? ctx->comm->transport() : PM_TRANSPORT_NONE;
     return 0;
   } catch (const std::exception& e) {
     pm::g_last_error = e.what();

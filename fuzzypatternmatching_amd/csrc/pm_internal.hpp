@@ -87,6 +87,8 @@ struct Comm {
   // consecutively (rbytes[g] from shard g).  Host byte counts, device buffers.
   virtual void alltoallv(const void* send, const uint64_t* sbytes, void* recv, const uint64_t* rbytes,
                          hipStream_t s) = 0;
+  virtual int ranks() const = 0;      // ranks of the communicator as its transport reports them
+  virtual int transport() const = 0;  // PM_TRANSPORT_* (pm_abi.h)
 };
 
 // Device scratch arena (bump allocator, reset per NLC line).
@@ -479,12 +481,14 @@ struct Ctx {
   unsigned long long* d_hkey = nullptr;  // (source, vertex) hash table, persistent
   unsigned long long* d_hval = nullptr;
   uint64_t hcap = 0;
-  bool hash_regrown = false;
+  bool hash_regrown = false;      // the last fused launch overflowed the table and grew it (rerun the line fused)
   uint64_t hash_slots = 0;        // PM_HASH_SLOTS (diagnostics): size of the context's first table (0: from |S|)
   int64_t nogrow_shard = -1;      // PM_DEBUG_NOGROW_SHARD (diagnostics): that shard reports no room to grow it
-  bool no_row_compaction = false;
+  int64_t overflow_shard = -1;    // PM_DEBUG_OVERFLOW_SHARD (diagnostics): that shard alone reports its first
+                                  // replicated path line of a search as overflowed (the agreement's test)
+  bool no_row_compaction = false; // PM_ROW_COMPACTION=0 (diagnostics): rows keep their dead entries
   uint32_t lcc_calls = 0;  // stamp of the LCC calls (the compaction's long-row word)
-  bool push_long = true;   // some row of S may be longer than a push-form piece (unknown: true)  // PM_ROW_COMPACTION=0 (diagnostics): rows keep their dead entries  // the last fused launch overflowed the table and grew it (rerun the line fused)
+  bool push_long = true;   // some row of S may be longer than a push-form piece (unknown: true)
   uint32_t* d_front = nullptr;    // slots inserted by a fused path line (cleared by it)
   unsigned* d_gbar = nullptr;     // grid barrier state of the fused line kernels
   unsigned line_grid = 0;         // blocks of a full-chip line launch (one per CU)
@@ -639,6 +643,7 @@ std::vector<uint64_t> shard_allreduce(Ctx& c, const std::vector<uint64_t>& v);  
 // part of a sharded search (arena, line hash table) must be the same on every shard, or an overflow -- and the
 // collectives of the path it takes -- could happen on some shards only.
 uint64_t shard_agree_min(Ctx& c, uint64_t v);
+std::vector<uint64_t> shard_gather_u64(Ctx& c, uint64_t v);  // every shard's v (collective)
 // S rows of the current state (slist entries with T_pub != 0) packed on the device: per row
 // {position, T_pub | T_state << 16, |M|, first entry} (4 u32) and its alive M entries; counts[0..1] =
 // rows, entries (device).  rec / ent hold nS_host rows / the caller's entry bound.

@@ -28,7 +28,9 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <stdexcept>
+#include <thread>
 #include <unordered_map>
 
 #include "pm_device.hpp"
@@ -2799,10 +2801,22 @@ void stream_wait(hipStream_t s) {
     PM_HIP_CHECK(hipStreamSynchronize(s));
     return;
   }
-  for (;;) {
+  // poll for a bounded time (the driver loop's read-backs are due within microseconds), then hand the core back
+  // between polls: a long wait (a 140 ms NLC search, a collective's partner) does not hold a CPU the other
+  // shards' host threads need
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t k = 1;; ++k) {
     const hipError_t e = hipStreamQuery(s);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) PM_HIP_CHECK(e);
+    if ((k & 63) == 0) {
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt > std::chrono::milliseconds(20)) {
+        PM_HIP_CHECK(hipStreamSynchronize(s));
+        return;
+      }
+      if (dt > std::chrono::microseconds(200)) std::this_thread::yield();
+    }
   }
 }
 

@@ -1457,6 +1457,32 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
       }
       std::fprintf(stderr, "%s\n", pos.c_str());
     }
+  if (c.comm && c.nshards > 1) {
+    // Sharded replica: the shards act on one agreed first overflowed line.  Every shard overflows the same
+    // replicated line as long as table sizes and insert outcomes are identical on all of them (regrow_hash);
+    // should one shard overflow alone, regrow_hash's agreement would meet collectives the others never make.
+    // So the first overflowed replicated line is gathered from every shard (one collective per launch): equal
+    // everywhere -> every shard regrows and reruns it; different -> every shard fails with the same message
+    // (the shards that went on have applied later lines' effects, so no rerun could restore one state).
+    uint64_t first = ~0ull;
+    for (unsigned j = 0; j + pl0 < done; ++j) {
+      if (hs[j].split) break;  // (a split line is the launch's last; split_line_finish agrees on it)
+      if (c.overflow_shard == static_cast<int64_t>(c.shard) && pl0 + j < 4) hs[j].overflow = 1;
+      if (hs[j].overflow) {
+        first = j;
+        break;
+      }
+    }
+    const std::vector<uint64_t> all = shard_gather_u64(c, first);
+    if (*std::min_element(all.begin(), all.end()) != *std::max_element(all.begin(), all.end())) {
+      std::string who;
+      for (size_t g = 0; g < all.size(); ++g)
+        who += (who.empty() ? "" : ", ") + ("shard " + std::to_string(g) + ": " +
+                                            (all[g] == ~0ull ? std::string("none") : std::to_string(pl0 + all[g])));
+      throw std::runtime_error("NLC line overflowed its table on some shards only (first overflowed line: " + who +
+                               ")");
+    }
+  }
   size_t completed = 0;
   for (unsigned j = 0; j + pl0 < done; ++j) {
     const LineStats& st = hs[j];

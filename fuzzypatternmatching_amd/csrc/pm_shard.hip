@@ -95,6 +95,12 @@ class RcclComm : public Comm {
     }
     PM_NCCL_CHECK(ncclGroupEnd());
   }
+  int ranks() const override {
+    int c = 0;
+    PM_NCCL_CHECK(ncclCommCount(comm_, &c));
+    return c;
+  }
+  int transport() const override { return PM_TRANSPORT_RCCL; }
 
  private:
   ncclComm_t comm_ = nullptr;
@@ -203,6 +209,8 @@ class HostComm : public Comm {
     check(h_.alltoallv(h_.user, hs, sbytes, hr, rbytes), "alltoallv");
     to_device(recv, hr, ro, s);
   }
+  int ranks() const override { return static_cast<int>(h_.nshards); }
+  int transport() const override { return PM_TRANSPORT_HOST; }
 
  private:
   struct Buf {
@@ -354,6 +362,8 @@ class ThreadComm : public Comm {
     PM_HIP_CHECK(hipStreamSynchronize(s));
     g_->barrier();
   }
+  int ranks() const override { return g_->n; }
+  int transport() const override { return PM_TRANSPORT_THREADS; }
 
  private:
   ThreadGroup* g_;
@@ -731,11 +741,15 @@ static void ensure_xcnt(Ctx& c) {
   if (!c.d_xcnt) PM_HIP_CHECK(hipMalloc(&c.d_xcnt, (64 + 4 * 64) * sizeof(uint64_t)));
 }
 
-uint64_t shard_agree_min(Ctx& c, uint64_t v) {
-  if (!c.comm || c.nshards <= 1) return v;
+std::vector<uint64_t> shard_gather_u64(Ctx& c, uint64_t v) {
+  if (!c.comm || c.nshards <= 1) return std::vector<uint64_t>(1, v);
   ensure_xcnt(c);
   PM_HIP_CHECK(hipMemcpyAsync(c.d_xcnt, &v, sizeof(uint64_t), hipMemcpyHostToDevice, c.stream));
-  const std::vector<uint64_t> all = gather_counts(c, 1);  // (synchronises the stream: v may leave scope)
+  return gather_counts(c, 1);  // (synchronises the stream: v may leave scope)
+}
+
+uint64_t shard_agree_min(Ctx& c, uint64_t v) {
+  const std::vector<uint64_t> all = shard_gather_u64(c, v);
   return *std::min_element(all.begin(), all.end());
 }
 
@@ -824,8 +838,32 @@ void shard_codes_after_first(Ctx& c) {
   if (!c.xcode_wide) {
     // a position's 2-bit code is set only by the shard that holds its row (a delegate's by its controller):
     // the shards' code arrays have disjoint fields, and their word-wise sum is their union -- one all-reduce
-    // of the code words (22 MB at S=28) instead of packing, gathering and unpacking every survivor's record
-    c.comm->allreduce_sum_u32(c.d_tcode, tcode_words(c.lr), c.stream);
+    // of the code words (22 MB at S=28) instead of packing, gathering and unpacking every survivor's record.
+    // Writers of tcode: superstep 0's finish paths for the rows a shard holds (a split delegate's share skips
+    // them) and k_hub_finish on the controller only.  PM_DEBUG_SYNC=1 checks the invariant: the nonzero
+    // 2-bit fields of the sum must number the shards' own (a field set by two shards carries into its
+    // neighbour or merges two codes, and both show as fewer fields).
+    static const bool check = std::getenv("PM_DEBUG_SYNC") != nullptr;
+    const size_t words = tcode_words(c.lr);
+    auto fields = [&]() {
+      std::vector<uint32_t> h(words);
+      if (words) PM_HIP_CHECK(hipMemcpyAsync(h.data(), c.d_tcode, words * 4, hipMemcpyDeviceToHost, c.stream));
+      PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+      uint64_t k = 0;
+      for (uint32_t x : h) k += __builtin_popcount((x | (x >> 1)) & 0x55555555u);
+      return k;
+    };
+    const uint64_t own = check ? fields() : 0;
+    c.comm->allreduce_sum_u32(c.d_tcode, words, c.stream);
+    if (check) {
+      const std::vector<uint64_t> all = shard_gather_u64(c, own);
+      uint64_t sum = 0;
+      for (uint64_t x : all) sum += x;
+      const uint64_t got = fields();
+      if (got != sum)
+        throw std::runtime_error("superstep-0 code exchange: " + std::to_string(sum) + " code fields set over the "
+                                 "shards but " + std::to_string(got) + " in their sum (two shards wrote one field)");
+    }
     c.xcode_n.clear();
     c.xcode_in_tpub = false;
     return;

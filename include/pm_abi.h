@@ -250,6 +250,36 @@ int pm_run_rmat_local_shards2(uint64_t scale, uint64_t p_gen, const char* patter
                               uint32_t nranks, uint64_t hub_threshold, const uint64_t* labels, const char* result_dir,
                               uint64_t max_iterations, uint32_t repeats, pm_run_stats* per_shard);
 
+/* The same with every shard's statistics (per_shard[q], q < nshards; may be NULL), the search run `repeats`
+ * times (result files from the first run) and -v label files: label_prefix (NULL: `labels`, or degree labels
+ * when both are NULL) is parsed on the device once and shared by the shards (vertex_data_db.hpp:137-257).
+ * The drop-in executable's mode for a P-partition graph on fewer GPUs than P (run_pattern_matching_beta). */
+int pm_run_beta_local_shards2(const pm_graph_desc* graph, const char* pattern_dir, int device, uint32_t nshards,
+                              const uint64_t* labels, const char* label_prefix, const char* result_dir,
+                              uint64_t max_iterations, uint32_t repeats, pm_run_stats* per_shard);
+
+/* Graph files of a sharded run.  pm_graph_partitions: P of <base>_<r>_of_<P> (-1: none found).
+ * pm_read_graph_shard: shard `shard` of `nshards` read straight from the files, as pm_create_shard takes it --
+ * the rows of ids v % nshards == shard whole, of a delegate (degree >= the files' hub threshold, nshards > 1)
+ * the entries whose target that shard owns (delegate_partitioned_graph.ipp:1402-1648), every other row empty
+ * -- plus the n global degrees.  Each rank of a launch reads its own shard (distributed_db.hpp:353-357 opens
+ * <base>_<rank>_of_<P>; here every file's row index is read for the global degrees, and only the held entries
+ * are copied).  off (n + 1), col (>= 1 element), degree (n) are malloc'ed (pm_free_host). */
+int pm_graph_partitions(const char* base);
+int pm_read_graph_shard(const char* base, uint32_t nshards, uint32_t shard, uint64_t** off, uint32_t** col,
+                        uint32_t** degree, uint64_t* n, int* symmetric, uint32_t* nranks, uint64_t* hub_threshold);
+
+/* HIP devices visible to this process (0 without a GPU; no context is created). */
+int pm_device_count(void);
+
+/* A context's place in its search: shard count, its shard, the ranks of its communicator as the transport
+ * reports them (RCCL: ncclCommCount; 0 on a one-context search) and the transport. */
+#define PM_TRANSPORT_NONE 0    /* one context, no exchange                                      */
+#define PM_TRANSPORT_RCCL 1    /* RCCL over xGMI, one rank per GPU                               */
+#define PM_TRANSPORT_HOST 2    /* caller's host collectives (pm_host_comm: MPI, gloo, TCP)      */
+#define PM_TRANSPORT_THREADS 3 /* in-process shards on one device                                */
+int pm_comm_info(const pm_ctx* ctx, uint32_t* nshards, uint32_t* shard, int32_t* comm_ranks, int32_t* transport);
+
 /* Host-side input builders (no device needed). */
 /* Directed pairs (u,v),(v,u) of generator ranks first, first + stride, ... < p_gen. */
 int pm_rmat_edges(uint64_t scale, uint64_t p_gen, uint64_t first, uint64_t stride, uint32_t** src, uint32_t** dst,
