@@ -368,6 +368,14 @@ inline uint32_t graph_file_partitions(const std::string& base) {
   return 0;
 }
 
+// The header of <base>_0_of_<P> (vertex count, P, hub threshold, symmetric flag).
+inline GraphFileHeader graph_file_header(const std::string& base) {
+  const uint32_t P = graph_file_partitions(base);
+  if (P == 0) throw std::runtime_error("no graph files found for base " + base);
+  MappedGraphFile f(graph_file_name(base, 0, P));
+  return f.header();
+}
+
 // One shard of a sharded search, read from the graph files.  The reference's rank r opens only
 // <base>_<r>_of_<P> (distributed_db.hpp:353-357, beta.cpp:209-223) because its files ARE the partition; the
 // search's partition here is owner = id % nshards with a delegate's row (global degree >= the hub threshold)

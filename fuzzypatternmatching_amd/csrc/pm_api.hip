@@ -297,6 +297,8 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   c->arena.cap = arena;
   if (const char* e = std::getenv("PM_FUSED_LINES")) c->fused_lines = std::string(e) != "0";
   if (const char* e = std::getenv("PM_ROW_COMPACTION")) c->no_row_compaction = std::string(e) == "0";
+  if (const char* e = std::getenv("PM_PULL_PIECES")) c->long_seen_off = std::string(e) == "0";
+  if (const char* e = std::getenv("PM_PULL_LONG")) c->pull_long = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("PM_DIAG_STEP")) c->diag_step = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
   c->any_sv = any_sv;
@@ -352,6 +354,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit, c->d_push,
+                  c->d_lrows,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -377,6 +380,7 @@ static void relayout(Ctx& c) {
   c.layout_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_lay).count();
   c.lcc_started = false;
   c.tpub_clean = false;  // positions changed: the next reset clears T_pub entirely
+  c.long_seen.clear();   // (new labels: where long rows survive is not known)
   // the line grid of a search's prelaunched lines is sized by the previous search's |S| (identical for repeated
   // searches of one layout); new labels: the full grid until a search has run
   c.live_hint = ~0ull;
@@ -613,6 +617,10 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         out.loc_surv += local[r];
         out.loc_edges += local[P + r];
       }
+    }
+    if (init_step && ss > 0) {  // pull supersteps that deferred long rows (the next search's pieces launches)
+      if (c.long_seen.size() < D) c.long_seen.assign(D, 1);
+      c.long_seen[ss] = h[2 * P + 4] != 0;
     }
     if (init_step) {  // the survivors' mean |M| per superstep (the next search's entries in flight)
       uint64_t v = 0, e = 0;

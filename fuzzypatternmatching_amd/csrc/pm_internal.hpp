@@ -447,6 +447,14 @@ struct Ctx {
   // next superstep's rows), and the superstep being launched
   std::vector<double> m_per_row;
   uint64_t cur_ss = 0;
+  // pull-form rows above kPullLong entries, worked in pieces by a second launch (k_lcc_step_pieces): the list,
+  // and per superstep of the first call whether the previous search deferred any there (empty: not known --
+  // every pull superstep gets the pieces launch; a superstep with none skips it from then on)
+  void* d_lrows = nullptr;
+  uint32_t lrows_cap = 0;
+  std::vector<uint8_t> long_seen;
+  bool long_seen_off = false;  // PM_PULL_PIECES=0 (diagnostics): long rows walked by one wave, as before
+  uint32_t pull_long = 0;      // PM_PULL_LONG (tests): list rows above this many entries (0: kPullLong)
   uint32_t* d_tcnt = nullptr;     // superstep-0 survivors per tile
   uint32_t* d_tstart = nullptr;   // position of a tile's row 0 (heavy tile: its row)
   void* d_scan_tmp = nullptr;     // rocPRIM scan workspace for the slist build
@@ -544,7 +552,7 @@ inline uint64_t m_cap(const Ctx& c) { return c.replicated ? c.rmcap : c.mcap; }
 void build_label_layout(Ctx& c, uint32_t* src_col, bool src_is_layout, uint32_t* dst);
 void build_tiling(Ctx& c);
 // Counter slots: W = slot_words(c) u64 = [vertices per rank | edges per rank |
-// traversed | matching rows | removed flag | asymmetry flag].
+// traversed | matching rows | removed flag | asymmetry flag | pull-form long rows deferred | their pieces].
 uint32_t slot_words(const Ctx& c);
 // ev0/ev1 (may be null) bracket the kernel launch alone (roofline timing)
 void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);

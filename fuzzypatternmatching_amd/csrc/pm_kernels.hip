@@ -1067,6 +1067,30 @@ __global__ void k_slist_write(const uint32_t* __restrict__ tcnt, const uint32_t*
 // through the live mask of the previous superstep.
 static constexpr uint32_t kLprMax = 32;
 
+// Rows above kPullLong entries (R-MAT hubs that survived superstep 0 with their superstep-0 length: up to millions
+// of entries at C5 S=27, of which a few thousand stay alive) are not walked by one wave, which made the pull
+// supersteps of C5's first call 15 / 6 / 5 ms long: the step kernel defers such a row to a list and every wave of a
+// second launch (k_lcc_step_pieces) takes kPullPiece-entry pieces of the listed rows; the last piece of a row to
+// finish verifies it.
+static constexpr uint32_t kPullLong = 4096;
+static constexpr uint32_t kPullPiece = 2048;
+struct LongRow {
+  uint32_t u;        // position
+  uint32_t i;        // slist index (chunk i / 64, bit i % 64 of the live / keep masks)
+  uint64_t beg;      // first M entry
+  uint32_t len;      // M entries
+  uint16_t Ts, nm;   // T_state, neighbour mask of T_pub
+  uint64_t pbase;    // number of its first piece (pieces are numbered over the whole list)
+  uint32_t tn, cnt;  // the pieces' OR / count
+  uint32_t done, pad_;
+};
+struct LongList {
+  LongRow* rows;            // null: every row is walked in the step kernel
+  unsigned long long* cnt;  // [0] listed rows, [1] pieces (counter slot words 2P + 4, 2P + 5)
+  uint32_t cap;
+  uint32_t min_len;         // rows above this many entries are listed (kPullLong; PM_PULL_LONG in tests)
+};
+
 // (store = false: timing variant PM_DIAG_STEP & 4)
 __device__ __forceinline__ void k2_entry(uint32_t* __restrict__ mcol, uint64_t e, uint32_t m, uint16_t tv,
                                          uint16_t nm, uint32_t& tn, uint32_t& cnt, bool& asym, bool store = true) {
@@ -1119,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
     const uint4* __restrict__ srec, uint64_t dbase, unsigned long long* __restrict__ keep_out, RecSrc rs,
-    uint32_t* __restrict__ slist_out) {
+    uint32_t* __restrict__ slist_out, LongList ll) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1226,6 +1250,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         tnxt[u] = 0;
       }
     }
+    // a row above kPullLong entries goes to the long-row list (its pieces: k_lcc_step_pieces, which also verifies
+    // it and sets its live / keep bits); a full list leaves it to this wave.  (A dense superstep-0 row -- at most
+    // 480 entries, moved to its padded row if it survives -- stays here whatever the threshold.)
+    bool deferred = false;
+    if (ll.rows && len > ll.min_len && !drow) {
+      const unsigned long long r = atomicAdd(ll.cnt, 1ull);
+      if (r < ll.cap) {
+        const uint32_t np = (len + kPullPiece - 1) / kPullPiece;
+        const unsigned long long pb = atomicAdd(ll.cnt + 1, static_cast<unsigned long long>(np));
+        LongRow lrow{};
+        lrow.u = u;
+        lrow.i = static_cast<uint32_t>(i);
+        lrow.beg = beg;
+        lrow.len = len;
+        lrow.Ts = Ts;
+        lrow.nm = nm;
+        lrow.pbase = pb;
+        ll.rows[r] = lrow;
+        deferred = true;
+        len = 0;
+      }
+    }
     uint32_t tn = 0, cnt = 0;
     bool asym = false;
     // short rows: flattened over the wave -- the chunk's rows are concatenated
@@ -1315,7 +1361,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     }
     bool survivor = false, removed = false, cleared = false;
     uint32_t mv = 0;  // entries of this lane's dense survivor row to move to its padded row
-    if (Tu) {
+    if (Tu && !deferred) {
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
         survivor = true;
@@ -1438,6 +1484,129 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       }
     }
   }
+  flush_block(acc, oa, s_hist, s_red, pp);
+}
+
+// The deferred long rows of a pull superstep (k_lcc_step: rows above kPullLong entries), in kPullPiece-entry pieces:
+// piece k of the list (rows in list order, row r's pieces numbered from its pbase) goes to wave k % W of the grid,
+// four entries in flight per lane.  A piece updates its entries as the step kernel does (k2_entry), ORs its TN and
+// adds its count into the row's words; the last piece of the row to finish (ticket) verifies it: T_state, T_pub,
+// |M| alive and its live / keep bits (OR-ed into the masks the step kernel wrote without it), or its removal.
+__global__ __launch_bounds__(kBlock) void k_lcc_step_pieces(LongList ll, uint16_t* tcur, uint16_t* __restrict__ tnxt,
+                                                            uint16_t* __restrict__ tst, PatArgs pa, OwnerArgs oa,
+                                                            uint32_t* __restrict__ mcol, uint32_t* __restrict__ malive,
+                                                            Partials pp, const uint32_t* __restrict__ tcode,
+                                                            LabelRuns lr, int has_srec,
+                                                            unsigned long long* __restrict__ mask_out,
+                                                            unsigned long long* __restrict__ keep_out) {
+  __shared__ unsigned long long s_hist[2 * kMaxRanks];
+  __shared__ unsigned long long s_red[kWpb * 6];
+  __shared__ uint16_t s_adj[16];
+  __shared__ uint32_t s_rlo[16], s_rlen[16], s_rtu[16], s_rcd[16];
+  for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
+  load_adj(s_adj, pa);
+  if (threadIdx.x < 16) {
+    const int l = threadIdx.x;
+    s_rlo[l] = lr.lo[l];
+    s_rlen[l] = l < lr.n ? lr.len[l] : 0u;
+    s_rtu[l] = lr.tu[l];
+    s_rcd[l] = lr.cd[l];
+  }
+  __syncthreads();
+  const int nruns = lr.n;
+  // neighbour T_pub as the step kernel reads it (2-bit codes right after superstep 0, else the T_pub array)
+  auto tpub_of = [&](uint32_t p) -> uint16_t {
+    if (!tcode) return tcur[p];
+    uint32_t tu = 0, ci = 0;
+    for (int l = 0; l < nruns; ++l)
+      if (p - s_rlo[l] < s_rlen[l]) {
+        tu = s_rtu[l];
+        ci = p + s_rcd[l];
+      }
+    const uint32_t code = (tcode[ci >> 4] >> ((ci & 15u) << 1)) & 3u;
+    if (!code) return 0;
+    const uint32_t rest = tu & (tu - 1);
+    if (rest & (rest - 1)) return tcur[p];
+    return static_cast<uint16_t>(((code & 1u) ? (tu & (0u - tu)) : 0u) | ((code & 2u) ? rest : 0u));
+  };
+  BlockAcc acc;
+  bool asym = false;
+  const int lane = lane_id();
+  const uint64_t W = uint64_t(gridDim.x) * kWpb;
+  const uint64_t gw = uint64_t(blockIdx.x) * kWpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t nrows = static_cast<uint32_t>(min<unsigned long long>(ll.cnt[0], ll.cap));
+  for (uint32_t r = 0; r < nrows; ++r) {
+    LongRow* R = ll.rows + r;
+    const uint64_t beg = R->beg, pbase = R->pbase;
+    const uint32_t len = R->len, np = (len + kPullPiece - 1) / kPullPiece;
+    const uint16_t nm = R->nm;
+    for (uint64_t q = (gw + W - pbase % W) % W; q < np; q += W) {
+      const uint32_t j0 = static_cast<uint32_t>(q) * kPullPiece;
+      const uint32_t j1 = min(len, j0 + kPullPiece);
+      uint32_t tn = 0, cnt = 0;
+      for (uint32_t jb = j0; jb < j1; jb += 4 * kWave) {
+        uint32_t m[4];
+        uint16_t tv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t j = jb + k * kWave + lane;
+          m[k] = j < j1 ? mcol[beg + j] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[k] = (m[k] & kAlive) ? tpub_of(m[k] & kPosMask) : uint16_t(0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (m[k] & kAlive) k2_entry(mcol, beg + jb + k * kWave + lane, m[k], tv[k], nm, tn, cnt, asym);
+      }
+      tn = wave_or32(tn);
+      cnt = static_cast<uint32_t>(wave_sum(cnt));
+      if (lane == 0) {
+        if (tn) atomicOr(&R->tn, tn);
+        if (cnt) atomicAdd(&R->cnt, cnt);
+        __threadfence();
+        if (atomicAdd(&R->done, 1u) == np - 1) {  // the row's last piece: verify it
+          __threadfence();
+          const uint16_t TN = static_cast<uint16_t>(atomicOr(&R->tn, 0u));
+          const uint32_t CNT = atomicAdd(&R->cnt, 0u);
+          const uint32_t u = R->u, i = R->i;
+          const unsigned long long bit = 1ull << (i % kWave);
+          const uint16_t T = keep_bits(R->Ts, TN, s_adj);
+          if (T) {
+            tst[u] = T;
+            tnxt[u] = T;
+            malive[u] = CNT;
+            atomicOr(&mask_out[i / kWave], bit);
+            if (keep_out) atomicOr(&keep_out[i / kWave], bit);
+            if (oa.nranks <= 1) {
+              acc.vs += 1;
+              acc.es += CNT;
+            } else {
+              acc_owner(s_hist, oa, u, CNT);
+            }
+          } else {
+            acc.removed = 1;
+            tnxt[u] = 0;
+            malive[u] = 0;
+            // (as the step kernel: right after superstep 0 a label of at most two template vertices is read
+            // through its codes, so the T_pub buffer read now is cleared at once and the row leaves the list)
+            bool cleared = false;
+            if (tcode) {
+              uint32_t tu = 0;
+              for (int l = 0; l < nruns; ++l)
+                if (u - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
+              const uint32_t rest = tu & (tu - 1);
+              if (!(rest & (rest - 1))) {
+                if (!has_srec) tcur[u] = 0;
+                cleared = true;
+              }
+            }
+            if (!cleared) atomicOr(&mask_out[i / kWave], bit);
+          }
+        }
+      }
+    }
+  }
+  acc.asym |= asym;
   flush_block(acc, oa, s_hist, s_red, pp);
 }
 
@@ -1734,7 +1903,7 @@ static OwnerArgs owner_args(const Ctx& c) {
   return oa;
 }
 
-uint32_t slot_words(const Ctx& c) { return 2 * (c.nranks <= 1 ? 1 : c.nranks) + 4; }
+uint32_t slot_words(const Ctx& c) { return 2 * (c.nranks <= 1 ? 1 : c.nranks) + 6; }
 
 static Partials partials(Ctx& c, uint64_t* d_slot) {
   return Partials{reinterpret_cast<unsigned long long*>(c.d_part), reinterpret_cast<unsigned long long*>(d_slot)};
@@ -2527,6 +2696,8 @@ void ensure_slist2(Ctx& c) {
   PM_HIP_CHECK(hipMemset(c.d_nS2, 0, 2 * sizeof(uint32_t)));
 }
 
+static constexpr unsigned kLongGrid = 2048;  // blocks of the long rows' pieces launch (8192 waves)
+
 void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   if (!c.d_kmask) PM_HIP_CHECK(hipMalloc(&c.d_kmask, ((c.n + 63) / 64 + 1) * sizeof(uint64_t)));
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
@@ -2549,12 +2720,33 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   // records and codes: the specialised instantiation (no spills at 6 waves per SIMD; budgets for 7 / 8 waves
   // spilled 13 / 31 VGPRs and ran 516-525 / 616-620 us against 513)
   if (first_after_ss0 && c.k1_records && c.d_srec) kern = short_rows ? k_lcc_step<3, true> : k_lcc_step<4, true>;
+  // long rows in pieces (a second launch) where the previous search of this layout deferred some, or while that
+  // is not known; the counters are the slot's words 2P + 4 / 2P + 5 (zeroed with the slots)
+  LongList ll{};
+  const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
+  const bool longs = !c.long_seen_off && (c.cur_ss >= c.long_seen.size() || c.long_seen[c.cur_ss]);
+  if (longs) {
+    if (!c.d_lrows) {
+      c.lrows_cap = 1u << 16;
+      PM_HIP_CHECK(hipMalloc(&c.d_lrows, uint64_t(c.lrows_cap) * sizeof(LongRow)));
+    }
+    ll = LongList{static_cast<LongRow*>(c.d_lrows), reinterpret_cast<unsigned long long*>(d_slot + 2 * P + 4),
+                  c.lrows_cap, c.pull_long ? c.pull_long : kPullLong};
+  }
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                      c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,
-                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist);
+                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist, ll);
   PM_HIP_CHECK(hipGetLastError());
+  if (longs) {
+    hipLaunchKernelGGL(k_lcc_step_pieces, dim3(kLongGrid), dim3(kBlock), 0, c.stream, ll, c.d_tpub[c.cur],
+                       c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_malive,
+                       partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
+                       first_after_ss0 && c.k1_records && c.d_srec ? 1 : 0, mout,
+                       reinterpret_cast<unsigned long long*>(c.d_kmask));
+    PM_HIP_CHECK(hipGetLastError());
+  }
   c.removed_cleared = first_after_ss0 && c.k1_records;  // (its removed rows cleared the T_pub they read)
   c.k1_dense = false;  // every M row of S is in its padded row from here on
   c.k1_records = false;

@@ -19,7 +19,8 @@
 //     one thread and one GPU each, one RCCL communicator (xGMI);
 //   * one process, P > 1 and fewer GPUs than P: the P shards in-process on
 //     device 0 (pm_run_beta_local_shards2);
-//   * P = 1: one context holds the whole graph.
+//   * P = 1, or a directed graph (the sharded search takes symmetric graphs): one context holds the whole graph
+//     (launched: on rank 0).
 // PM_SHARDS=<k> overrides the shard count of a one-process run (any k: the
 // shards are read from the files whatever their P); PM_TRANSPORT=rccl|host
 // forces a launched run's transport.  Results are identical in every mode.
@@ -338,6 +339,23 @@ int run_launched(const Options& o, const pm::LaunchEnv& env) {
     return 1;
   }
   grp.bcast(uid.data(), uid.size());
+  // a directed graph (ingest_edge_list -u 0): the sharded search takes symmetric graphs, so rank 0 runs the
+  // search on one context and the other ranks only wait for it
+  bool directed = false;
+  try {
+    directed = !pm::graph_file_header(o.graph_input).symmetric;
+  } catch (const std::exception&) {
+    // (a missing file is reported by the shard read below, on every rank)
+  }
+  if (directed) {
+    int rc = 0;
+    if (me == 0) {
+      std::cout << "Directed input graph: one context on rank 0 (the sharded search takes symmetric graphs)"
+                << std::endl;
+      rc = run_one_context(o);
+    }
+    return grp.agree(rc == 0) ? 0 : 1;
+  }
   if (me == 0)
     std::cout << "Loading Graph ... (" << G << " ranks launched by " << env.launcher << ", "
               << (rccl ? "RCCL" : "host collectives over TCP") << ")" << std::endl;
@@ -437,6 +455,8 @@ int main(int argc, char** argv) {
       std::cerr << "Error: " << pm_last_error(nullptr) << std::endl;
       return 1;
     }
+    // a directed graph (ingest_edge_list -u 0) runs on one context: the sharded search takes symmetric graphs
+    if (!pm::graph_file_header(o.graph_input).symmetric) return run_one_context(o);
     uint32_t nshards = static_cast<uint32_t>(P);
     if (const char* s = std::getenv("PM_SHARDS")) nshards = static_cast<uint32_t>(std::strtoul(s, nullptr, 10));
     if (nshards == 0 || nshards > 64) {

@@ -87,6 +87,40 @@ def test_exact_count_token_passing_matches_oracle(pat, scale, p_gen, alphabet, n
     assert sg["nlcc_edges"] == so["nlcc_edges"] and sg["tds_edges"] == so["tds_edges"]
 
 
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards", [("tree", 16, 4, None, 4, 0), ("cycle", 14, 4, None, 1, 0),
+                                                                    ("cycle", 12, 4, 8, 3, 0), ("cycle", 15, 4, 64, 1, 0),
+                                                                    ("tree", 15, 4, None, 2, 3), ("cycle", 13, 4, 8, 1, 2)])
+def test_pull_long_rows_in_pieces(pat, scale, p_gen, alphabet, nranks, shards, tmp_path, monkeypatch):
+    """PM_PULL_LONG=8: every pull-superstep row above 8 entries goes to the long-row list and is worked in pieces by
+    k_lcc_step_pieces (the path of C5's hub rows, normally above 4096 entries), its verify by the row's last piece;
+    three searches per context (from the second on, the pieces launch runs only where the previous search listed
+    rows), and the sharded path, against the oracle."""
+    monkeypatch.setenv("PM_PULL_LONG", "8")
+    g = pm.rmat_graph(scale, p_gen)
+    labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
+    a = tmp_path / "oracle"
+    hub = 64 if shards else pm.DEFAULT_HUB_THRESHOLD  # (sharded: delegates split by target owner)
+    so = oracle.run(g.off, g.col, PATTERNS[pat], str(a), labels=labels, nranks=nranks, hub_threshold=hub)
+    keys = ("lcc_edges", "nlcc_edges", "tds_edges", "walks", "final_vertices", "final_edges")
+    want = tuple(so["paths" if k == "walks" else k] for k in keys)
+    if shards:
+        b = tmp_path / "gpu_shards"
+        sg = pm.run_beta_local_shards(pm.Graph(g.off, g.col, True, nranks, hub_threshold=hub), PATTERNS[pat], shards,
+                                      str(b), labels=labels)
+        assert pmtest.compare_result_dirs(str(a), str(b), nranks) == []
+        assert tuple(sg[k] for k in keys) == want
+        return
+    m = pm.PatternMatcher(pm.Graph(g.off, g.col, True, nranks), PATTERNS[pat], labels=labels)
+    try:
+        for i in range(3):
+            b = tmp_path / f"gpu{i}"
+            sg = m.run_beta(str(b))
+            assert pmtest.compare_result_dirs(str(a), str(b), nranks) == [], i
+            assert tuple(sg[k] for k in keys) == want, i
+    finally:
+        m.close()
+
+
 def _tree_pairs():
     return [(0, 1), (1, 2), (1, 3), (3, 5), (4, 5), (5, 6)], np.array([3, 4, 7, 2, 3, 5, 7], np.uint64)
 
