@@ -354,7 +354,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit, c->d_push,
-                  c->d_lrows,
+                  c->d_lrows, c->d_lscr,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -549,7 +549,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         // entries inside the superstep, one counter reservation per 64-entry chunk, measured 1.2 ms slower
         // at S=28: 153 k atomics on one address serialise.)
         c.cur_ss = init_step ? ss : 0;
-        launch_lcc_step(c, slot, init_step && ss == 1);
+        launch_lcc_step(c, slot, init_step && ss == 1, ss + 1 == D);
         debug_point(c, "pull superstep"); debug_watch(c, "pull superstep");
         if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
         debug_point(c, "list compaction"); debug_watch(c, "list compaction");

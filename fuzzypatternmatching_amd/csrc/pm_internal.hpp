@@ -452,6 +452,8 @@ struct Ctx {
   // every pull superstep gets the pieces launch; a superstep with none skips it from then on)
   void* d_lrows = nullptr;
   uint32_t lrows_cap = 0;
+  void* d_lscr = nullptr;          // the last pull superstep's packing scratch (k_long_pack): pieces + counts
+  uint64_t lscr_pieces = 0;
   std::vector<uint8_t> long_seen;
   bool long_seen_off = false;  // PM_PULL_PIECES=0 (diagnostics): long rows walked by one wave, as before
   uint32_t pull_long = 0;      // PM_PULL_LONG (tests): list rows above this many entries (0: kPullLong)
@@ -562,7 +564,7 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
 unsigned lcc_first_grid(const Ctx& c);
 // first_after_ss0: the superstep right after superstep 0 of the first call
 // (T_pub is still superstep 0's output: neighbours' T_pub from the 2-bit codes)
-void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false);
+void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false, bool last_of_call = false);
 void ensure_slist2(Ctx& c);
 // Push form of a later superstep (send + verify launches): directed inputs and
 // LCC calls after the first (M may be asymmetric there).

@@ -1071,7 +1071,9 @@ static constexpr uint32_t kLprMax = 32;
 // of entries at C5 S=27, of which a few thousand stay alive) are not walked by one wave, which made the pull
 // supersteps of C5's first call 15 / 6 / 5 ms long: the step kernel defers such a row to a list and every wave of a
 // second launch (k_lcc_step_pieces) takes kPullPiece-entry pieces of the listed rows; the last piece of a row to
-// finish verifies it.
+// finish verifies it.  In the call's last pull superstep the pieces also pack the row's alive entries (a scratch
+// slice per piece) and k_long_pack moves them to the row start: the row compaction at the end of the call
+// (k_compact_rows: one wave per row, 12 ms at C5) finds these rows compacted.
 static constexpr uint32_t kPullLong = 4096;
 static constexpr uint32_t kPullPiece = 2048;
 struct LongRow {
@@ -1080,15 +1082,20 @@ struct LongRow {
   uint64_t beg;      // first M entry
   uint32_t len;      // M entries
   uint16_t Ts, nm;   // T_state, neighbour mask of T_pub
-  uint64_t pbase;    // number of its first piece (pieces are numbered over the whole list)
+  uint64_t pbase;    // number of its first piece (pieces are numbered over the whole list, in list order)
   uint32_t tn, cnt;  // the pieces' OR / count
-  uint32_t done, pad_;
+  uint32_t done;     // pieces finished (ticket)
+  uint32_t T;        // T_pub after the verify (0: removed)
 };
 struct LongList {
   LongRow* rows;            // null: every row is walked in the step kernel
-  unsigned long long* cnt;  // [0] listed rows, [1] pieces (counter slot words 2P + 4, 2P + 5)
+  unsigned long long* cnt;  // listed rows << 32 | their pieces (counter slot word 2P + 4): one atomic reserves both,
+                            // so the rows' first pieces increase with their list index
   uint32_t cap;
   uint32_t min_len;         // rows above this many entries are listed (kPullLong; PM_PULL_LONG in tests)
+  uint32_t* scr;            // last pull superstep: piece k's alive entries at scr + k * kPullPiece (null: no packing)
+  uint32_t* pcnt;           // ... and their number
+  uint64_t scr_pieces;      // pieces the scratch holds (a row with a piece beyond it is left to k_compact_rows)
 };
 
 // (store = false: timing variant PM_DIAG_STEP & 4)
@@ -1255,10 +1262,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     // 480 entries, moved to its padded row if it survives -- stays here whatever the threshold.)
     bool deferred = false;
     if (ll.rows && len > ll.min_len && !drow) {
-      const unsigned long long r = atomicAdd(ll.cnt, 1ull);
+      const uint32_t np = (len + kPullPiece - 1) / kPullPiece;
+      const unsigned long long old = atomicAdd(ll.cnt, (1ull << 32) | np);
+      const unsigned long long r = old >> 32, pb = old & 0xFFFFFFFFull;
       if (r < ll.cap) {
-        const uint32_t np = (len + kPullPiece - 1) / kPullPiece;
-        const unsigned long long pb = atomicAdd(ll.cnt + 1, static_cast<unsigned long long>(np));
         LongRow lrow{};
         lrow.u = u;
         lrow.i = static_cast<uint32_t>(i);
@@ -1488,10 +1495,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 }
 
 // The deferred long rows of a pull superstep (k_lcc_step: rows above kPullLong entries), in kPullPiece-entry pieces:
-// piece k of the list (rows in list order, row r's pieces numbered from its pbase) goes to wave k % W of the grid,
-// four entries in flight per lane.  A piece updates its entries as the step kernel does (k2_entry), ORs its TN and
-// adds its count into the row's words; the last piece of the row to finish (ticket) verifies it: T_state, T_pub,
-// |M| alive and its live / keep bits (OR-ed into the masks the step kernel wrote without it), or its removal.
+// piece k of the list (rows in list order, row r's pieces numbered from its pbase) goes to wave k % W of the grid
+// (its row found by a binary search over the rows' first pieces), four entries in flight per lane.  A piece updates
+// its entries as the step kernel does (k2_entry), ORs its TN and adds its count into the row's words; the last
+// piece of the row to finish (ticket) verifies it: T_state, T_pub, |M| alive and its live / keep bits (OR-ed into
+// the masks the step kernel wrote without it), or its removal.  Packing (ll.scr): the piece's alive entries go to
+// its scratch slice in order, their number to pcnt.
 __global__ __launch_bounds__(kBlock) void k_lcc_step_pieces(LongList ll, uint16_t* tcur, uint16_t* __restrict__ tnxt,
                                                             uint16_t* __restrict__ tst, PatArgs pa, OwnerArgs oa,
                                                             uint32_t* __restrict__ mcol, uint32_t* __restrict__ malive,
@@ -1534,80 +1543,138 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step_pieces(LongList ll, uint16_
   const int lane = lane_id();
   const uint64_t W = uint64_t(gridDim.x) * kWpb;
   const uint64_t gw = uint64_t(blockIdx.x) * kWpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint32_t nrows = static_cast<uint32_t>(min<unsigned long long>(ll.cnt[0], ll.cap));
-  for (uint32_t r = 0; r < nrows; ++r) {
-    LongRow* R = ll.rows + r;
-    const uint64_t beg = R->beg, pbase = R->pbase;
+  const uint32_t nrows = static_cast<uint32_t>(min<unsigned long long>(*ll.cnt >> 32, ll.cap));
+  const LongRow* rows = ll.rows;
+  const uint64_t pend = nrows ? rows[nrows - 1].pbase + (rows[nrows - 1].len + kPullPiece - 1) / kPullPiece : 0;
+  for (uint64_t k = gw; k < pend; k += W) {
+    uint32_t lo = 0, hi = nrows - 1;  // the last row whose first piece is at or below k
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (rows[mid].pbase <= k) lo = mid; else hi = mid - 1;
+    }
+    LongRow* R = ll.rows + __builtin_amdgcn_readfirstlane(lo);
+    const uint64_t beg = R->beg;
     const uint32_t len = R->len, np = (len + kPullPiece - 1) / kPullPiece;
+    const uint32_t q = static_cast<uint32_t>(k - R->pbase);
     const uint16_t nm = R->nm;
-    for (uint64_t q = (gw + W - pbase % W) % W; q < np; q += W) {
-      const uint32_t j0 = static_cast<uint32_t>(q) * kPullPiece;
-      const uint32_t j1 = min(len, j0 + kPullPiece);
-      uint32_t tn = 0, cnt = 0;
-      for (uint32_t jb = j0; jb < j1; jb += 4 * kWave) {
-        uint32_t m[4];
-        uint16_t tv[4];
+    const uint32_t j0 = q * kPullPiece, j1 = min(len, j0 + kPullPiece);
+    const bool pack = ll.scr && k < ll.scr_pieces;
+    uint32_t* const out = pack ? ll.scr + k * kPullPiece : nullptr;
+    uint32_t tn = 0, cnt = 0, kept = 0;
+    for (uint32_t jb = j0; jb < j1; jb += 4 * kWave) {
+      uint32_t m[4];
+      uint16_t tv[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t j = jb + k * kWave + lane;
-          m[k] = j < j1 ? mcol[beg + j] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) tv[k] = (m[k] & kAlive) ? tpub_of(m[k] & kPosMask) : uint16_t(0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (m[k] & kAlive) k2_entry(mcol, beg + jb + k * kWave + lane, m[k], tv[k], nm, tn, cnt, asym);
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t j = jb + t * kWave + lane;
+        m[t] = j < j1 ? mcol[beg + j] : 0u;
       }
-      tn = wave_or32(tn);
-      cnt = static_cast<uint32_t>(wave_sum(cnt));
-      if (lane == 0) {
-        if (tn) atomicOr(&R->tn, tn);
-        if (cnt) atomicAdd(&R->cnt, cnt);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) tv[t] = (m[t] & kAlive) ? tpub_of(m[t] & kPosMask) : uint16_t(0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        uint32_t c1 = 0;
+        if (m[t] & kAlive) k2_entry(mcol, beg + jb + t * kWave + lane, m[t], tv[t], nm, tn, c1, asym);
+        cnt += c1;
+        if (pack) {  // (entries stay in row order: component t covers jb + 64 t .. jb + 64 t + 63)
+          const uint64_t b = __ballot(c1 != 0);
+          if (c1) out[kept + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u))] =
+              (m[t] & kPosMask) | kAlive;
+          kept += static_cast<uint32_t>(__builtin_popcountll(b));
+        }
+      }
+    }
+    tn = wave_or32(tn);
+    cnt = static_cast<uint32_t>(wave_sum(cnt));
+    if (lane == 0) {
+      if (pack) ll.pcnt[k] = kept;
+      if (tn) atomicOr(&R->tn, tn);
+      if (cnt) atomicAdd(&R->cnt, cnt);
+      __threadfence();
+      if (atomicAdd(&R->done, 1u) == np - 1) {  // the row's last piece: verify it
         __threadfence();
-        if (atomicAdd(&R->done, 1u) == np - 1) {  // the row's last piece: verify it
-          __threadfence();
-          const uint16_t TN = static_cast<uint16_t>(atomicOr(&R->tn, 0u));
-          const uint32_t CNT = atomicAdd(&R->cnt, 0u);
-          const uint32_t u = R->u, i = R->i;
-          const unsigned long long bit = 1ull << (i % kWave);
-          const uint16_t T = keep_bits(R->Ts, TN, s_adj);
-          if (T) {
-            tst[u] = T;
-            tnxt[u] = T;
-            malive[u] = CNT;
-            atomicOr(&mask_out[i / kWave], bit);
-            if (keep_out) atomicOr(&keep_out[i / kWave], bit);
-            if (oa.nranks <= 1) {
-              acc.vs += 1;
-              acc.es += CNT;
-            } else {
-              acc_owner(s_hist, oa, u, CNT);
-            }
+        const uint16_t TN = static_cast<uint16_t>(atomicOr(&R->tn, 0u));
+        const uint32_t CNT = atomicAdd(&R->cnt, 0u);
+        const uint32_t u = R->u, i = R->i;
+        const unsigned long long bit = 1ull << (i % kWave);
+        const uint16_t T = keep_bits(R->Ts, TN, s_adj);
+        R->T = T;
+        if (T) {
+          tst[u] = T;
+          tnxt[u] = T;
+          malive[u] = CNT;
+          atomicOr(&mask_out[i / kWave], bit);
+          if (keep_out) atomicOr(&keep_out[i / kWave], bit);
+          if (oa.nranks <= 1) {
+            acc.vs += 1;
+            acc.es += CNT;
           } else {
-            acc.removed = 1;
-            tnxt[u] = 0;
-            malive[u] = 0;
-            // (as the step kernel: right after superstep 0 a label of at most two template vertices is read
-            // through its codes, so the T_pub buffer read now is cleared at once and the row leaves the list)
-            bool cleared = false;
-            if (tcode) {
-              uint32_t tu = 0;
-              for (int l = 0; l < nruns; ++l)
-                if (u - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
-              const uint32_t rest = tu & (tu - 1);
-              if (!(rest & (rest - 1))) {
-                if (!has_srec) tcur[u] = 0;
-                cleared = true;
-              }
-            }
-            if (!cleared) atomicOr(&mask_out[i / kWave], bit);
+            acc_owner(s_hist, oa, u, CNT);
           }
+        } else {
+          acc.removed = 1;
+          tnxt[u] = 0;
+          malive[u] = 0;
+          // (as the step kernel: right after superstep 0 a label of at most two template vertices is read
+          // through its codes, so the T_pub buffer read now is cleared at once and the row leaves the list)
+          bool cleared = false;
+          if (tcode) {
+            uint32_t tu = 0;
+            for (int l = 0; l < nruns; ++l)
+              if (u - s_rlo[l] < s_rlen[l]) tu = s_rtu[l];
+            const uint32_t rest = tu & (tu - 1);
+            if (!(rest & (rest - 1))) {
+              if (!has_srec) tcur[u] = 0;
+              cleared = true;
+            }
+          }
+          if (!cleared) atomicOr(&mask_out[i / kWave], bit);
         }
       }
     }
   }
   acc.asym |= asym;
   flush_block(acc, oa, s_hist, s_red, pp);
+}
+
+// Packing of the listed rows that survived the call's last pull superstep (their pieces all in the scratch): one
+// block per row scans its pieces' counts and copies their alive entries to the row start, in order; mlen = |M|.
+__global__ __launch_bounds__(kBlock) void k_long_pack(LongList ll, uint32_t* __restrict__ mcol,
+                                                      uint32_t* __restrict__ mlen) {
+  __shared__ uint32_t s_w[kWpb];
+  __shared__ uint32_t s_carry;
+  const uint32_t nrows = static_cast<uint32_t>(min<unsigned long long>(*ll.cnt >> 32, ll.cap));
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const LongRow& R = ll.rows[r];
+    const uint32_t np = (R.len + kPullPiece - 1) / kPullPiece;
+    if (!R.T || R.pbase + np > ll.scr_pieces) continue;  // (block-uniform) removed, or not all in the scratch
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t q0 = 0; q0 < np; q0 += blockDim.x) {
+      const uint32_t q = q0 + threadIdx.x;
+      const uint32_t c = q < np ? ll.pcnt[R.pbase + q] : 0u;
+      const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(c));
+      if (lane == kWave - 1) s_w[w] = incl;
+      __syncthreads();
+      uint32_t wpre = 0, tot = 0;
+      for (int j = 0; j < kWpb; ++j) {
+        wpre += j < w ? s_w[j] : 0u;
+        tot += s_w[j];
+      }
+      const uint32_t base = s_carry;
+      __syncthreads();
+      if (threadIdx.x == 0) s_carry = base + tot;
+      // this thread's piece: c entries from its scratch slice to the row at base + wpre + incl - c
+      const uint32_t* src = ll.scr + (R.pbase + q) * uint64_t(kPullPiece);
+      uint32_t* dst = mcol + R.beg + base + wpre + incl - c;
+      for (uint32_t j = 0; j < c; ++j) dst[j] = src[j];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) mlen[R.u] = s_carry;
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2698,7 +2765,7 @@ void ensure_slist2(Ctx& c) {
 
 static constexpr unsigned kLongGrid = 2048;  // blocks of the long rows' pieces launch (8192 waves)
 
-void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
+void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0, bool last_of_call) {
   if (!c.d_kmask) PM_HIP_CHECK(hipMalloc(&c.d_kmask, ((c.n + 63) / 64 + 1) * sizeof(uint64_t)));
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   // first later superstep (every slist entry live): one chunk per wave, the
@@ -2721,17 +2788,30 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
   // spilled 13 / 31 VGPRs and ran 516-525 / 616-620 us against 513)
   if (first_after_ss0 && c.k1_records && c.d_srec) kern = short_rows ? k_lcc_step<3, true> : k_lcc_step<4, true>;
   // long rows in pieces (a second launch) where the previous search of this layout deferred some, or while that
-  // is not known; the counters are the slot's words 2P + 4 / 2P + 5 (zeroed with the slots)
+  // is not known; the counter is the slot's word 2P + 4 (zeroed with the slots).  The call's last pull superstep
+  // also packs them (k_long_pack) when the row compaction follows it.
   LongList ll{};
   const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
   const bool longs = !c.long_seen_off && (c.cur_ss >= c.long_seen.size() || c.long_seen[c.cur_ss]);
+  const bool pack = longs && last_of_call && !c.no_row_compaction;
   if (longs) {
     if (!c.d_lrows) {
       c.lrows_cap = 1u << 16;
       PM_HIP_CHECK(hipMalloc(&c.d_lrows, uint64_t(c.lrows_cap) * sizeof(LongRow)));
     }
     ll = LongList{static_cast<LongRow*>(c.d_lrows), reinterpret_cast<unsigned long long*>(d_slot + 2 * P + 4),
-                  c.lrows_cap, c.pull_long ? c.pull_long : kPullLong};
+                  c.lrows_cap, c.pull_long ? c.pull_long : kPullLong, nullptr, nullptr, 0};
+    if (pack) {
+      if (!c.d_lscr) {
+        const uint64_t pieces =  // (PM_PACK_PIECES: tests; read per context)
+            std::getenv("PM_PACK_PIECES") ? std::strtoull(std::getenv("PM_PACK_PIECES"), nullptr, 10) : (1u << 15);
+        c.lscr_pieces = std::max<uint64_t>(pieces, 1);
+        PM_HIP_CHECK(hipMalloc(&c.d_lscr, c.lscr_pieces * (kPullPiece + 1) * sizeof(uint32_t)));
+      }
+      ll.scr = static_cast<uint32_t*>(c.d_lscr);
+      ll.pcnt = ll.scr + c.lscr_pieces * kPullPiece;
+      ll.scr_pieces = c.lscr_pieces;
+    }
   }
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, c.stream, m_off(c), c.d_slist, c.d_nS, min, mout,
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
@@ -2746,6 +2826,10 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0) {
                        first_after_ss0 && c.k1_records && c.d_srec ? 1 : 0, mout,
                        reinterpret_cast<unsigned long long*>(c.d_kmask));
     PM_HIP_CHECK(hipGetLastError());
+    if (pack) {
+      hipLaunchKernelGGL(k_long_pack, dim3(256), dim3(kBlock), 0, c.stream, ll, m_col(c), c.d_mlen);
+      PM_HIP_CHECK(hipGetLastError());
+    }
   }
   c.removed_cleared = first_after_ss0 && c.k1_records;  // (its removed rows cleared the T_pub they read)
   c.k1_dense = false;  // every M row of S is in its padded row from here on

@@ -87,15 +87,20 @@ def test_exact_count_token_passing_matches_oracle(pat, scale, p_gen, alphabet, n
     assert sg["nlcc_edges"] == so["nlcc_edges"] and sg["tds_edges"] == so["tds_edges"]
 
 
-@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards", [("tree", 16, 4, None, 4, 0), ("cycle", 14, 4, None, 1, 0),
-                                                                    ("cycle", 12, 4, 8, 3, 0), ("cycle", 15, 4, 64, 1, 0),
-                                                                    ("tree", 15, 4, None, 2, 3), ("cycle", 13, 4, 8, 1, 2)])
-def test_pull_long_rows_in_pieces(pat, scale, p_gen, alphabet, nranks, shards, tmp_path, monkeypatch):
+@pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards,pack",
+                         [("tree", 16, 4, None, 4, 0, None), ("cycle", 14, 4, None, 1, 0, None),
+                          ("cycle", 12, 4, 8, 3, 0, None), ("cycle", 15, 4, 64, 1, 0, None),
+                          ("cycle", 15, 4, 64, 1, 0, 3), ("tree", 15, 4, None, 2, 3, None),
+                          ("cycle", 13, 4, 8, 1, 2, None)])
+def test_pull_long_rows_in_pieces(pat, scale, p_gen, alphabet, nranks, shards, pack, tmp_path, monkeypatch):
     """PM_PULL_LONG=8: every pull-superstep row above 8 entries goes to the long-row list and is worked in pieces by
-    k_lcc_step_pieces (the path of C5's hub rows, normally above 4096 entries), its verify by the row's last piece;
-    three searches per context (from the second on, the pieces launch runs only where the previous search listed
-    rows), and the sharded path, against the oracle."""
+    k_lcc_step_pieces (the path of C5's hub rows, normally above 4096 entries), its verify by the row's last piece,
+    and in the call's last superstep packed by k_long_pack (PM_PACK_PIECES=3: most rows do not fit the scratch and
+    are left to the row compaction); three searches per context (from the second on, the pieces launch runs only
+    where the previous search listed rows), and the sharded path, against the oracle."""
     monkeypatch.setenv("PM_PULL_LONG", "8")
+    if pack:
+        monkeypatch.setenv("PM_PACK_PIECES", str(pack))
     g = pm.rmat_graph(scale, p_gen)
     labels = None if alphabet is None else pmtest.hash_labels(g.n, alphabet)
     a = tmp_path / "oracle"

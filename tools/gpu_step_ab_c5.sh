@@ -24,7 +24,7 @@ for d in sorted(glob.glob("gpurun_out/c5ab_*/")):
         tot[n] = tot.get(n, 0) + dur
         if "k_lcc_step" in n:
             seq.append(round(dur))
-    top = sorted(tot.items(), key=lambda x: -x[1])[:8]
+    top = sorted(tot.items(), key=lambda x: -x[1])[:16]
     print(os.path.basename(d.rstrip("/")), "k_lcc_step:", seq)
     print("   top:", [(k, round(v)) for k, v in top])
 PY
