@@ -138,6 +138,9 @@ def main():
     ap.add_argument("--pmc", default=None, help="PMC summary of k_lcc_first (default: the newest profiles/r*_pmc_lcc_first.json)")
     ap.add_argument("--c3", choices=["auto", "off"], default="auto",
                     help="also time BASELINE config C3 (S=26, P_gen=4, 4-cycle: the token-passing stress) at N=1")
+    ap.add_argument("--sharded-n1", choices=["auto", "off"], default="auto",
+                    help="at N=1 also time the sharded path with one shard (one-rank RCCL communicator, the code every "
+                         "rank of an N-GPU run executes) on the same search")
     ap.add_argument("--nlcc", choices=["auto", "off"], default="auto",
                     help="also time the token-passing path with real work at N=1: config C5's search (S=27, "
                          "hash32(v ^ 5) % 256 labels, 4-cycle) on the GPU-generated graph, checked against "
@@ -421,6 +424,37 @@ def main():
             f"lines {nlcc['nlc_lines_ms_per_step']} ms ({nlcc['nlc_lines_share']:.0%}), fixture "
             f"{nlcc.get('fixture', {}).get('match')}")
 
+    # the sharded path at N=1: the same S=28 search through the code every rank of an N-GPU run executes (shard
+    # generation + owner routing, delegates' combine, code exchange, T_pub exchange, replica hand-off) with a
+    # one-rank RCCL communicator -- its fixed cost over the one-context step
+    sharded1 = None
+    if args.sharded_n1 == "auto" and world == 1 and not sharded:
+        uid1 = pm.comm_unique_id()
+        ms1, g1s = pm.rmat_shard_matcher(args.scale, args.p_gen, pattern_dir, 1, 0, uid1, device=0,
+                                         hub_threshold=args.hub_threshold)
+        for _ in range(max(args.warmup, 1)):
+            ms1.run_beta("", args.max_iterations)
+        raw1 = [_abi.RunStats() for _ in range(args.steps)]
+        t1 = time.perf_counter()
+        for st1 in raw1:
+            ms1.run_beta_into(st1, args.max_iterations)
+        e1 = (time.perf_counter() - t1) / args.steps
+        l1 = raw1[-1].as_dict()
+        info1 = ms1.comm_info()
+        ms1.close()
+        same = all(l1[k] == s0[k] for k in ("lcc_edges", "nlcc_edges", "tds_edges", "walks", "final_vertices",
+                                            "final_edges", "iterations"))
+        if not same:
+            invalid.append("the sharded path at N=1 differs from the one-context search")
+        sharded1 = {"ms_per_step": round(e1 * 1e3, 4), "value": round(edges_of(l1) / e1, 1), "unit": "edges/s",
+                    "over_one_context": round(e1 / (elapsed / args.steps), 4), "steps": args.steps,
+                    "transport": info1["transport"], "comm_ranks": info1["comm_ranks"],
+                    "comm_calls_per_search": l1["comm_calls"], "comm_bytes": l1["comm_bytes"],
+                    "replica_rows": l1["replica_rows"], "shard_sharded_ms": round(l1["shard_sharded_ms"], 4),
+                    "same_counters_as_one_context": same, "generate_and_route_s": round(g1s, 3)}
+        log(f"sharded path at N=1: {sharded1['ms_per_step']} ms/step ({sharded1['over_one_context']}x the one-context "
+            f"step), {l1['comm_calls']} collectives")
+
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -515,6 +549,7 @@ def main():
         "c3_config": c3,
         "nlcc_config": nlcc,
         "shards": shards,
+        "sharded_n1": sharded1,
         # one-time work outside the timed region (the reference's graph load + label init analogue)
         "setup_s": setup,
     }

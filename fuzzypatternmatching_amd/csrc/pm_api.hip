@@ -365,6 +365,8 @@ static void destroy_ctx(pm_ctx* c) {
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->ev_handoff) (void)hipEventDestroy(c->ev_handoff);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->rstream) (void)hipStreamDestroy(c->rstream);
+  if (c->ev_rb) (void)hipEventDestroy(c->ev_rb);
   delete c;
 }
 
@@ -520,7 +522,9 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
     uint64_t* slot = c.d_counts + ss * W;
     if (ss == 0 && init_step) {
       if (c.lcc_started) throw std::runtime_error("init_step LCC after the state map was built");
-      launch_lcc_first(c, slot, ev[D + 1], ev[D + 2]);
+      // (the call's start event ev[0] directly precedes the kernel -- the search's fills were flushed before it --
+      // so it also opens the kernel's own interval: one event record less before superstep 0)
+      launch_lcc_first(c, slot, nullptr, ev[D + 2]);
       c.probe("superstep 0 launched");
       debug_point(c, "superstep 0"); debug_watch(c, "superstep 0");
       k_timed = true;
@@ -573,16 +577,32 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   c.probe("lcc issued");
   // read-back through pinned memory: [nS | local counts | summed counts]
   uint64_t* pin = pinned(c, 1 + 2 * D * W);
-  PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));  // + stamp
   // sharded: the supersteps before the replica counted this shard's rows only: their slots are summed
   // over the shards (the replica's supersteps count the whole state on every shard)
   const uint64_t sharded_slots = c.comm && init_step ? handoff_ss + 1 : 0;
+  // one context with prelaunched lines: the read-back copies go on a side stream ordered after the call's last
+  // kernel, so they run beside the lines instead of in front of them (the lines read neither the list count nor
+  // the counters, and the host waits for both)
+  const bool side = c.prelaunch_lines && !sharded_slots;
+  hipStream_t rs = c.stream;
+  if (side) {
+    if (!c.rstream) {
+      PM_HIP_CHECK(hipStreamCreateWithFlags(&c.rstream, hipStreamNonBlocking));
+      PM_HIP_CHECK(hipEventCreateWithFlags(&c.ev_rb, hipEventDisableTiming));
+    }
+    PM_HIP_CHECK(hipEventRecord(c.ev_rb, c.stream));
+    PM_HIP_CHECK(hipStreamWaitEvent(c.rstream, c.ev_rb, 0));
+    rs = c.rstream;
+    prelaunch_lines_fused(c);  // the device goes on with the lines while the host parses
+  }
+  PM_HIP_CHECK(hipMemcpyAsync(pin, c.d_nS, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, rs));  // + stamp
   if (sharded_slots) {  // this shard's counts, then the sums over the shards
     PM_HIP_CHECK(hipMemcpyAsync(pin + 1, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     c.comm->allreduce_sum_u64(c.d_counts, sharded_slots * W, c.stream);
   }
-  PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
-  if (c.prelaunch_lines) prelaunch_lines_fused(c);  // the device goes on with the lines while the host parses
+  PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, rs));
+  if (c.prelaunch_lines && !side) prelaunch_lines_fused(c);
+  if (side) stream_wait(c.rstream);
   debug_point(c, "counters + prelaunched lines");
   stream_wait(c.stream);
   c.probe("lcc synced");
@@ -645,7 +665,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   }
   if (k_timed) {
     float ms = 0.f;
-    PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[D + 1], ev[D + 2]));
+    PM_HIP_CHECK(hipEventElapsedTime(&ms, ev[0], ev[D + 2]));
     c.lcc_first_ms = ms;
   }
   if (handed_off) {  // minus the collectives' host time, during which the stream idles (in-process shards wait

@@ -268,6 +268,8 @@ struct LineDesc {
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t rstream = nullptr;    // read-backs that overlap the next kernels of `stream` (created on first use)
+  hipEvent_t ev_rb = nullptr;       // ... ordered after this event of `stream`
   uint64_t n = 0, nnz = 0;
   bool symmetric = true;
   uint32_t nranks = 1;

@@ -1257,7 +1257,7 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   static_assert(((kGbarWords + 64) * sizeof(unsigned)) % alignof(LineStats) == 0, "LineStats alignment");
   static_assert(sizeof(LineStats) % sizeof(unsigned) == 0, "LineStats size");
   if (!c.d_lstats) {
-    const size_t words = kGbarWords + 64 + std::max<size_t>(nl_all, 1) * (sizeof(LineStats) / sizeof(unsigned));
+    const size_t words = kGbarWords + 64 + std::max<size_t>(nl_all, 1) * (sizeof(LineStats) / sizeof(unsigned)) + 16;
     c.d_gbar = dmalloc<unsigned>(words);
     PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, words * sizeof(unsigned), c.stream));
     c.d_lstats = reinterpret_cast<LineStats*>(c.d_gbar + kGbarWords + 64);
@@ -1279,7 +1279,8 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   unsigned* d_done = c.d_gbar + kGbarWords;                                   // [0] lines done
   auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
   const size_t ctl_bytes = 64 * sizeof(unsigned) + nl * sizeof(LineStats);  // control words + stats of lines < nl
-  PM_HIP_CHECK(hipMemsetAsync(d_done, 0, ctl_bytes, c.stream));
+  // (the fill rounded up to 64 B -- the buffer has the slack: one fill kernel instead of an aligned part and a tail)
+  PM_HIP_CHECK(hipMemsetAsync(d_done, 0, (ctl_bytes + 63) & ~size_t(63), c.stream));
   LineKernelArgs a{};
   a.offp = m_off(c);
   a.mcol = m_col(c);
