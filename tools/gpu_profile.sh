@@ -13,7 +13,7 @@ SCALE=${SCALE:-28}
 PGEN=${PGEN:-8}
 if [ "${SKIP_STATS:-0}" != 1 ]; then
   PM_LINES_NOCOOP=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-    python3 bench.py --steps 5 --warmup 2 --cpu-baseline off --fixture-check off --c3 off --nlcc off > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.log
+    python3 bench.py --steps 5 --warmup 2 --cpu-baseline off --fixture-check off --c3 off --nlcc off --sharded-n1 off > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.log
   rc=$?; echo "rocprof stats rc=$rc"; tail -2 gpurun_out/prof_$TAG.log
   [ $rc -eq 0 ] || exit $rc
 fi
@@ -38,7 +38,7 @@ if [ "${SKIP_STEP:-0}" != 1 ]; then
   for ctr in "$G1" "$G2" "$G4" "$G5"; do
     i=$((i+1))
     PM_LINES_NOCOOP=1 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $ctr --kernel-include-regex "k_lcc_step" --output-format csv \
-      -d gpurun_out/pmcstep_${TAG}_$i -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline off --fixture-check off --c3 off --nlcc off \
+      -d gpurun_out/pmcstep_${TAG}_$i -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline off --fixture-check off --c3 off --nlcc off --sharded-n1 off \
       > gpurun_out/pmcstep_${TAG}_$i.log 2>&1
     rc=$?; echo "k_lcc_step pmc pass $i ($ctr) rc=$rc"
     [ $rc -eq 0 ] || exit $rc
