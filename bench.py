@@ -106,6 +106,16 @@ def launch_ranks(n, argv):
     return subprocess.run(cmd, env=rank_launch_env()).returncode
 
 
+def line_stream():
+    """The stream the JSON line goes to: this process's original stdout.  File descriptor 1 itself is pointed at
+    stderr, so whatever the libraries write there (RCCL's version banner at communicator creation, on every rank)
+    cannot come before or between the JSON lines of a run."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def spread(vals):
     vals = [float(v) for v in vals]
     mean = sum(vals) / len(vals) if vals else 0.0
@@ -153,6 +163,7 @@ def main():
     if env_world is not None and int(env_world) != args.gpus:
         log(f"bench.py: launched with WORLD_SIZE={env_world} but --gpus {args.gpus}; the line would mislabel the run")
         return 2
+    out_stream = line_stream()  # (after the launcher branch: its ranks inherit the real stdout)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -557,7 +568,7 @@ def main():
         for x in invalid:
             log("PARITY FAILURE: " + x)
         out["invalid"] = " | ".join(invalid)
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=out_stream, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -553,7 +553,7 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         // entries inside the superstep, one counter reservation per 64-entry chunk, measured 1.2 ms slower
         // at S=28: 153 k atomics on one address serialise.)
         c.cur_ss = init_step ? ss : 0;
-        launch_lcc_step(c, slot, init_step && ss == 1, ss + 1 == D);
+        launch_lcc_step(c, slot, init_step && ss == 1, ss + 1 == D, init_step);
         debug_point(c, "pull superstep"); debug_watch(c, "pull superstep");
         if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
         debug_point(c, "list compaction"); debug_watch(c, "list compaction");

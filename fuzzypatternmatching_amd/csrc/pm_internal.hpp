@@ -566,7 +566,9 @@ void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slo
 unsigned lcc_first_grid(const Ctx& c);
 // first_after_ss0: the superstep right after superstep 0 of the first call
 // (T_pub is still superstep 0's output: neighbours' T_pub from the 2-bit codes)
-void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false, bool last_of_call = false);
+// pub_state: the first LCC call (T_state == T_pub for every member of S; its alive count is counted, not loaded)
+void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0 = false, bool last_of_call = false,
+                     bool pub_state = false);
 void ensure_slist2(Ctx& c);
 // Push form of a later superstep (send + verify launches): directed inputs and
 // LCC calls after the first (M may be asymmetric there).

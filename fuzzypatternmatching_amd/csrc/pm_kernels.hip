@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
     const uint4* __restrict__ srec, uint64_t dbase, unsigned long long* __restrict__ keep_out, RecSrc rs,
-    uint32_t* __restrict__ slist_out, LongList ll) {
+    uint32_t* __restrict__ slist_out, LongList ll, int pub_state) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1192,6 +1192,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t nS = *nSp;
   const uint64_t nchunks = (uint64_t(nS) + kWave - 1) / kWave;
+  // the first LCC call (pub_state): a member's T_state equals its T_pub -- every superstep writes both, only the
+  // NLC post-processing after the call clears T_pub bits alone -- and its alive count is the number of its alive
+  // entries, which the walk counts: two of the five scattered state loads per row (T_state, |M| alive) are not
+  // made (the second later superstep at S=28 is bound by random line fetches, ~5 per row)
+  const bool derive = pub_state && !FIRST && !srec;
   // one chunk of 64 slist entries (live: the chunk's live mask, non-zero)
   auto chunk_body = [&](uint64_t chunk, uint64_t live) {
     const uint64_t i = chunk * kWave + lane;
@@ -1241,8 +1246,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       uint32_t a0 = l;
       if (dm == kNone) {
         b = offp[u];
-        a0 = (diag & 16) ? l : malive[u];  // (timing variant: two of the row's scattered state loads dropped)
-        Ts = (diag & 16) ? Tu : tst[u];
+        // (timing variant diag 16: the same two loads dropped without the count: results wrong)
+        a0 = derive ? 0u : (diag & 16) ? l : malive[u];
+        Ts = derive || (diag & 16) ? Tu : tst[u];
       } else {
         Ts = Tu;
       }
@@ -1280,6 +1286,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       }
     }
     uint32_t tn = 0, cnt = 0;
+    uint32_t talive = 0;  // (derive) alive entries this lane walked: the superstep's traversed count
     bool asym = false;
     // short rows: flattened over the wave -- the chunk's rows are concatenated
     // and every lane takes every 64th entry (four in flight), so a chunk costs
@@ -1325,6 +1332,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         for (int q = 0; q < U; ++q)
           if (m[q] & kAlive) {
             uint32_t tq = 0, cq = 0;
+            ++talive;
             k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym, !(diag & 4));
             if (tq) atomicOr(&s_tn[w][rr[q]], tq);
             if (cq) atomicAdd(&s_cnt[w][rr[q]], cq);
@@ -1357,7 +1365,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         for (int q = 0; q < 4; ++q) tv[q] = (m[q] & kAlive) ? tpub_of(m[q] & kPosMask) : uint16_t(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (m[q] & kAlive) k2_entry(mcol, br + j0 + q * kWave + lane, m[q], tv[q], nmr, tnr, cntr, asym, !(diag & 4));
+          if (m[q] & kAlive) {
+            ++talive;
+            k2_entry(mcol, br + j0 + q * kWave + lane, m[q], tv[q], nmr, tnr, cntr, asym, !(diag & 4));
+          }
       }
       tnr = wave_or32(tnr);
       cntr = static_cast<uint32_t>(wave_sum(cntr));
@@ -1451,7 +1462,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     // keep_out: the survivors (T_pub just written != 0), the list compaction's keep mask
     const uint64_t km = __ballot(survivor);
     if (keep_out && lane == 0) keep_out[chunk] = km;
-    acc.trav += alive0;
+    acc.trav += derive ? talive : alive0;
     acc.removed |= removed;
     acc.asym |= asym;
     if (survivor) {
@@ -1507,7 +1518,8 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step_pieces(LongList ll, uint16_
                                                             Partials pp, const uint32_t* __restrict__ tcode,
                                                             LabelRuns lr, int has_srec,
                                                             unsigned long long* __restrict__ mask_out,
-                                                            unsigned long long* __restrict__ keep_out) {
+                                                            unsigned long long* __restrict__ keep_out,
+                                                            int count_trav) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1574,7 +1586,10 @@ __global__ __launch_bounds__(kBlock) void k_lcc_step_pieces(LongList ll, uint16_
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         uint32_t c1 = 0;
-        if (m[t] & kAlive) k2_entry(mcol, beg + jb + t * kWave + lane, m[t], tv[t], nm, tn, c1, asym);
+        if (m[t] & kAlive) {
+          if (count_trav) ++acc.trav;  // (the step kernel did not load the row's alive count)
+          k2_entry(mcol, beg + jb + t * kWave + lane, m[t], tv[t], nm, tn, c1, asym);
+        }
         cnt += c1;
         if (pack) {  // (entries stay in row order: component t covers jb + 64 t .. jb + 64 t + 63)
           const uint64_t b = __ballot(c1 != 0);
@@ -2765,7 +2780,7 @@ void ensure_slist2(Ctx& c) {
 
 static constexpr unsigned kLongGrid = 2048;  // blocks of the long rows' pieces launch (8192 waves)
 
-void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0, bool last_of_call) {
+void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0, bool last_of_call, bool pub_state) {
   if (!c.d_kmask) PM_HIP_CHECK(hipMalloc(&c.d_kmask, ((c.n + 63) / 64 + 1) * sizeof(uint64_t)));
   const uint64_t chunks = (uint64_t(c.nS_host) + kWave - 1) / kWave;
   // first later superstep (every slist entry live): one chunk per wave, the
@@ -2817,14 +2832,15 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0, bool last_o
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                      c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,
-                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist, ll);
+                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist, ll, pub_state ? 1 : 0);
   PM_HIP_CHECK(hipGetLastError());
   if (longs) {
     hipLaunchKernelGGL(k_lcc_step_pieces, dim3(kLongGrid), dim3(kBlock), 0, c.stream, ll, c.d_tpub[c.cur],
                        c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_malive,
                        partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                        first_after_ss0 && c.k1_records && c.d_srec ? 1 : 0, mout,
-                       reinterpret_cast<unsigned long long*>(c.d_kmask));
+                       reinterpret_cast<unsigned long long*>(c.d_kmask),
+                       pub_state && !(first_after_ss0 && c.k1_records && c.d_srec) ? 1 : 0);
     PM_HIP_CHECK(hipGetLastError());
     if (pack) {
       hipLaunchKernelGGL(k_long_pack, dim3(256), dim3(kBlock), 0, c.stream, ll, m_col(c), c.d_mlen);
