@@ -118,6 +118,7 @@ class RunStats(ctypes.Structure):
         ("replica_rows", c_u64),
         ("replica_entries", c_u64),
         ("comm_seconds", ctypes.c_double),
+        ("path_batches", c_u64),
     ]
 
     def as_dict(self):

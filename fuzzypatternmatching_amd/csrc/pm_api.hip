@@ -282,6 +282,9 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
     if (in.inprocess_shards > 1)  // in-process shard groups share one device
       arena = std::min<size_t>(arena, std::max<size_t>(size_t(1) << 30, free_b / (2 * in.inprocess_shards)));
     arena = std::max<size_t>(arena, size_t(64) << 20);
+    // PM_ARENA_MB=<MiB> (tests): a smaller arena (the exact path lines' source batches)
+    if (const char* e = std::getenv("PM_ARENA_MB"))
+      arena = std::min<size_t>(arena, std::max<size_t>(1, std::strtoull(e, nullptr, 10)) << 20);
   } catch (const std::exception& e) {
     build_err = e.what();
     arena = 0;
@@ -354,7 +357,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit, c->d_push,
-                  c->d_lrows, c->d_lscr,
+                  c->d_lrows, c->d_lscr, c->d_clstat,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -405,6 +408,7 @@ static void reset_state(Ctx& c, bool defer = false) {
   // d_tsm needs no reset: only sources are read, and selecting a source resets its entry
   c.smask_valid = false;
   zero_later(c, c.d_flags, 4 * sizeof(uint32_t));
+  queue_lines_ctl_clear(c);
   if (!defer) flush_zero(c);
   c.cur = 0;
   c.nS_host = 0;
@@ -993,6 +997,7 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
             s.tds_chunks += c.last_tds_chunks;
           } else {
             tr = run_path_line(c, line);
+            s.path_batches += tr.batches;
           }
           ph_tp += since(t1);
           auto t2 = tick();

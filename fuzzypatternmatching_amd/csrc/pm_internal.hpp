@@ -91,13 +91,17 @@ struct Comm {
   virtual int transport() const = 0;  // PM_TRANSPORT_* (pm_abi.h)
 };
 
-// Device scratch arena (bump allocator, reset per NLC line).
+// Device scratch arena (bump allocator, reset per NLC line).  A request past its end throws ArenaFull (the exact
+// path-line enumeration catches it and retries in smaller source batches).
+struct ArenaFull : std::runtime_error {
+  ArenaFull() : std::runtime_error("device scratch arena exhausted") {}
+};
 struct Arena {
   char* base = nullptr;
   size_t cap = 0, used = 0;
   void* get(size_t bytes) {
     size_t a = (used + 255) & ~size_t(255);
-    if (a + bytes > cap) throw std::runtime_error("device scratch arena exhausted");
+    if (a + bytes > cap) throw ArenaFull();
     used = a + bytes;
     return base + a;
   }
@@ -401,6 +405,10 @@ struct Ctx {
   void* d_ctmp = nullptr;
   size_t ctmp_bytes = 0;
   uint64_t ccap = 0;              // chunk capacity of d_ccnt / d_cbase
+  // list compaction (k_compact_scan): tile status words, their capacity, the launch epoch, the co-resident grid
+  void* d_clstat = nullptr;
+  uint64_t clstat_cap = 0, cl_epoch = 0;
+  unsigned cl_grid = 0;
   bool slist_compacted = false;   // d_slist holds S only (shorter than the host bound nS_host)
   // live mask of slist per 64 entries, written by every later superstep
   // (members of S plus vertices removed in that superstep): later passes
@@ -503,6 +511,7 @@ struct Ctx {
   bool push_long = true;   // some row of S may be longer than a push-form piece (unknown: true)
   uint32_t* d_front = nullptr;    // slots inserted by a fused path line (cleared by it)
   unsigned* d_gbar = nullptr;     // grid barrier state of the fused line kernels
+  bool lines_ctl_clean = false;   // the line launches' control words are zero (the search's fills cleared them)
   unsigned line_grid = 0;         // blocks of a full-chip line launch (one per CU)
   uint64_t live_hint = ~0ull;     // S members on this context after the last LCC call (line grid size)
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
@@ -593,6 +602,7 @@ static constexpr unsigned kPartGridMax = 2048;
 
 struct TpResult {
   uint64_t sources = 0, acked = 0, edges = 0, tokens = 0, walks = 0;
+  uint64_t batches = 0, batch_retries = 0;  // exact path lines: initiator batches run, and those that did not fit
 };
 TpResult run_path_line(Ctx& c, const NlcLine& line);
 // Output of one line of the fused kernel (token passing + post-processing).
@@ -622,6 +632,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
 // (the first LCC call of a search, whose lines always run: beta.cpp:686-688); the
 // next run_lines_fused(c, 0, ...) then only waits for it and reads its results.
 void prelaunch_lines_fused(Ctx& c);
+void queue_lines_ctl_clear(Ctx& c);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 // The same with the kept walks handed to `sink` chunk by chunk (positions, stride C+2 each) instead of

@@ -1158,6 +1158,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   __shared__ uint32_t s_end[kWpb][kWave], s_tn[kWpb][kWave], s_cnt[kWpb][kWave];
   __shared__ uint16_t s_nm[kWpb][kWave];
   __shared__ uint64_t s_dst[kWpb][kWave];  // dense survivors' padded row starts (flattened copy)
+  // FIRST: the flattened dense rows' entries are not updated in place -- their alive bits after the walk (bit t of the
+  // walk) go to LDS and the survivors' row moves apply them; a removed row's dense entries are never read again
+  constexpr int kAlvWords = kWave * kLprMax / 64 + 4;
+  __shared__ unsigned long long s_alv[FIRST ? kWpb : 1][FIRST ? kAlvWords : 1];
+  __shared__ uint32_t s_wofs[FIRST ? kWpb : 1][FIRST ? kWave : 1];  // the row's first walk entry (~0: stored in place)
   __shared__ uint32_t s_rlo[16], s_rlen[16], s_rtu[16], s_rcd[16];
   for (int i = threadIdx.x; i < 2 * kMaxRanks; i += blockDim.x) s_hist[i] = 0;
   load_adj(s_adj, pa);
@@ -1296,6 +1301,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     const uint32_t ls = lng ? 0u : len;
     const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(ls));
     const uint32_t total = static_cast<uint32_t>(__shfl(incl, kWave - 1, kWave));
+    uint64_t dmask = 0;  // (FIRST) flattened dense rows: updates deferred to the row moves
+    if constexpr (FIRST) {
+      const bool dfr = drow && ls > 0 && !(diag & 4);
+      dmask = __ballot(dfr);
+      s_wofs[w][lane] = dfr ? incl - ls : ~0u;
+    }
     if (total) {
       s_end[w][lane] = incl;
       s_beg[w][lane] = beg;
@@ -1329,14 +1340,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         for (int q = 0; q < U; ++q)
           tv[q] = (m[q] & kAlive) ? ((diag & 1) ? uint16_t(m[q] & 0x7Fu) : tpub_of(m[q] & kPosMask)) : uint16_t(0);
 #pragma unroll
-        for (int q = 0; q < U; ++q)
+        for (int q = 0; q < U; ++q) {
+          const bool dr = FIRST && ((dmask >> rr[q]) & 1ull) && t0 + q * kWave + lane < total;
+          uint32_t cq = 0;
           if (m[q] & kAlive) {
-            uint32_t tq = 0, cq = 0;
+            uint32_t tq = 0;
             ++talive;
-            k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym, !(diag & 4));
+            k2_entry(mcol, e[q], m[q], tv[q], s_nm[w][rr[q]], tq, cq, asym, !(diag & 4) && !dr);
             if (tq) atomicOr(&s_tn[w][rr[q]], tq);
             if (cq) atomicAdd(&s_cnt[w][rr[q]], cq);
           }
+          if constexpr (FIRST) {  // (walk entries t0 + 64 q .. + 63: one word)
+            const uint64_t av = __ballot(dr && cq != 0);
+            if (dmask && lane == 0 && (t0 >> 6) + q < static_cast<uint32_t>(kAlvWords)) s_alv[w][(t0 >> 6) + q] = av;
+          }
+        }
       }
       __builtin_amdgcn_wave_barrier();
       tn = s_tn[w][lane];
@@ -1445,6 +1463,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
               const uint32_t j = t - (lo ? s_end[w][lo - 1] : 0u);
               x[q] = mcol[s_beg[w][lo] + j];
               d[q] = s_dst[w][lo] + j;
+              if constexpr (FIRST) {  // a deferred row: its alive bits from the walk
+                const uint32_t wo = s_wofs[w][lo];
+                if (wo != ~0u) {
+                  const uint32_t tw = wo + j;
+                  x[q] = (x[q] & kPosMask) | (((s_alv[w][tw >> 6] >> (tw & 63u)) & 1ull) ? kAlive : 0u);
+                }
+              }
             }
           }
 #pragma unroll
@@ -2643,6 +2668,69 @@ __global__ void k_chunk_slices(const uint64_t* rofs_in, const uint32_t* __restri
   }
 }
 
+// The same in one launch with the slices' scan (round 6: it replaces the library scan's two launches): every block
+// scans the W <= 8192 slice counts in LDS (32 KB, read from L2), block 0 writes rofs[0..W] and the list count, and
+// the blocks share the chunk descriptors.
+static constexpr uint32_t kRsMaxW = 8192;
+__global__ __launch_bounds__(kBlock) void k_record_slices(const uint32_t* __restrict__ rcnt,
+                                                          const uint64_t* __restrict__ rbase, uint32_t W,
+                                                          uint64_t* __restrict__ rofs, uint4* __restrict__ cdesc,
+                                                          uint32_t* __restrict__ nS) {
+  // (counts staged coalesced, one pad word per 32 so that a thread's 32 consecutive counts sit in distinct banks;
+  // the offsets then overwrite them -- the block barrier of the scan lies between)
+  __shared__ uint32_t s_buf[kRsMaxW + kRsMaxW / 32];
+  uint32_t* const s_pad = s_buf;
+  uint32_t* const s_ofs = s_buf;
+  __shared__ uint32_t s_w[kWpb];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  constexpr uint32_t per = kRsMaxW / kBlock;  // consecutive counts per thread
+#pragma unroll
+  for (uint32_t q = 0; q < per; ++q) {
+    const uint32_t i = q * kBlock + tid;
+    s_pad[i + i / 32] = i < W ? rcnt[i] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[per];
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < per; ++q) {
+    const uint32_t i = tid * per + q;
+    v[q] = s_pad[i + i / 32];
+    sum += v[q];
+  }
+  const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(sum));
+  if (lane == kWave - 1) s_w[w] = incl;
+  __syncthreads();
+  uint32_t o = incl - sum;
+  for (int j = 0; j < w; ++j) o += s_w[j];
+#pragma unroll
+  for (uint32_t q = 0; q < per; ++q) {
+    s_ofs[tid * per + q] = o;
+    o += v[q];
+  }
+  if (tid == kBlock - 1) s_ofs[kRsMaxW] = o;  // (the total: every count past W is 0)
+  __syncthreads();
+  const uint32_t total = s_ofs[kRsMaxW];
+  if (blockIdx.x == 0) {
+    for (uint32_t i = tid; i <= W; i += kBlock) rofs[i] = i < W ? s_ofs[i] : total;
+    if (tid == 0) *nS = total;
+  }
+  const uint64_t nch = (uint64_t(total) + kWave - 1) / kWave;
+  for (uint64_t ch = blockIdx.x * uint64_t(kBlock) + tid; ch < nch; ch += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t o0 = static_cast<uint32_t>(ch * kWave);
+    uint32_t lo = 0, hi = W - 1;  // the last slice starting at or before o0 (empty slices share offsets)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_ofs[mid] <= o0) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint32_t end = lo + 1 < W ? s_ofs[lo + 1] : total;
+    const uint64_t b = rbase[lo] + (o0 - s_ofs[lo]);
+    cdesc[ch] = make_uint4(static_cast<uint32_t>(b), static_cast<uint32_t>(b >> 32), min(uint32_t(kWave), end - o0),
+                           lo + 1);
+  }
+}
+
 // heavy-row scratch, heavy records and the 2-bit codes of a superstep-0 launch (queued with the search's reset)
 void queue_lcc_first_fills(Ctx& c) {
   if (c.ntiles == 0) return;
@@ -2675,17 +2763,26 @@ void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) 
   c.smask_valid = false;
   if (c.k1_records) {
     // slist = the records of the waves' slices (wave order), then the heavy survivors
-    rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> rit(c.d_rcnt, Widen());
-    size_t tb = c.rscan_tmp_bytes;
-    PM_HIP_CHECK(rocprim::exclusive_scan(c.d_rscan_tmp, tb, rit, c.d_rofs, uint64_t(0), size_t(c.rwaves),
-                                         rocprim::plus<uint64_t>(), c.stream));
     // the first later superstep reads the records in place (no copy); a sharded context whose labels need the
     // wide code exchange packs every survivor's T_pub from the records before that superstep, so it copies
     c.records_in_place = !c.comm || !c.xcode_wide;
+    static const bool lib_scan = std::getenv("PM_RSCAN_LIB") && std::string(std::getenv("PM_RSCAN_LIB")) == "1";
+    // (32-bit offsets: the records are light rows, fewer than 2^32)
+    const bool one = c.records_in_place && c.rwaves <= kRsMaxW && c.rarea_cap < (1ull << 32) && !lib_scan;
+    if (!one) {
+      rocprim::transform_iterator<const uint32_t*, Widen, uint64_t> rit(c.d_rcnt, Widen());
+      size_t tb = c.rscan_tmp_bytes;
+      PM_HIP_CHECK(rocprim::exclusive_scan(c.d_rscan_tmp, tb, rit, c.d_rofs, uint64_t(0), size_t(c.rwaves),
+                                           rocprim::plus<uint64_t>(), c.stream));
+    }
     if (c.records_in_place) {
       if (!c.d_cdesc) PM_HIP_CHECK(hipMalloc(&c.d_cdesc, (c.rarea_cap / kWave + 2) * sizeof(uint4)));
-      hipLaunchKernelGGL(k_chunk_slices, dim3(grid_for(c.rarea_cap / kWave + 1, kBlock, 1024)), dim3(kBlock), 0,
-                         c.stream, c.d_rofs, c.d_rcnt, c.d_rbase, c.rwaves, c.d_rofs, c.d_cdesc, c.d_nS);
+      if (one)  // (PM_RSCAN_LIB=1: the library scan and k_chunk_slices, A/B)
+        hipLaunchKernelGGL(k_record_slices, dim3(grid_for(c.rarea_cap / kWave + 1, kBlock, 256)), dim3(kBlock), 0,
+                           c.stream, c.d_rcnt, c.d_rbase, c.rwaves, c.d_rofs, c.d_cdesc, c.d_nS);
+      else
+        hipLaunchKernelGGL(k_chunk_slices, dim3(grid_for(c.rarea_cap / kWave + 1, kBlock, 1024)), dim3(kBlock), 0,
+                           c.stream, c.d_rofs, c.d_rcnt, c.d_rbase, c.rwaves, c.d_rofs, c.d_cdesc, c.d_nS);
     } else {
       hipLaunchKernelGGL(k_slist_from_records, dim3(grid_for(c.rwaves, kWpb, 8192)), dim3(kBlock), 0, c.stream,
                          c.d_rarea, c.d_rbase, c.d_rcnt, c.d_rofs, c.rwaves, c.d_srec, c.d_slist, c.d_nS);
@@ -2993,6 +3090,131 @@ __global__ void k_live_write(const uint32_t* __restrict__ slist, const unsigned 
   if (nS == 0 && blockIdx.x == 0 && threadIdx.x == 0) *nS_out = 0;
 }
 
+// List compaction in two launches (round 6; the four above: keep counts, the two scan passes, the write).
+// k_compact_scan: tile b = chunks [256 b, 256 b + 256): their kept counts and block scan, the tile's offset in the
+// new list by a decoupled look-back over the tiles before it, each chunk's first kept slot (cbase) and, after the
+// first later superstep, the T_pub clears of its few removed entries.  Status word of a tile: epoch << 40 | flag << 38
+// | value (flag 1: the tile's own count, 2: its inclusive offset); the epoch (the launch's number, never 0) tells a
+// word of this launch from an older one, so the words are never cleared.  (A block ticket taken with one atomic per
+// block -- the usual way to order the look-back -- cost 60 us for 600 blocks: same-address atomics serialise; the
+// grid is a cooperative launch instead, every block resident, each walking its tiles in increasing order.)
+// k_compact_write: the kept entries to the new list (and, PER_ENTRY, the clears of the removed ones) with every CU
+// busy: a wave takes 16 chunks and requests their 16 entries per lane before any store.  (One launch doing both ran
+// 83-86 us per compaction at S=28: 49-600 blocks walking their entries could not keep the memory system busy.)
+static constexpr uint32_t kClEpochBits = 24;
+__device__ __forceinline__ unsigned long long cl_word(uint64_t epoch, uint32_t flag, uint64_t v) {
+  return (epoch << 40) | (uint64_t(flag) << 38) | v;
+}
+template <bool PER_ENTRY>
+__global__ __launch_bounds__(kBlock) void k_compact_scan(const uint32_t* __restrict__ slist,
+                                                         const unsigned long long* __restrict__ mask,
+                                                         const unsigned long long* __restrict__ keep,
+                                                         const uint32_t* __restrict__ nSp, uint64_t cap,
+                                                         uint16_t* __restrict__ told, uint32_t* __restrict__ cbase,
+                                                         uint32_t* __restrict__ nS_out, unsigned long long* status,
+                                                         uint64_t epoch) {
+  __shared__ uint32_t s_w[kWpb];
+  __shared__ uint64_t s_base;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const uint64_t nch = min(cap, (static_cast<uint64_t>(*nSp) + kWave - 1) / kWave);
+  const uint64_t nblk = (nch + kBlock - 1) / kBlock;
+  if (nch == 0 && blockIdx.x == 0 && tid == 0) *nS_out = 0;
+  // tiles of 256 chunks in increasing order per block; the grid is co-resident (cooperative launch), so the tile a
+  // look-back waits for is always being worked on
+  for (uint64_t bid = blockIdx.x; bid < nblk; bid += gridDim.x) {
+    const uint64_t c = bid * kBlock + tid;
+    unsigned long long k = 0, g = 0;
+    if (c < nch) {  // (mask and keep bits of entries past the list's end are 0)
+      k = keep[c];
+      g = mask[c] & ~k;
+    }
+    const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(k));
+    const uint32_t incl = static_cast<uint32_t>(wave_incl_scan(cnt));
+    if (lane == kWave - 1) s_w[w] = incl;
+    __syncthreads();
+    uint32_t wpre = 0, agg = 0;
+    for (int j = 0; j < kWpb; ++j) {
+      wpre += j < w ? s_w[j] : 0u;
+      agg += s_w[j];
+    }
+    if (w == 0) {  // look-back: 64 tiles per poll, back to the nearest one whose inclusive offset is out
+      uint64_t excl = 0;
+      if (bid > 0) {
+        if (lane == 0)
+          __hip_atomic_store(&status[bid], cl_word(epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t top = int64_t(bid) - 1;
+        for (;;) {
+          const int64_t j = top - lane;
+          const unsigned long long sw =
+              j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : cl_word(epoch, 2, 0);
+          const uint32_t fl = static_cast<uint32_t>(sw >> 38) & 3u;
+          const bool ready = (sw >> 40) == epoch && fl != 0;
+          const uint64_t pm = __ballot(ready && fl == 2);
+          const uint64_t rm = __ballot(ready);
+          const int fp = pm ? __builtin_ctzll(pm) : kWave;  // nearest tile with its offset out
+          const uint64_t need = fp >= kWave - 1 ? ~0ull : ((2ull << fp) - 1ull);
+          if ((rm & need) != need) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;  // a tile up to there has not published yet
+          }
+          excl += wave_sum(lane <= fp ? (sw & ((1ull << 38) - 1ull)) : 0ull);
+          if (fp < kWave) break;
+          top -= kWave;
+        }
+      }
+      if (lane == 0) {
+        __hip_atomic_store(&status[bid], cl_word(epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_base = excl;
+        if (bid == nblk - 1) *nS_out = static_cast<uint32_t>(excl + agg);
+      }
+    }
+    __syncthreads();
+    if (c < nch) cbase[c] = static_cast<uint32_t>(s_base + wpre + incl - cnt);
+    if (!PER_ENTRY) {  // few entries leave: one thread per chunk
+      while (g) {
+        const int b = __builtin_ctzll(g);
+        g &= g - 1;
+        told[slist[c * kWave + b]] = 0;
+      }
+    }
+    __syncthreads();  // (s_w and s_base are reused by the next tile)
+  }
+}
+
+template <bool PER_ENTRY>
+__global__ __launch_bounds__(kBlock) void k_compact_write(const uint32_t* __restrict__ slist,
+                                                          const unsigned long long* __restrict__ mask,
+                                                          const unsigned long long* __restrict__ keep,
+                                                          const uint32_t* __restrict__ cbase,
+                                                          const uint32_t* __restrict__ nSp, uint64_t cap,
+                                                          uint16_t* __restrict__ told, uint32_t* __restrict__ out,
+                                                          uint64_t lcap) {
+  constexpr int kR = 16;
+  const int lane = lane_id();
+  const uint64_t nch = min(cap, (static_cast<uint64_t>(*nSp) + kWave - 1) / kWave);
+  const uint64_t wv = __builtin_amdgcn_readfirstlane(blockIdx.x * kWpb + threadIdx.x / kWave);
+  const uint64_t nw = uint64_t(gridDim.x) * kWpb;
+  for (uint64_t g0 = wv * kR; g0 < nch; g0 += nw * kR) {
+    uint32_t u[kR], b[kR];
+    unsigned long long kk[kR], gg[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const uint64_t c = g0 + q;
+      const bool valid = c < nch;  // (wave-uniform)
+      kk[q] = valid ? keep[c] : 0ull;
+      gg[q] = PER_ENTRY && valid ? mask[c] & ~kk[q] : 0ull;
+      b[q] = valid ? cbase[c] : 0u;
+      // (unconditional, clamped to the list's allocation: one wait for all 16, not one per store)
+      u[q] = slist[min(c * kWave + lane, lcap - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      if ((kk[q] >> lane) & 1ull) out[b[q] + __builtin_popcountll(kk[q] & ((1ull << lane) - 1ull))] = u[q];
+      if (PER_ENTRY && ((gg[q] >> lane) & 1ull)) told[u[q]] = 0;
+    }
+  }
+}
+
 void launch_compact_slist(Ctx& c) {
   ensure_slist2(c);
   const uint64_t cap = (uint64_t(c.nS_host) + kWave - 1) / kWave;  // nS_host: upper bound of the device count
@@ -3015,6 +3237,58 @@ void launch_compact_slist(Ctx& c) {
   // cleared at its live entries that were not kept (after launch_lcc_step: tpub[cur] was just written,
   // tpub[cur ^ 1] was read)
   auto* kmask = reinterpret_cast<unsigned long long*>(c.d_kmask);
+  static const bool four = std::getenv("PM_COMPACT4") && std::string(std::getenv("PM_COMPACT4")) == "1";
+  if (!four) {  // two launches (PM_COMPACT4=1: the four-launch form below, A/B)
+    const uint64_t blocks = (cap + kBlock - 1) / kBlock;
+    if (c.clstat_cap < blocks) {
+      if (c.d_clstat) (void)hipFree(c.d_clstat);
+      c.d_clstat = nullptr;
+      c.clstat_cap = std::max<uint64_t>(blocks, ((c.n + kWave - 1) / kWave + kBlock - 1) / kBlock);
+      PM_HIP_CHECK(hipMalloc(&c.d_clstat, c.clstat_cap * sizeof(unsigned long long) + 64));
+      PM_HIP_CHECK(hipMemsetAsync(c.d_clstat, 0, c.clstat_cap * sizeof(unsigned long long) + 64, c.stream));
+      c.cl_epoch = 0;
+    }
+    if (++c.cl_epoch >= (1ull << kClEpochBits)) {  // epochs wrapped: the words are cleared and counting restarts
+      PM_HIP_CHECK(hipMemsetAsync(c.d_clstat, 0, c.clstat_cap * sizeof(unsigned long long), c.stream));
+      c.cl_epoch = 1;
+    }
+    auto* st = static_cast<unsigned long long*>(c.d_clstat);
+    auto scan = c.removed_cleared ? k_compact_scan<false> : k_compact_scan<true>;
+    if (!c.cl_grid) {  // co-resident blocks of the scan (a cooperative launch checks it)
+      int per_cu = 0;
+      PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_compact_scan<true>, kBlock, 0));
+      int per_cu2 = 0;
+      PM_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_compact_scan<false>, kBlock, 0));
+      hipDeviceProp_t prop;
+      PM_HIP_CHECK(hipGetDeviceProperties(&prop, c.device));
+      c.cl_grid = static_cast<unsigned>(std::max(1, std::min({per_cu, per_cu2, 4}) * prop.multiProcessorCount));
+    }
+    const unsigned sgrid = static_cast<unsigned>(std::min<uint64_t>(blocks, c.cl_grid));
+    const uint32_t* a_slist = c.d_slist;
+    const uint32_t* a_nS = c.d_nS;
+    uint16_t* a_told = c.d_tpub[c.cur ^ 1];
+    uint32_t* a_cbase = c.d_cbase;
+    uint32_t* a_nSo = c.d_nS2;
+    uint64_t a_cap = cap, a_epoch = c.cl_epoch;
+    void* sargs[] = {&a_slist, &mask, &kmask, &a_nS, &a_cap, &a_told, &a_cbase, &a_nSo, &st, &a_epoch};
+    // (PM_LINES_NOCOOP=1, rocprofv3 runs on one context: an ordinary launch of the same co-resident grid -- the
+    // cooperative queue crashes the profiler's teardown)
+    static const bool nocoop = std::getenv("PM_LINES_NOCOOP") && std::string(std::getenv("PM_LINES_NOCOOP")) == "1";
+    if (nocoop)
+      PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(scan), dim3(sgrid), dim3(kBlock), sargs, 0, c.stream));
+    else
+      PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(scan), dim3(sgrid), dim3(kBlock), sargs, 0,
+                                              c.stream));
+    auto write = c.removed_cleared ? k_compact_write<false> : k_compact_write<true>;
+    hipLaunchKernelGGL(write, dim3(grid_for((cap + 15) / 16, kWpb, 2048)), dim3(kBlock), 0, c.stream, c.d_slist, mask,
+                       kmask, c.d_cbase, c.d_nS, cap, c.d_tpub[c.cur ^ 1], c.d_slist2, std::max<uint64_t>(c.n, 1));
+    PM_HIP_CHECK(hipGetLastError());
+    std::swap(c.d_slist, c.d_slist2);
+    std::swap(c.d_nS, c.d_nS2);
+    c.smask_valid = false;
+    c.slist_compacted = true;
+    return;
+  }
   if (c.removed_cleared)
     hipLaunchKernelGGL(k_live_keep_masks<false>, dim3(grid_for(cap, kBlock, 2048)), dim3(kBlock), 0, c.stream,
                        c.d_slist, mask, kmask, c.d_nS, cap, c.d_tpub[c.cur ^ 1], c.d_ccnt);
@@ -3710,44 +3984,30 @@ static void pseen_end(Ctx& c, const SeenSet& seen) {
   c.npseen = static_cast<uint64_t>(n);
 }
 
-TpResult run_path_line(Ctx& c, const NlcLine& line) {
-  TpResult res;
-  c.arena.reset();
-  const LineArgs la = make_line_args(c, line);
+// The tokens of initiators init[0, ninit) through the line's positions (one launch + sync per position) and the
+// terminal check; the line's seen sets are appended to `seen`.  Returns the batch's tokens and its traversed edges
+// (level-1 scans included).  Every device buffer comes from the arena: a batch that does not fit throws ArenaFull
+// before its terminal launch, with no effect outside the arena (its traversal counter is its own).
+static void path_batch(Ctx& c, const LineArgs& la, const uint32_t* init, uint64_t ninit, SeenSet& seen,
+                       uint64_t& tokens_out, uint64_t& edges_out) {
+  const uint16_t* tpub = c.d_tpub[c.cur];
   auto* d_trav = arena_alloc<unsigned long long>(c, 1);
   PM_HIP_CHECK(hipMemsetAsync(d_trav, 0, sizeof(unsigned long long), c.stream));
-  SeenSet seen{};
-  seen.count = 0;
-  const unsigned long long* p0 = nullptr;
-  const uint64_t np0 = pseen_start(c, line, &p0);  // the token-source sets this line starts from
-  if (np0) {
-    seen.keys[0] = p0;
-    seen.n[0] = np0;
-    seen.count = 1;
-  }
-  uint32_t* init = nullptr;  // token initiators
-  uint64_t ninit = 0;
-  ensure_sources(c, la, 0, line, &init, &ninit);
-  res.sources = c.nsources;
-  if (ninit == 0) {
-    pseen_end(c, seen);
-    return res;
-  }
-  const uint16_t* tpub = c.d_tpub[c.cur];
+  uint64_t tokens = 0;
   // level 1 tokens
   auto* cnt = arena_alloc<uint32_t>(c, ninit);
   auto* obase = arena_alloc<uint64_t>(c, ninit + 1);
   hipLaunchKernelGGL(k_row_alive, dim3(grid_for(ninit, kBlock, 4096)), dim3(kBlock), 0, c.stream, init, ninit, 1, 0,
                      m_off(c), c.d_malive, cnt);
   uint64_t ntok = exclusive_scan_u32_to_u64(c, cnt, obase, ninit);
-  uint64_t trav_init = ntok;  // sources scan all of M[s]
+  const uint64_t trav_init = ntok;  // sources scan all of M[s]
   auto* tu = arena_alloc<uint32_t>(c, ntok);
   auto* ts = arena_alloc<uint32_t>(c, ntok);
   auto* tp = arena_alloc<uint32_t>(c, ntok);
   hipLaunchKernelGGL(k_tp_init, dim3(grid_for(ninit, kBlock, 4096)), dim3(kBlock), 0, c.stream, init, ninit, obase,
                      m_off(c), m_col(c), c.d_mlen, tu, ts, tp);
   PM_HIP_CHECK(hipGetLastError());
-  res.tokens += ntok;
+  tokens += ntok;
   const int C = la.C;
   for (int k = 1; k <= C && ntok > 0; ++k) {
     auto* keys = arena_alloc<unsigned long long>(c, ntok);
@@ -3799,7 +4059,7 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
                        m_off(c), m_col(c), c.d_mlen, tu, ts, tp);
     PM_HIP_CHECK(hipGetLastError());
     ntok = nnext;
-    res.tokens += ntok;
+    tokens += ntok;
   }
   if (ntok > 0 && la.sv) {  // the terminal vertex is verified here
     hipLaunchKernelGGL(k_tp_terminal_sv, dim3(grid_for(ntok, kBlock, 1024)), dim3(kBlock), 0, c.stream, tu, ts, ntok,
@@ -3810,11 +4070,70 @@ TpResult run_path_line(Ctx& c, const NlcLine& line) {
                        la, tpub, m_off(c), m_col(c), c.d_mlen, c.d_perm, c.d_tsm);
     PM_HIP_CHECK(hipGetLastError());
   }
-  pseen_end(c, seen);
   unsigned long long trav = 0;
   PM_HIP_CHECK(hipMemcpyAsync(&trav, d_trav, sizeof(trav), hipMemcpyDeviceToHost, c.stream));
   PM_HIP_CHECK(hipStreamSynchronize(c.stream));
-  res.edges = trav + trav_init;
+  tokens_out = tokens;
+  edges_out = trav + trav_init;
+}
+
+// nem_1.hpp path / cycle check on the exact path.  The initiators run in batches: all of them while their tokens
+// fit the arena, otherwise halves, quarters, ... (a batch that ran out of room is discarded -- nothing outside the
+// arena was written -- and its first half runs again).  A (source, vertex) key carries its source, so batches never
+// share a dedup entry, and each source's acknowledgement comes from its own batch: the result is the unbatched one.
+// The token-source sets a later selected-vertices line reads (pseen) are kept only when the line ran in one batch;
+// a pattern with such a line whose line needs batches fails with the arena message.
+TpResult run_path_line(Ctx& c, const NlcLine& line) {
+  TpResult res;
+  c.arena.reset();
+  const LineArgs la = make_line_args(c, line);
+  SeenSet seen0{};
+  seen0.count = 0;
+  const unsigned long long* p0 = nullptr;
+  const uint64_t np0 = pseen_start(c, line, &p0);  // the token-source sets this line starts from
+  if (np0) {
+    seen0.keys[0] = p0;
+    seen0.n[0] = np0;
+    seen0.count = 1;
+  }
+  uint32_t* init = nullptr;  // token initiators
+  uint64_t ninit = 0;
+  ensure_sources(c, la, 0, line, &init, &ninit);
+  res.sources = c.nsources;
+  if (ninit == 0) {
+    pseen_end(c, seen0);
+    return res;
+  }
+  const size_t mark = c.arena.used;
+  const char* fe = std::getenv("PM_PATH_BATCH");  // PM_PATH_BATCH=<initiators> (tests): batches of at most this many
+  const uint64_t forced = fe ? std::max<uint64_t>(1, std::strtoull(fe, nullptr, 10)) : 0;
+  uint64_t batch = forced ? std::min(forced, ninit) : ninit;
+  SeenSet seen = seen0;
+  for (uint64_t i0 = 0; i0 < ninit;) {
+    const uint64_t n = std::min(batch, ninit - i0);
+    if (n < ninit && c.any_sv)
+      throw std::runtime_error("device scratch arena exhausted (a path line of a pattern with selected-vertices "
+                               "lines needs source batches)");
+    seen = seen0;
+    uint64_t tokens = 0, edges = 0;
+    try {
+      path_batch(c, la, init + i0, n, seen, tokens, edges);
+    } catch (const ArenaFull&) {
+      PM_HIP_CHECK(hipStreamSynchronize(c.stream));  // (the batch's queued kernels write the arena it reuses)
+      c.arena.used = mark;
+      if (n == 1) throw std::runtime_error("device scratch arena exhausted (one source's tokens of a path line)");
+      batch = (n + 1) / 2;
+      ++res.batch_retries;
+      continue;
+    }
+    res.tokens += tokens;
+    res.edges += edges;
+    ++res.batches;
+    i0 += n;
+    if (i0 < ninit) c.arena.used = mark;
+  }
+  if (res.batches == 1) pseen_end(c, seen);
+  else c.npseen = 0;  // (no selected-vertices line reads them: any_sv is false here)
   return res;
 }
 

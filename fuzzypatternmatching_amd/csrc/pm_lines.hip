@@ -1261,6 +1261,7 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
     c.d_gbar = dmalloc<unsigned>(words);
     PM_HIP_CHECK(hipMemsetAsync(c.d_gbar, 0, words * sizeof(unsigned), c.stream));
     c.d_lstats = reinterpret_cast<LineStats*>(c.d_gbar + kGbarWords + 64);
+    c.lines_ctl_clean = true;
   }
   if (!c.line_grid) {
     int per_cu = 0;
@@ -1280,7 +1281,9 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   auto* d_kept_ctr = reinterpret_cast<unsigned long long*>(c.d_gbar + kGbarWords + 2);
   const size_t ctl_bytes = 64 * sizeof(unsigned) + nl * sizeof(LineStats);  // control words + stats of lines < nl
   // (the fill rounded up to 64 B -- the buffer has the slack: one fill kernel instead of an aligned part and a tail)
-  PM_HIP_CHECK(hipMemsetAsync(d_done, 0, (ctl_bytes + 63) & ~size_t(63), c.stream));
+  // The search's first launch finds them cleared by the search's zero batch (queue_lines_ctl_clear)
+  if (!c.lines_ctl_clean) PM_HIP_CHECK(hipMemsetAsync(d_done, 0, (ctl_bytes + 63) & ~size_t(63), c.stream));
+  c.lines_ctl_clean = false;
   LineKernelArgs a{};
   a.offp = m_off(c);
   a.mcol = m_col(c);
@@ -1381,6 +1384,15 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   PM_HIP_CHECK(hipMemcpyAsync(pin, d_done, ctl_bytes, hipMemcpyDeviceToHost, c.stream));
   kept_out = a.kept;
   return nl;
+}
+
+// The control words and line statistics of a search's first line launch, cleared with the search's other fills
+// (one batched launch at its start instead of a fill in front of the lines).
+void queue_lines_ctl_clear(Ctx& c) {
+  if (!c.d_gbar || c.pattern.lines.empty()) return;
+  const size_t ctl_bytes = 64 * sizeof(unsigned) + c.pattern.lines.size() * sizeof(LineStats);
+  zero_later(c, c.d_gbar + kGbarWords, (ctl_bytes + 63) & ~size_t(63));
+  c.lines_ctl_clean = true;
 }
 
 void prelaunch_lines_fused(Ctx& c) {

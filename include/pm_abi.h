@@ -131,6 +131,8 @@ typedef struct pm_run_stats {
   uint64_t replica_rows;        /* rows / M entries of the replica at the hand-off                       */
   uint64_t replica_entries;
   double comm_seconds;          /* host time inside the collectives of the search                        */
+  uint64_t path_batches;        /* initiator batches of the exact-path path / cycle lines (one per line unless
+                                   a line's tokens did not fit the device scratch arena at once)          */
 } pm_run_stats;
 
 /* One shard (rank) of a sharded search: the rows of ids v % nshards == shard. */

@@ -87,6 +87,25 @@ def test_exact_count_token_passing_matches_oracle(pat, scale, p_gen, alphabet, n
     assert sg["nlcc_edges"] == so["nlcc_edges"] and sg["tds_edges"] == so["tds_edges"]
 
 
+@pytest.mark.parametrize("env", [{"PM_PATH_BATCH": "1"}, {"PM_PATH_BATCH": "7"}, {"PM_ARENA_MB": "1"}])
+def test_exact_path_lines_in_source_batches(env, tmp_path, monkeypatch):
+    """The exact path's path / cycle lines in initiator batches: forced (PM_PATH_BATCH) or because a line's tokens
+    do not fit a 1 MiB scratch arena (PM_ARENA_MB=1: the batch that ran out of room is discarded and halved) --
+    config C5's S=26 search with 64 letters ran out of the 32 GiB arena before batches existed.  Every result file
+    and counter against the oracle."""
+    monkeypatch.setenv("PM_FUSED_LINES", "0")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = pm.rmat_graph(12, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS["cycle"], tmp_path, labels, 3)
+    assert diffs == []
+    assert (sg["lcc_edges"], sg["nlcc_edges"], sg["tds_edges"], sg["walks"]) == \
+        (so["lcc_edges"], so["nlcc_edges"], so["tds_edges"], so["paths"])
+    print(f"exact lines {sg['exact_lines']}, path batches {sg['path_batches']}")
+    assert sg["path_batches"] > sg["exact_lines"]  # (batches did run: more than one per line)
+
+
 @pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards,pack",
                          [("tree", 16, 4, None, 4, 0, None), ("cycle", 14, 4, None, 1, 0, None),
                           ("cycle", 12, 4, 8, 3, 0, None), ("cycle", 15, 4, 64, 1, 0, None),
