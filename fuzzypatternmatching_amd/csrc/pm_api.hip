@@ -370,6 +370,8 @@ static void destroy_ctx(pm_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->rstream) (void)hipStreamDestroy(c->rstream);
   if (c->ev_rb) (void)hipEventDestroy(c->ev_rb);
+  if (c->ev_tz0) (void)hipEventDestroy(c->ev_tz0);
+  if (c->ev_tz) (void)hipEventDestroy(c->ev_tz);
   delete c;
 }
 
@@ -386,6 +388,7 @@ static void relayout(Ctx& c) {
   c.lcc_started = false;
   c.tpub_clean = false;  // positions changed: the next reset clears T_pub entirely
   c.long_seen.clear();   // (new labels: where long rows survive is not known)
+  c.tcode_zeroed = false;  // (new labels: more code words than the last clear covered)
   // the line grid of a search's prelaunched lines is sized by the previous search's |S| (identical for repeated
   // searches of one layout); new labels: the full grid until a search has run
   c.live_hint = ~0ull;
@@ -560,6 +563,9 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
         launch_lcc_step(c, slot, init_step && ss == 1, ss + 1 == D, init_step);
         debug_point(c, "pull superstep"); debug_watch(c, "pull superstep");
         if (init_step && (ss == 1 || ss == 2) && ss + 1 < D) launch_compact_slist(c);
+        // the codes' clear for the next search (their last reader was the first later superstep), beside the
+        // latency-bound small supersteps after the second compaction rather than beside the first
+        if (init_step && (ss == 2 || (ss == 1 && D == 2))) side_clear_codes(c);
         debug_point(c, "list compaction"); debug_watch(c, "list compaction");
       }
       // sharded: the state of S goes to the replica after superstep handoff_ss; before, the supersteps run

@@ -274,6 +274,11 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t rstream = nullptr;    // read-backs that overlap the next kernels of `stream` (created on first use)
   hipEvent_t ev_rb = nullptr;       // ... ordered after this event of `stream`
+  // one context: the 2-bit codes are cleared on rstream right after the first later superstep read them (beside the
+  // rest of the search) instead of in the next search's fills; the next superstep-0 launch waits for ev_tz
+  hipEvent_t ev_tz0 = nullptr, ev_tz = nullptr;
+  bool tcode_zeroed = false;   // the codes are clear (or being cleared) for the current layout
+  bool tcode_zpending = false; // ... by a clear on rstream that superstep 0 has not yet waited for
   uint64_t n = 0, nnz = 0;
   bool symmetric = true;
   uint32_t nranks = 1;
@@ -633,6 +638,7 @@ size_t run_lines_fused(Ctx& c, size_t pl0, bool want_walks, std::vector<FusedLin
 // next run_lines_fused(c, 0, ...) then only waits for it and reads its results.
 void prelaunch_lines_fused(Ctx& c);
 void queue_lines_ctl_clear(Ctx& c);
+void side_clear_codes(Ctx& c);
 void free_line_buffers(Ctx& c);
 TpResult run_tds_line(Ctx& c, const NlcLine& line, std::vector<uint32_t>& walks_out, uint32_t& stride);
 // The same with the kept walks handed to `sink` chunk by chunk (positions, stride C+2 each) instead of

@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     OwnerArgs oa, uint32_t* __restrict__ mcol, uint32_t* __restrict__ mlen,
     uint32_t* __restrict__ malive, Partials pp, const uint32_t* __restrict__ tcode, LabelRuns lr, uint32_t diag,
     const uint4* __restrict__ srec, uint64_t dbase, unsigned long long* __restrict__ keep_out, RecSrc rs,
-    uint32_t* __restrict__ slist_out, LongList ll, int pub_state) {
+    uint32_t* __restrict__ slist_out, LongList ll, int pub_state, int dead_state) {
   __shared__ unsigned long long s_hist[2 * kMaxRanks];
   __shared__ unsigned long long s_red[kWpb * 6];
   __shared__ uint16_t s_adj[16];
@@ -1401,9 +1401,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       const uint16_t T = keep_bits(Ts, static_cast<uint16_t>(tn), s_adj);
       if (T) {
         survivor = true;
-        tst[u] = T;
+        // dead_state: a later superstep of this call rewrites T_state and |M| alive of its survivors and derives
+        // them from T_pub and the walk until then (derive), so these stores are dead
+        if (!dead_state) {
+          tst[u] = T;
+          malive[u] = cnt;
+        }
         tnxt[u] = T;
-        malive[u] = cnt;
         // dense M: the survivor's (updated) row moves to its padded row (below, flattened over the wave)
         if (drow) {
           pb = pstart != ~0ull ? pstart : offp[u];
@@ -2525,6 +2529,11 @@ static K1Out k1_out(Ctx& c, unsigned grid) {
 
 void launch_lcc_first_kernel(Ctx& c, int variant, unsigned grid, uint64_t* d_slot) {
   if (c.ntiles == 0) return;
+  if (c.tcode_zpending) {  // (the codes' clear on rstream, side_clear_codes)
+    PM_HIP_CHECK(hipStreamWaitEvent(c.stream, c.ev_tz, 0));
+    c.tcode_zpending = false;
+  }
+  c.tcode_zeroed = false;  // (this launch writes them)
 #define PM_K1_ARGS                                                                                                    \
   dim3(grid), dim3(kBlock), 0, c.stream, c.d_ktab, c.d_ttab, c.ntiles, c.d_hseg,                                                  \
       c.d_offp, c.d_colp, c.lr, c.pa, owner_args(c), k1_out(c, grid), c.d_hscr, c.nheavy, c.nhseg,                         \
@@ -2736,8 +2745,28 @@ void queue_lcc_first_fills(Ctx& c) {
   if (c.ntiles == 0) return;
   if (c.nheavy) zero_later(c, c.d_hscr, 3 * size_t(c.nheavy) * sizeof(uint32_t));
   if (c.nheavy && c.d_hrec) zero_later(c, c.d_hrec, size_t(c.nheavy) * sizeof(uint4));
-  zero_later(c, c.d_tcode, tcode_words(c.lr) * sizeof(uint32_t));
+  if (!c.tcode_zeroed) zero_later(c, c.d_tcode, tcode_words(c.lr) * sizeof(uint32_t));
   c.k1_fills_queued = true;
+}
+
+// The codes' clear for the next search, on rstream after the first later superstep (their last reader) -- one
+// context only (a sharded search exchanges codes in collectives on its stream).
+void side_clear_codes(Ctx& c) {
+  if (c.comm || c.ntiles == 0) return;
+  if (!c.rstream) {
+    PM_HIP_CHECK(hipStreamCreateWithFlags(&c.rstream, hipStreamNonBlocking));
+    PM_HIP_CHECK(hipEventCreateWithFlags(&c.ev_rb, hipEventDisableTiming));
+  }
+  if (!c.ev_tz) {
+    PM_HIP_CHECK(hipEventCreateWithFlags(&c.ev_tz0, hipEventDisableTiming));
+    PM_HIP_CHECK(hipEventCreateWithFlags(&c.ev_tz, hipEventDisableTiming));
+  }
+  PM_HIP_CHECK(hipEventRecord(c.ev_tz0, c.stream));
+  PM_HIP_CHECK(hipStreamWaitEvent(c.rstream, c.ev_tz0, 0));
+  PM_HIP_CHECK(hipMemsetAsync(c.d_tcode, 0, tcode_words(c.lr) * sizeof(uint32_t), c.rstream));
+  PM_HIP_CHECK(hipEventRecord(c.ev_tz, c.rstream));
+  c.tcode_zeroed = true;
+  c.tcode_zpending = true;
 }
 
 void launch_lcc_first(Ctx& c, uint64_t* d_slot, hipEvent_t ev0, hipEvent_t ev1) {
@@ -2929,7 +2958,8 @@ void launch_lcc_step(Ctx& c, uint64_t* d_slot, bool first_after_ss0, bool last_o
                      c.d_tpub[c.cur], c.d_tpub[c.cur ^ 1], c.d_tst, c.pa, owner_args(c), m_col(c), c.d_mlen,
                      c.d_malive, partials(c, d_slot), first_after_ss0 ? c.d_tcode : nullptr, c.lr,
                      c.diag_step, first_after_ss0 && c.k1_records ? c.d_srec : nullptr, c.dbase,
-                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist, ll, pub_state ? 1 : 0);
+                     reinterpret_cast<unsigned long long*>(c.d_kmask), rs, c.d_slist, ll, pub_state ? 1 : 0,
+                     pub_state && !last_of_call && !c.comm ? 1 : 0);
   PM_HIP_CHECK(hipGetLastError());
   if (longs) {
     hipLaunchKernelGGL(k_lcc_step_pieces, dim3(kLongGrid), dim3(kBlock), 0, c.stream, ll, c.d_tpub[c.cur],
