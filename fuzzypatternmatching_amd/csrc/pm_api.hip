@@ -305,6 +305,16 @@ static pm_ctx* create_ctx(const CtxInput& in, const char* pattern_dir, int devic
   if (const char* e = std::getenv("PM_DIAG_STEP")) c->diag_step = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));
   if (any_sv) c->fused_lines = false;  // token-source sets across lines: the per-position path keeps them
   c->any_sv = any_sv;
+  // Grid-barrier kernels (k_lines, the list compaction's scan) need every block resident.  A cooperative launch
+  // guarantees it but costs ~28 us per launch (85 us per S=28 step for three launches, tools/gpu_coop_ab.sh); with one
+  // context on the device the grids are sized to fit and nothing else that waits on them runs beside them, so an
+  // ordinary launch is used.  Shards sharing a device (in-process shards, host-collective ranks) could hold each
+  // other's blocks out with their spinning grids: cooperative.  PM_COOP=1 / PM_LINES_NOCOOP=1 force either.
+  c->coop = in.inprocess_shards > 1 || (c->comm && c->comm->transport() != PM_TRANSPORT_RCCL);
+  // (host collectives: the ranks may share the device -- several processes on one GPU; RCCL never puts two ranks
+  // on one device.  A caller running two unrelated contexts concurrently on one GPU sets PM_COOP=1.)
+  if (const char* e = std::getenv("PM_COOP")) c->coop = std::string(e) == "1";
+  if (const char* e = std::getenv("PM_LINES_NOCOOP")) if (std::string(e) == "1") c->coop = false;
   if (const char* e = std::getenv("PM_SPLIT_LINES")) c->split_min = std::strtoull(e, nullptr, 10);
   if (const char* e = std::getenv("PM_HASH_SLOTS")) c->hash_slots = std::strtoull(e, nullptr, 10);
   if (const char* e = std::getenv("PM_HANDOFF")) c->handoff_ss = static_cast<uint32_t>(std::strtoul(e, nullptr, 10));

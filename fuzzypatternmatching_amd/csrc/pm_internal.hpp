@@ -521,6 +521,7 @@ struct Ctx {
   uint64_t live_hint = ~0ull;     // S members on this context after the last LCC call (line grid size)
   bool fused_lines = true;        // PM_FUSED_LINES=0 forces the exact-count path
   bool any_sv = false;            // some line has selected_vertices (token-source sets span lines)
+  bool coop = false;              // grid-barrier kernels by cooperative launch (several contexts on the device)
   // sharded search on the replica: an NLC line whose work census (first-position tokens of its sources on the
   // replica, sum of |M[s]|) reaches split_min runs split by owner -- every shard passes the tokens of the
   // sources it owns (hub ordinal % nshards, else id % nshards) -- and the shards then exchange the line's

@@ -3301,10 +3301,8 @@ void launch_compact_slist(Ctx& c) {
     uint32_t* a_nSo = c.d_nS2;
     uint64_t a_cap = cap, a_epoch = c.cl_epoch;
     void* sargs[] = {&a_slist, &mask, &kmask, &a_nS, &a_cap, &a_told, &a_cbase, &a_nSo, &st, &a_epoch};
-    // (PM_LINES_NOCOOP=1, rocprofv3 runs on one context: an ordinary launch of the same co-resident grid -- the
-    // cooperative queue crashes the profiler's teardown)
-    static const bool nocoop = std::getenv("PM_LINES_NOCOOP") && std::string(std::getenv("PM_LINES_NOCOOP")) == "1";
-    if (nocoop)
+    // (one context on the device: an ordinary launch of the co-resident grid, Ctx::coop)
+    if (!c.coop)
       PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(scan), dim3(sgrid), dim3(kBlock), sargs, 0, c.stream));
     else
       PM_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(scan), dim3(sgrid), dim3(kBlock), sargs, 0,

@@ -31,15 +31,13 @@
 // through ld_dev (L1-bypassing atomic loads); TDS walk regions are fresh,
 // 128-B aligned memory per position.
 //
-// Launch: hipLaunchCooperativeKernel with at most one 1024-thread block per CU
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor >= 1 checked), so the runtime
-// guarantees that every block of the grid is resident before the software grid
-// barrier below is relied on.  PM_LINES_NOCOOP=1 (profiling only) takes an
-// ordinary launch instead: the dedicated cooperative queue crashes
-// libhsa-runtime's exit-time teardown under rocprofv3 (the profile is written,
-// the process then dies with SIGSEGV in libamdhip64 -> libhsa-runtime64;
-// tools/rp_exit.py beta vs beta_nocoop); the grid is then co-resident only
-// because nothing else runs on the device during a profiled bench.
+// Launch: at most one 1024-thread block per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor >= 1 checked).
+// Round 6: an ordinary launch when the context is alone on its device (Ctx::coop false): the grid fits, and what
+// runs beside it on the context's side stream (read-back copies, a fill) finishes without waiting for it, so every
+// block becomes resident.  In-process shards sharing a device take hipLaunchCooperativeKernel, whose guarantee
+// covers their concurrent grids; it costs ~28 us per launch (tools/gpu_coop_ab.sh: 2.484 vs 2.397 ms per S=28
+// step with the compaction scans' two launches).  The cooperative queue also crashes libhsa-runtime's exit-time
+// teardown under rocprofv3 (tools/rp_exit.py beta vs beta_nocoop), hence PM_LINES_NOCOOP=1 for profiled runs.
 
 #include <hip/hip_runtime.h>
 
@@ -1361,8 +1359,7 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   // (live_hint ~0: unknown after a relayout -- the full grid; the rounding must not wrap)
   const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
       16, c.live_hint == ~0ull ? c.line_grid : std::min<uint64_t>(c.line_grid, c.live_hint / 256 + 1)));
-  static const bool nocoop = std::getenv("PM_LINES_NOCOOP") && std::string(std::getenv("PM_LINES_NOCOOP")) == "1";
-  if (nocoop)
+  if (!c.coop)  // (one context on the device, Ctx::coop)
     PM_HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(k_lines), dim3(grid), dim3(kLineBlock), args, 0,
                                  c.stream));
   else
