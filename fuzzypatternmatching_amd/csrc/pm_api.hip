@@ -979,7 +979,19 @@ static void run_beta(Ctx& c, const std::string& out_dir, uint64_t max_iterations
               batch_pl0 = pl;
               const bool regrown = c.hash_regrown;
               c.hash_regrown = false;
-              if (overflow && !regrown) exact_at = pl + n;  // (walk storage, or no room to grow the table)
+              if (overflow && !regrown) {  // (walk storage, or no room to grow the table)
+                // one context: the line's sources in parts on the fused kernel (local_split_line), else the
+                // exact path
+                FusedLineOut lo;
+                static const bool no_local = std::getenv("PM_LOCAL_SPLIT") && std::string(std::getenv("PM_LOCAL_SPLIT")) == "0";
+                if (!no_local && !c.comm && pl + n < P.lines.size() && local_split_line(c, pl + n, files, lo)) {
+                  if (phase_times)
+                    std::fprintf(stderr, "[pm] line %zu: local split in %u parts\n", pl + n, c.local_split_parts);
+                  batch.push_back(std::move(lo));
+                } else {
+                  exact_at = pl + n;
+                }
+              }
               if (!(overflow && regrown && n == 0)) break;   // the overflowed line reruns with the grown table
             }
           }

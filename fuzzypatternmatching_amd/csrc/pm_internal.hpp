@@ -509,6 +509,13 @@ struct Ctx {
   bool hash_regrown = false;      // the last fused launch overflowed the table and grew it (rerun the line fused)
   uint64_t hash_slots = 0;        // PM_HASH_SLOTS (diagnostics): size of the context's first table (0: from |S|)
   int64_t nogrow_shard = -1;      // PM_DEBUG_NOGROW_SHARD (diagnostics): that shard reports no room to grow it
+  // local split lines (one context): the part the next line launch runs (parts > 1), the parts' sources and the
+  // post-processing's cleared-source list
+  uint32_t lsplit_parts = 0, lsplit_part = 0;
+  uint32_t* d_lsrc = nullptr;
+  unsigned long long* d_ldels = nullptr;
+  uint64_t lsrc_cap = 0, ldels_cap = 0;
+  uint32_t local_split_parts = 0;  // parts of the last local split line (diagnostics)
   int64_t overflow_shard = -1;    // PM_DEBUG_OVERFLOW_SHARD (diagnostics): that shard alone reports its first
                                   // replicated path line of a search as overflowed (the agreement's test)
   bool no_row_compaction = false; // PM_ROW_COMPACTION=0 (diagnostics): rows keep their dead entries
@@ -663,6 +670,12 @@ void debug_point(Ctx& c, const char* where);
 // all of them), sums the stats, and gathers the kept walks (want_walks).  kept: this shard's kept walk slots.
 bool split_line_finish(Ctx& c, size_t pl, const LineStats& st, const uint32_t* kept_dev, bool want_walks,
                        FusedLineOut& out);
+// One context, a line whose (source, vertex) pairs outgrew the largest table: the fused kernel over the line's
+// sources in parts (the owner rule with `parts` parts), the post-processing once after every part.  false: some
+// part still overflowed at the finest split tried (the caller takes the exact path).
+bool local_split_line(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out);
+// One part of such a line (pm_lines.hip): its statistics; on overflow the table is cleared.
+LineStats run_line_part(Ctx& c, size_t pl, uint32_t parts, uint32_t part, uint32_t*& kept_dev);
 // after superstep 0 (sharded, delegates): the shares' TN / counts all-gathered and OR-ed / summed, the
 // shares' M entries sent to the controller (all-to-all), the controller verifies (slot: ss0 counters)
 void shard_hub_combine(Ctx& c, uint64_t* d_slot);

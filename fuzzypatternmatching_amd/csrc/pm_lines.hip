@@ -225,7 +225,7 @@ __device__ __forceinline__ void tp_terminal(const LineKernelArgs& a, uint32_t u,
     if (lo < e && (a.mcol[lo] & kAlive)) {
       if (!a.split) {
         a.mcol[lo] |= kFlag;
-      } else if (!(atomicOr(&a.mcol[lo], kFlag) & kFlag)) {  // newly flagged: the other replicas get it too
+      } else if (!(atomicOr(&a.mcol[lo], kFlag) & kFlag) && a.xflag) {  // newly flagged: the other replicas too
         const unsigned long long at = atomicAdd(a.nxflag, 1ull);
         if (at < a.xflag_cap) a.xflag[at] = lo;
         else atomicOr(&a.st->overflow, 1u);
@@ -1197,7 +1197,8 @@ static void regrow_hash(Ctx& c) {
   size_t free_b = 0, total_b = 0;
   PM_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
   bool room = grow <= (1ull << 31) && grow * kSlotBytes + (size_t(2) << 30) <= free_b + c.hcap * kSlotBytes;
-  if (c.comm && c.nogrow_shard == static_cast<int64_t>(c.shard)) room = false;  // (PM_DEBUG_NOGROW_SHARD, tests)
+  if (c.nogrow_shard == static_cast<int64_t>(c.shard) && (c.comm || c.nogrow_shard == 0))
+    room = false;  // (PM_DEBUG_NOGROW_SHARD, tests; 0 on one context: its local split lines)
   room = shard_agree_min(c, room ? 1 : 0) != 0;
   if (!room) return;
   ensure_hash(c, grow);
@@ -1318,7 +1319,13 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   a.so.nranks = c.comm ? c.nshards : 1;
   a.shard = c.shard;
   a.split_min = c.comm && c.nshards > 1 && c.pattern.lines.size() && !c.any_sv ? c.split_min : 0;
-  if (a.split_min) {
+  if (c.lsplit_parts > 1) {  // one context, a local split line's part (local_split_line): flags set in place
+    a.so.nranks = c.lsplit_parts;
+    a.shard = c.lsplit_part;
+    a.split_min = 1;
+    a.xflag = nullptr;
+    a.xflag_cap = 0;
+  } else if (a.split_min) {
     const uint64_t want = m_cap(c) + c.nS_host + 2;
     if (c.xsplit_cap < want) {
       if (c.d_xsplit) (void)hipFree(c.d_xsplit);
@@ -1351,6 +1358,8 @@ static size_t launch_lines(Ctx& c, size_t pl0, size_t max_lines, uint32_t*& kept
   // PM_TDS_CAP (tests): the fused walk storage is bounded too, so that a larger enumeration overflows into the
   // exact path's chunked enumeration
   if (const char* e = std::getenv("PM_TDS_CAP")) a.wcap = std::min<uint64_t>(a.wcap, std::strtoull(e, nullptr, 10));
+  // PM_FUSED_WCAP (tests): the fused walk storage alone bounded (a TDS line then overflows into a local split)
+  if (const char* e = std::getenv("PM_FUSED_WCAP")) a.wcap = std::min<uint64_t>(a.wcap, std::strtoull(e, nullptr, 10));
   a.wbuf = static_cast<uint32_t*>(c.arena.get(a.wcap * sizeof(uint32_t)));
   void* args[] = {&a};
   c.probe("lines launch");
@@ -1390,6 +1399,28 @@ void queue_lines_ctl_clear(Ctx& c) {
   const size_t ctl_bytes = 64 * sizeof(unsigned) + c.pattern.lines.size() * sizeof(LineStats);
   zero_later(c, c.d_gbar + kGbarWords, (ctl_bytes + 63) & ~size_t(63));
   c.lines_ctl_clean = true;
+}
+
+LineStats run_line_part(Ctx& c, size_t pl, uint32_t parts, uint32_t part, uint32_t*& kept_dev) {
+  if (c.comm || c.lines_prelaunched) throw std::runtime_error("internal: local split line on a sharded or busy context");
+  c.lsplit_parts = parts;
+  c.lsplit_part = part;
+  try {
+    launch_lines(c, pl, 1, kept_dev);
+  } catch (...) {
+    c.lsplit_parts = 0;
+    throw;
+  }
+  c.lsplit_parts = 0;
+  stream_wait(c.stream);
+  LineStats st;
+  std::memcpy(&st, reinterpret_cast<const char*>(c.h_pin_lines) + 64 * sizeof(unsigned) + pl * sizeof(LineStats),
+              sizeof(LineStats));
+  if (st.overflow) {  // (partial inserts are not all in the frontier list: the table is cleared)
+    PM_HIP_CHECK(hipMemsetAsync(c.d_hkey, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+    PM_HIP_CHECK(hipMemsetAsync(c.d_hval, 0xFF, c.hcap * sizeof(unsigned long long), c.stream));
+  }
+  return st;
 }
 
 void prelaunch_lines_fused(Ctx& c) {

@@ -1347,4 +1347,86 @@ bool split_line_finish(Ctx& c, size_t pl, const LineStats& st, const uint32_t* k
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// Local split lines (one context).  A path / cycle line whose (source, vertex) pairs outgrow the largest table
+// (2^31 slots, or no device room) ran on the exact per-position path at ~18 G edges/s (C5 with 64 letters at S=27,
+// DESIGN.md §4.6).  Here the fused kernel runs the line over its sources in parts instead -- the split lines'
+// owner rule with `parts` parts on one context, each part's post-processing deferred -- and the post-processing
+// runs once after every part (line_post's rule over all the line's sources, k_split_post): no part's tokens see
+// another part's cleared bits, as in the unsplit line.  Terminal effects (acknowledgements in the token-source
+// map, cycle flags on M) are set in place; a part that overflows leaves none, so the line restarts with four times
+// the parts (what the earlier parts set, the restart sets again).
+bool local_split_line(Ctx& c, size_t pl, bool want_walks, FusedLineOut& out) {
+  if (c.comm) return false;
+  // (PM_TDS_CAP, tests: a TDS line that overflows the bounded walk storage takes the exact path's chunked
+  // enumeration, which those tests exercise)
+  if (pl >= 4 && std::getenv("PM_TDS_CAP")) return false;
+  const NlcLine& line = c.pattern.lines[pl];
+  const uint32_t stride = static_cast<uint32_t>(line.cycle_length + 2);
+  const uint32_t P = c.nranks <= 1 ? 1 : c.nranks;
+  regrow(c.d_lsrc, c.lsrc_cap, std::max<size_t>(c.n, 1));
+  static const uint32_t max_parts =  // PM_LOCAL_SPLIT_MAX (tests): the finest split tried
+      std::getenv("PM_LOCAL_SPLIT_MAX") ? static_cast<uint32_t>(std::strtoul(std::getenv("PM_LOCAL_SPLIT_MAX"), nullptr, 10))
+                                        : (1u << 14);
+  for (uint32_t k = 4; k <= max_parts; k *= 4) {
+    FusedLineOut o;
+    o.stride = stride;
+    uint64_t ns = 0;
+    bool ovf = false;
+    for (uint32_t i = 0; i < k; ++i) {
+      uint32_t* kept = nullptr;
+      const LineStats st = run_line_part(c, pl, k, i, kept);
+      if (st.overflow) {
+        ovf = true;
+        break;
+      }
+      if (ns + st.nsrc > c.lsrc_cap) throw std::runtime_error("internal: local split line sources out of range");
+      if (st.nsrc)
+        PM_HIP_CHECK(hipMemcpyAsync(c.d_lsrc + ns, c.d_sources, st.nsrc * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                    c.stream));
+      ns += st.nsrc;
+      o.tr.sources += st.nsrc;
+      o.tr.edges += st.trav;
+      o.tr.tokens += st.tokens;
+      o.tr.walks += st.walks;
+      if (want_walks && pl >= 4 && st.walks) {
+        const size_t at = o.walks.size();
+        o.walks.resize(at + st.walks * stride);
+        PM_HIP_CHECK(hipMemcpy(o.walks.data() + at, kept + st.wbase[0], st.walks * stride * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost));
+      }
+    }
+    if (ovf) continue;
+    // the post-processing over every part's sources (line_post's rule)
+    regrow(c.d_ldels, c.ldels_cap, std::max<size_t>(ns, 1));
+    ensure_xcnt(c);
+    auto* d_out = reinterpret_cast<unsigned long long*>(c.d_xcnt);  // 3 + 2P <= 64 + 4 * 64 words
+    PM_HIP_CHECK(hipMemsetAsync(d_out, 0, (3 + 2 * P) * sizeof(uint64_t), c.stream));
+    OwnerArgs oa{c.d_hubs, c.d_perm, static_cast<uint32_t>(c.hubs_host.size()), c.nranks};
+    if (ns)
+      hipLaunchKernelGGL(k_split_post, dim3(xgrid(ns)), dim3(kXBlock), 0, c.stream, c.d_lsrc, uint64_t(ns), c.d_tsm,
+                         c.d_tpub[c.cur], static_cast<int>(line.indices[0]), c.d_malive, oa, c.d_ldels, d_out);
+    PM_HIP_CHECK(hipGetLastError());
+    std::vector<uint64_t> loc(3 + 2 * P);
+    PM_HIP_CHECK(hipMemcpyAsync(loc.data(), d_out, loc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    PM_HIP_CHECK(hipStreamSynchronize(c.stream));
+    o.tr.acked = loc[0];
+    o.deleted = loc[1] ? 1u : 0u;
+    o.rm_v.assign(c.nranks, 0);
+    o.rm_e.assign(c.nranks, 0);
+    for (uint32_t r = 0; r < c.nranks; ++r) {
+      o.rm_v[r] = loc[3 + r];
+      o.rm_e[r] = loc[3 + P + r];
+    }
+    o.split = true;
+    // (the line's sources stay the last part's in d_sources; the exact path and launch_post_tp are not used)
+    c.nsources = 0;
+    c.last_acked = o.tr.acked;
+    c.local_split_parts = k;
+    out = std::move(o);
+    return true;
+  }
+  return false;
+}
+
 }  // namespace pm

@@ -106,6 +106,26 @@ def test_exact_path_lines_in_source_batches(env, tmp_path, monkeypatch):
     assert sg["path_batches"] > sg["exact_lines"]  # (batches did run: more than one per line)
 
 
+@pytest.mark.parametrize("env,nranks", [({"PM_HASH_SLOTS": "16384", "PM_DEBUG_NOGROW_SHARD": "0"}, 1),
+                                         ({"PM_HASH_SLOTS": "16384", "PM_DEBUG_NOGROW_SHARD": "0"}, 3),
+                                         ({"PM_FUSED_WCAP": "1048576"}, 1)])
+def test_local_split_lines_match_oracle(env, nranks, tmp_path, monkeypatch):
+    """One context, a path / cycle line that outgrows the (source, vertex) table with no room to grow it
+    (PM_HASH_SLOTS, PM_DEBUG_NOGROW_SHARD=0), or a TDS line that outgrows the fused walk storage (PM_FUSED_WCAP):
+    the fused kernel runs the line over its sources in parts, the post-processing once after every part
+    (local_split_line), instead of the exact path.  Every result file and counter against the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = pm.rmat_graph(13, 4)
+    labels = pmtest.hash_labels(g.n, 8)
+    so, sg, diffs = _run_both(g.off, g.col, PATTERNS["cycle"], tmp_path, labels, nranks)
+    assert diffs == []
+    assert (sg["lcc_edges"], sg["nlcc_edges"], sg["tds_edges"], sg["walks"], sg["final_vertices"]) == \
+        (so["lcc_edges"], so["nlcc_edges"], so["tds_edges"], so["paths"], so["final_vertices"])
+    print(f"overflows {sg['line_overflows']}, local split lines {sg['split_lines']}, exact lines {sg['exact_lines']}")
+    assert sg["line_overflows"] > 0 and sg["split_lines"] > 0
+
+
 @pytest.mark.parametrize("pat,scale,p_gen,alphabet,nranks,shards,pack",
                          [("tree", 16, 4, None, 4, 0, None), ("cycle", 14, 4, None, 1, 0, None),
                           ("cycle", 12, 4, 8, 3, 0, None), ("cycle", 15, 4, 64, 1, 0, None),
