@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--oracle-edges", type=float, default=2e9, help="the oracle checks searches up to this many edges")
     ap.add_argument("--total-budget", type=float, default=700.0)
     ap.add_argument("--p-gen", type=int, default=8)
+    ap.add_argument("--no-capped", action="store_true", help="skip the capped rerun (timing runs)")
     ap.add_argument("--search-limit", type=float, default=400.0,
                     help="a search still running after this many seconds ends the run (one line says so)")
     args = ap.parse_args()
@@ -81,7 +82,7 @@ def main():
             a = watched(lambda: m.run_beta("", 64), args.search_limit, {"alphabet": alphabet, "scale": scale})
             ta = time.perf_counter() - t0
             b, tb = None, None
-            if ta <= args.budget / 3:
+            if ta <= args.budget / 3 and not args.no_capped:
                 os.environ["PM_TDS_CAP"] = str(args.cap)
                 t0 = time.perf_counter()
                 b = m.run_beta("", 64)
@@ -94,6 +95,7 @@ def main():
                    "path_cycle_edges": a["nlcc_edges"], "lcc_edges": a["lcc_edges"],
                    "final_vertices": a["final_vertices"], "exact_lines": a["exact_lines"],
                    "line_overflows": a["line_overflows"], "path_batches": a["path_batches"],
+                   "split_lines": a["split_lines"], "tds_chunks": a["tds_chunks"],
                    "gen_s": round(gen_s, 3)}
             if b is not None:
                 row.update({"capped_seconds": round(tb, 3), "capped_tds_chunks": b["tds_chunks"],
