@@ -113,7 +113,9 @@ typedef struct pm_run_stats {
                                    the fused kernel; see run_tds_line, PM_TDS_CAP)    */
   double nlcc_seconds;          /* NLC lines of the search: device time of the fused line launches (first
                                    block start to the last line's end) + host time of exact-path lines */
-  uint64_t split_lines;         /* sharded: NLC lines run split by owner (sources over the shards)      */
+  uint64_t split_lines;         /* NLC lines run split: sharded, by owner (sources over the shards); one
+                                   context, in local parts after the fused kernel's table or walk storage
+                                   overflowed                                            */
   uint64_t line_overflows;      /* fused NLC launches that overflowed a capacity (the line reran with a grown
                                    table, or on the exact path)                                          */
   uint64_t exact_lines;         /* NLC lines run on the exact per-position path                          */
