@@ -367,7 +367,7 @@ static void destroy_ctx(pm_ctx* c) {
                   c->d_tcode, c->d_rarea, c->d_rbase, c->d_rcnt, c->d_rofs, c->d_hrec, c->d_srec, c->d_rscan_tmp, c->d_cdesc,
                   c->d_xsend, c->d_xrecv, c->d_xent_send,
                   c->d_xent_recv, c->d_xcnt, c->d_rmoff, c->d_rmcol, c->d_xred, c->d_hubinfo, c->d_moff, c->d_hubpart, c->d_xsplit, c->d_push,
-                  c->d_lrows, c->d_lscr, c->d_clstat,
+                  c->d_lrows, c->d_lscr, c->d_clstat, c->d_lsrc, c->d_ldels,
                   };
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
