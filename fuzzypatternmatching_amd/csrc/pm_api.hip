@@ -622,9 +622,11 @@ static LccOut lcc_call(Ctx& c, bool init_step) {
   }
   PM_HIP_CHECK(hipMemcpyAsync(pin + 1 + D * W, c.d_counts, D * W * sizeof(uint64_t), hipMemcpyDeviceToHost, rs));
   if (c.prelaunch_lines && !side) prelaunch_lines_fused(c);
+  // (with the read-back on the side stream the host parses the counters while the prelaunched lines run; the
+  // lines' own read-back waits for the stream in run_lines_fused)
   if (side) stream_wait(c.rstream);
   debug_point(c, "counters + prelaunched lines");
-  stream_wait(c.stream);
+  if (!side) stream_wait(c.stream);
   c.probe("lcc synced");
   std::vector<uint64_t> host(pin + 1 + D * W, pin + 1 + 2 * D * W);
   std::vector<uint64_t> local = sharded_slots ? std::vector<uint64_t>(pin + 1, pin + 1 + D * W) : host;
